@@ -1,0 +1,25 @@
+# Builds the in-tree C-ABI library cubed_amd/libcubed_amd.so for gfx950.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CSRC := cubed_amd/csrc
+SRCS := $(CSRC)/fused.hip $(CSRC)/copy_random.hip $(CSRC)/gemm.hip
+OBJS := $(SRCS:.hip=.o)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -Iinclude
+LIB := cubed_amd/libcubed_amd.so
+
+all: $(LIB) oracle
+
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h include/cubed_amd.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(OBJS) $(LIB)
+
+.PHONY: all clean oracle

@@ -1,0 +1,146 @@
+"""ctypes binding of libcubed_amd.so (the C ABI in include/cubed_amd.h).
+
+The library is built in-tree (``make`` / ``__graft_entry__.build()``) and is
+the only compute path: if it is missing, or no GPU is visible, every call
+raises -- there is no host fallback.  torch is imported first so the HIP
+runtime torch ships (soname libamdhip64.so.7) is the one the library binds
+to; streams and device pointers therefore come straight from torch.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (
+    POINTER,
+    Structure,
+    Union,
+    c_char_p,
+    c_double,
+    c_int,
+    c_int32,
+    c_int64,
+    c_uint8,
+    c_uint16,
+    c_uint64,
+    c_void_p,
+)
+
+import numpy as np
+
+MAX_DIMS = 6
+MAX_LEAVES = 4
+MAX_FIELDS = 2
+MAX_OUTS = 2
+MAX_INSNS = 48
+MAX_EPI = 16
+MAX_CONSTS = 16
+NREGS = 6
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
+
+
+class Insn(Structure):
+    _fields_ = [("op", c_uint8), ("a", c_uint8), ("b", c_uint8), ("c", c_uint8),
+                ("t", c_uint8), ("pad", c_uint8), ("imm", c_uint16)]
+
+
+class ConstVal(Union):
+    _fields_ = [("f", c_double), ("i", c_int64)]
+
+
+class Program(Structure):
+    _fields_ = [
+        ("vtype", c_int32), ("ndim", c_int32), ("nred", c_int32), ("mode", c_int32),
+        ("nleaves", c_int32),
+        ("leaf_kind", c_uint8 * MAX_LEAVES), ("leaf_dtype", c_uint8 * MAX_LEAVES),
+        ("nfields", c_int32),
+        ("field_rop", c_uint8 * MAX_FIELDS), ("field_acc", c_uint8 * MAX_FIELDS),
+        ("field_src", c_uint8 * MAX_FIELDS), ("pad0", c_uint8 * 2),
+        ("nouts", c_int32),
+        ("out_dtype", c_uint8 * MAX_OUTS), ("out_src", c_uint8 * MAX_OUTS),
+        ("ninsns", c_int32), ("nepi", c_int32),
+        ("insns", Insn * MAX_INSNS), ("epi", Insn * MAX_EPI),
+        ("consts", ConstVal * MAX_CONSTS),
+    ]
+
+
+# numpy mirror of cubed_task_t (one row per task, uploaded as bytes)
+TASK_DTYPE = np.dtype([
+    ("extent", np.int64, (MAX_DIMS,)),
+    ("leaf_base", np.int64, (MAX_LEAVES,)),
+    ("leaf_stride", np.int64, (MAX_LEAVES, MAX_DIMS)),
+    ("out_base", np.int64, (MAX_OUTS,)),
+    ("out_stride", np.int64, (MAX_OUTS, MAX_DIMS)),
+    ("key_lo", np.uint64), ("key_hi", np.uint64),
+    ("block_offset", np.int64), ("pad", np.int64),
+])
+
+BOX_DTYPE = np.dtype([
+    ("src_base", np.int64), ("dst_base", np.int64),
+    ("extent", np.int64, (MAX_DIMS,)),
+    ("src_stride", np.int64, (MAX_DIMS,)),
+    ("dst_stride", np.int64, (MAX_DIMS,)),
+])
+
+GEMM_DTYPE = np.dtype([
+    ("a", np.int64), ("b", np.int64), ("c", np.int64),
+    ("m", np.int64), ("n", np.int64), ("k", np.int64),
+    ("lda", np.int64), ("ldb", np.int64), ("ldc", np.int64),
+    ("accumulate", np.int64),
+])
+
+COPY_ROWS, COPY_ELEMS, COPY_TILE = 0, 1, 2
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the native library; raise if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  -- bind to torch's HIP runtime first
+
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
+            "cubed_amd has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.cubed_fused_chunks.argtypes = [POINTER(Program), c_void_p, c_int64, c_int64, c_int64,
+                                     c_void_p, c_int64, c_void_p]
+    L.cubed_fused_chunks.restype = c_int
+    L.cubed_fused_workspace_bytes.argtypes = [POINTER(Program), c_int64, c_int64, c_int64]
+    L.cubed_fused_workspace_bytes.restype = c_int64
+    L.cubed_random_chunks.argtypes = [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]
+    L.cubed_random_chunks.restype = c_int
+    L.cubed_copy_boxes.argtypes = [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
+                                   c_int64, c_int64, c_void_p]
+    L.cubed_copy_boxes.restype = c_int
+    L.cubed_gemm_chunks.argtypes = [c_void_p, c_int64, c_int32, c_int64, c_int64, c_void_p]
+    L.cubed_gemm_chunks.restype = c_int
+    L.cubed_abi_version.restype = c_int
+    L.cubed_last_error.restype = c_char_p
+    L.cubed_device_count.restype = c_int
+    if L.cubed_abi_version() != 1:
+        raise NativeError("libcubed_amd.so ABI version mismatch; rebuild it")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().cubed_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed with code {rc}: {msg}")
+
+
+EXPORTED_SYMBOLS = (
+    "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_random_chunks",
+    "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
+    "cubed_device_count",
+)

@@ -1,0 +1,261 @@
+// common.h -- device helpers shared by the libcubed_amd kernels (gfx950).
+//
+// Element loads/stores for every cubed_dtype, the numpy-compatible scalar
+// semantics of the VM ops (npy_divmod, NaN-propagating maximum, ...), and
+// the Philox4x64-10 generator numpy uses for Generator.random().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <type_traits>
+#include "../../include/cubed_amd.h"
+
+#define CUBED_DEV __device__ __forceinline__
+
+namespace cubed {
+
+static constexpr int kBlock = 256;  // 4 waves of 64
+
+CUBED_DEV bool dt_is_float(int dt) {
+  return dt == CUBED_F32 || dt == CUBED_F64 || dt == CUBED_F16 || dt == CUBED_BF16;
+}
+
+__host__ __device__ inline int dt_size(int dt) {
+  switch (dt) {
+    case CUBED_BOOL: case CUBED_I8: case CUBED_U8: return 1;
+    case CUBED_I16: case CUBED_U16: case CUBED_F16: case CUBED_BF16: return 2;
+    case CUBED_I32: case CUBED_U32: case CUBED_F32: return 4;
+    default: return 8;
+  }
+}
+
+// ---------------------------------------------------------------- scalar I/O
+// Read one element of dtype dt at p and convert to V.
+template <typename V>
+CUBED_DEV V ld1(const char* p, int dt) {
+  switch (dt) {
+    case CUBED_BOOL: return (V)(*(const uint8_t*)p != 0);
+    case CUBED_I8: return (V)(*(const int8_t*)p);
+    case CUBED_I16: return (V)(*(const int16_t*)p);
+    case CUBED_I32: return (V)(*(const int32_t*)p);
+    case CUBED_I64: return (V)(*(const int64_t*)p);
+    case CUBED_U8: return (V)(*(const uint8_t*)p);
+    case CUBED_U16: return (V)(*(const uint16_t*)p);
+    case CUBED_U32: return (V)(*(const uint32_t*)p);
+    case CUBED_U64: return (V)(*(const uint64_t*)p);
+    case CUBED_F32: return (V)(*(const float*)p);
+    case CUBED_F64: return (V)(*(const double*)p);
+    case CUBED_F16: return (V)(float)(*(const __half*)p);
+    case CUBED_BF16: return (V)(float)(*(const __hip_bfloat16*)p);
+  }
+  return (V)0;
+}
+
+// float -> int conversion with defined results for NaN/out of range (x86
+// cvttsd2si behaviour: the "integer indefinite" value).
+CUBED_DEV int64_t f2i64(double x) {
+  if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return INT64_MIN;
+  return (int64_t)x;
+}
+
+template <typename V>
+CUBED_DEV int64_t to_i64(V x) {
+  if constexpr (std::is_same<V, int64_t>::value) return x;
+  else return f2i64((double)x);
+}
+
+// Convert V to dtype dt and write it at p.
+template <typename V>
+CUBED_DEV void st1(char* p, int dt, V v) {
+  switch (dt) {
+    case CUBED_BOOL: *(uint8_t*)p = (v != (V)0) ? 1 : 0; return;
+    case CUBED_I8: *(int8_t*)p = (int8_t)to_i64(v); return;
+    case CUBED_I16: *(int16_t*)p = (int16_t)to_i64(v); return;
+    case CUBED_I32: *(int32_t*)p = (int32_t)to_i64(v); return;
+    case CUBED_I64: *(int64_t*)p = to_i64(v); return;
+    case CUBED_U8: *(uint8_t*)p = (uint8_t)to_i64(v); return;
+    case CUBED_U16: *(uint16_t*)p = (uint16_t)to_i64(v); return;
+    case CUBED_U32: *(uint32_t*)p = (uint32_t)to_i64(v); return;
+    case CUBED_U64:
+      if constexpr (std::is_same<V, int64_t>::value) *(uint64_t*)p = (uint64_t)v;
+      else *(uint64_t*)p = ((double)v >= 9223372036854775808.0)
+                               ? (uint64_t)((double)v)
+                               : (uint64_t)to_i64(v);
+      return;
+    case CUBED_F32: *(float*)p = (float)v; return;
+    case CUBED_F64: *(double*)p = (double)v; return;
+    case CUBED_F16: *(__half*)p = __half((float)v); return;
+    case CUBED_BF16: *(__hip_bfloat16*)p = __hip_bfloat16((float)v); return;
+  }
+}
+
+// ---------------------------------------------------------------- vector I/O
+// VEC consecutive elements starting at element offset `off` (contiguous,
+// aligned to VEC*itemsize; the host checks alignment before choosing VEC>1).
+template <typename V, int VEC>
+CUBED_DEV void ldv(V (&o)[VEC], const char* base, int64_t off, int dt) {
+  if constexpr (VEC == 1) {
+    o[0] = ld1<V>(base + off * dt_size(dt), dt);
+  } else {
+    static_assert(VEC == 4, "VEC is 1 or 4");
+    switch (dt) {
+      case CUBED_F32: {
+        float4 v = *(const float4*)(base + off * 4);
+        o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
+      }
+      case CUBED_F64: {
+        const double2* q = (const double2*)(base + off * 8);
+        double2 a = q[0], b = q[1];
+        o[0] = (V)a.x; o[1] = (V)a.y; o[2] = (V)b.x; o[3] = (V)b.y; return;
+      }
+      case CUBED_I32: {
+        int4 v = *(const int4*)(base + off * 4);
+        o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
+      }
+      case CUBED_U32: {
+        uint4 v = *(const uint4*)(base + off * 4);
+        o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
+      }
+      case CUBED_I64: case CUBED_U64: {
+        const longlong2* q = (const longlong2*)(base + off * 8);
+        longlong2 a = q[0], b = q[1];
+        if (dt == CUBED_I64) { o[0] = (V)a.x; o[1] = (V)a.y; o[2] = (V)b.x; o[3] = (V)b.y; }
+        else { o[0] = (V)(uint64_t)a.x; o[1] = (V)(uint64_t)a.y; o[2] = (V)(uint64_t)b.x; o[3] = (V)(uint64_t)b.y; }
+        return;
+      }
+      default: {
+        const int sz = dt_size(dt);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = ld1<V>(base + (off + j) * sz, dt);
+        return;
+      }
+    }
+  }
+}
+
+template <typename V, int VEC>
+CUBED_DEV void stv(char* base, int64_t off, int dt, const V (&v)[VEC]) {
+  if constexpr (VEC == 1) {
+    st1<V>(base + off * dt_size(dt), dt, v[0]);
+  } else {
+    switch (dt) {
+      case CUBED_F32: {
+        float4 w; w.x = (float)v[0]; w.y = (float)v[1]; w.z = (float)v[2]; w.w = (float)v[3];
+        *(float4*)(base + off * 4) = w; return;
+      }
+      case CUBED_F64: {
+        double2* q = (double2*)(base + off * 8);
+        double2 a, b; a.x = (double)v[0]; a.y = (double)v[1]; b.x = (double)v[2]; b.y = (double)v[3];
+        q[0] = a; q[1] = b; return;
+      }
+      default: {
+        const int sz = dt_size(dt);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st1<V>(base + (off + j) * sz, dt, v[j]);
+        return;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- Philox
+// numpy's Philox4x64-10 (bit_generator "Philox"): counter incremented
+// before each block, so element e of a fresh stream is word e%4 of
+// philox(ctr = e/4 + 1, key); Generator.random() = (u64 >> 11) * 2^-53.
+struct P4 { uint64_t x[4]; };
+
+CUBED_DEV P4 philox4x64_10(uint64_t c0, uint64_t c1, uint64_t k0, uint64_t k1) {
+  uint64_t x0 = c0, x1 = c1, x2 = 0, x3 = 0;
+  const uint64_t M0 = 0xD2E7470EE14C6C93ull, M1 = 0xCA5A826395121157ull;
+  const uint64_t W0 = 0x9E3779B97F4A7C15ull, W1 = 0xBB67AE8584CAA73Bull;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t hi0 = __umul64hi(M0, x0), lo0 = M0 * x0;
+    const uint64_t hi1 = __umul64hi(M1, x2), lo1 = M1 * x2;
+    const uint64_t y0 = hi1 ^ x1 ^ k0;
+    const uint64_t y2 = hi0 ^ x3 ^ k1;
+    x0 = y0; x1 = lo1; x2 = y2; x3 = lo0;
+    k0 += W0; k1 += W1;
+  }
+  P4 r; r.x[0] = x0; r.x[1] = x1; r.x[2] = x2; r.x[3] = x3;
+  return r;
+}
+
+CUBED_DEV double u64_to_unit(uint64_t u) {
+  return (double)(u >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// element e of the stream (block counter e/4+1 carried into word 1)
+CUBED_DEV double philox_at(uint64_t k0, uint64_t k1, int64_t e) {
+  const uint64_t b = (uint64_t)(e >> 2) + 1ull;
+  P4 r = philox4x64_10(b, b == 0 ? 1ull : 0ull, k0, k1);
+  return u64_to_unit(r.x[e & 3]);
+}
+
+// ---------------------------------------------------------------- numpy ops
+template <typename F>
+CUBED_DEV F npy_divmod(F a, F b, F* mod_out) {
+  F mod = fmod(a, b);
+  if (!b) { *mod_out = mod; return a / b; }
+  F div = (a - mod) / b;
+  if (mod) {
+    if ((b < 0) != (mod < 0)) { mod += b; div -= (F)1; }
+  } else {
+    mod = copysign((F)0, b);
+  }
+  F floordiv;
+  if (div) {
+    floordiv = floor(div);
+    if (div - floordiv > (F)0.5) floordiv += (F)1;
+  } else {
+    floordiv = copysign((F)0, a / b);
+  }
+  *mod_out = mod;
+  return floordiv;
+}
+
+CUBED_DEV int64_t ifloordiv(int64_t a, int64_t b) {
+  if (b == 0) return 0;
+  if (b == -1 && a == INT64_MIN) return INT64_MIN;
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) q -= 1;
+  return q;
+}
+CUBED_DEV int64_t imod(int64_t a, int64_t b) {
+  if (b == 0) return 0;
+  if (b == -1) return 0;
+  int64_t r = a % b;
+  if (r != 0 && ((r < 0) != (b < 0))) r += b;
+  return r;
+}
+CUBED_DEV int64_t ipow(int64_t b, int64_t e) {
+  if (e < 0) return 0;
+  uint64_t r = 1, x = (uint64_t)b;
+  while (e) { if (e & 1) r *= x; x *= x; e >>= 1; }
+  return (int64_t)r;
+}
+
+template <typename F>
+CUBED_DEV F npy_max(F a, F b) { return (a >= b || a != a) ? a : b; }
+template <typename F>
+CUBED_DEV F npy_min(F a, F b) { return (a <= b || a != a) ? a : b; }
+
+template <typename F>
+CUBED_DEV F npy_logaddexp(F x, F y) {
+  if (x == y) return x + (F)0.69314718055994530942;
+  F t = x - y;
+  if (t > 0) return x + log1p(exp(-t));
+  if (t <= 0) return y + log1p(exp(t));
+  return t;
+}
+template <typename F>
+CUBED_DEV F npy_logaddexp2(F x, F y) {
+  if (x == y) return x + (F)1;
+  F t = x - y;
+  if (t > 0) return x + log1p(exp2(-t)) * (F)1.44269504088896340736;
+  if (t <= 0) return y + log1p(exp2(t)) * (F)1.44269504088896340736;
+  return t;
+}
+
+}  // namespace cubed

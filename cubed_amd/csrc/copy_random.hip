@@ -1,0 +1,221 @@
+// copy_random.hip -- Philox chunk generation and strided box copies.
+//
+// cubed_random_chunks replaces the per-task numpy call of cubed/random.py:31-36
+// (Generator(Philox(key=root_seed + block_offset)).random(shape)): one thread
+// produces one Philox4x64-10 block = 4 consecutive doubles, stored as two
+// 16-byte stores, so a chunk is written at HBM rate.
+//
+// cubed_copy_boxes replaces copy_read_to_write (primitive/rechunk.py:187-192)
+// and the map_direct region reads (core/ops.py:481,784): every (source chunk
+// x target chunk) intersection is one box.  Rechunk never permutes axes, so
+// both views of a box are C-ordered sub-boxes of the same index space and the
+// innermost run is contiguous on both sides: the row kernel moves each row
+// with 16/8/4/1-byte lanes.  Boxes whose innermost runs differ (after the host
+// drops unit dims -- e.g. (1,N) chunks -> (N,1) chunks) go through a 64x64
+// LDS tile so both the read and the write stay coalesced.
+#include "common.h"
+#include <stdio.h>
+
+namespace cubed {
+extern thread_local char g_err[512];
+}
+using namespace cubed;
+
+static int fail(const char* m) { snprintf(g_err, sizeof(g_err), "%s", m); return CUBED_E_ARG; }
+
+__global__ __launch_bounds__(kBlock) void k_random(const int64_t* __restrict__ outs,
+                                                   const int64_t* __restrict__ counts,
+                                                   const uint64_t* __restrict__ keys,
+                                                   int64_t ntasks, int64_t bpt) {
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t t = g / bpt, b = g % bpt;
+  if (t >= ntasks) return;
+  double* __restrict__ out = (double*)outs[t];
+  const int64_t n = counts[t];
+  const uint64_t k0 = keys[2 * t], k1 = keys[2 * t + 1];
+  const int64_t nblk = (n + 3) >> 2;
+  for (int64_t i = b * kBlock + threadIdx.x; i < nblk; i += bpt * kBlock) {
+    P4 r = philox4x64_10((uint64_t)i + 1ull, 0ull, k0, k1);
+    const int64_t e = i << 2;
+    if (e + 4 <= n && (((uintptr_t)(out + e)) & 15) == 0) {
+      double2 a, c;
+      a.x = u64_to_unit(r.x[0]); a.y = u64_to_unit(r.x[1]);
+      c.x = u64_to_unit(r.x[2]); c.y = u64_to_unit(r.x[3]);
+      ((double2*)(out + e))[0] = a;
+      ((double2*)(out + e))[1] = c;
+    } else {
+      for (int j = 0; j < 4 && e + j < n; ++j) out[e + j] = u64_to_unit(r.x[j]);
+    }
+  }
+}
+
+extern "C" int cubed_random_chunks(const int64_t* d_out_ptrs, const int64_t* d_counts,
+                                   const uint64_t* d_keys, int64_t ntasks, int64_t max_count,
+                                   void* stream) {
+  if (ntasks == 0) return 0;
+  if (!d_out_ptrs || !d_counts || !d_keys || max_count < 0) return fail("cubed_random_chunks: bad argument");
+  const int64_t nblk = (max_count + 3) / 4;
+  int64_t bpt = (nblk + kBlock - 1) / kBlock;
+  if (bpt < 1) bpt = 1;
+  if (bpt > 16384) bpt = 16384;
+  const int64_t blocks = ntasks * bpt;
+  dim3 grid(blocks <= 0x7fffffff ? (unsigned)blocks : 0x7fffffffu,
+            blocks <= 0x7fffffff ? 1u : (unsigned)((blocks + 0x7ffffffe) / 0x7fffffff));
+  hipLaunchKernelGGL(k_random, grid, dim3(kBlock), 0, (hipStream_t)stream, d_out_ptrs, d_counts,
+                     d_keys, ntasks, bpt);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+// ------------------------------------------------------------------ box copies
+// Row kernel: rows = product of all but the innermost extent; one wave copies
+// one row at a time in W-byte lanes.  Template W = lane width in bytes.
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restrict__ boxes,
+                                                      int64_t nboxes, int32_t ndim, int32_t isz,
+                                                      int64_t bpb, int64_t rows_per_block) {
+  using T = typename std::conditional<W == 16, uint4,
+            typename std::conditional<W == 8, uint2,
+            typename std::conditional<W == 4, uint32_t, uint8_t>::type>::type>::type;
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t bi = g / bpb, blk = g % bpb;
+  if (bi >= nboxes) return;
+  const cubed_box_t* __restrict__ B = boxes + bi;
+  const int nd = ndim;
+  int64_t nrows = 1;
+  for (int d = 0; d < nd - 1; ++d) nrows *= B->extent[d];
+  const int64_t rowbytes = B->extent[nd - 1] * isz;
+  const int64_t nw = rowbytes / W;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row_begin = blk * rows_per_block;
+  int64_t row_end = row_begin + rows_per_block;
+  if (row_end > nrows) row_end = nrows;
+  for (int64_t row = row_begin + wave; row < row_end; row += kBlock / 64) {
+    // decompose the row index over dims [0, nd-1)
+    int64_t so = 0, dof = 0, rr = row;
+    for (int d = nd - 2; d >= 0; --d) {
+      const int64_t e = B->extent[d];
+      const int64_t c = rr % e;
+      rr /= e;
+      so += c * B->src_stride[d];
+      dof += c * B->dst_stride[d];
+    }
+    const T* __restrict__ src = (const T*)((const char*)B->src_base + so * isz);
+    T* __restrict__ dst = (T*)((char*)B->dst_base + dof * isz);
+    for (int64_t i = lane; i < nw; i += 64) dst[i] = src[i];
+  }
+}
+
+// 64x64 LDS tile transpose-copy for 2-d boxes whose contiguous axes differ:
+// src contiguous along dim 1, dst contiguous along dim 0 (host arranges).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_copy_tile(const cubed_box_t* __restrict__ boxes,
+                                                      int64_t nboxes, int64_t tiles_per_box) {
+  __shared__ T tile[64][65];
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t bi = g / tiles_per_box, ti = g % tiles_per_box;
+  if (bi >= nboxes) return;
+  const cubed_box_t* __restrict__ B = boxes + bi;
+  const int64_t e0 = B->extent[0], e1 = B->extent[1];
+  const int64_t nt1 = (e1 + 63) / 64;
+  const int64_t t0 = (ti / nt1) * 64, t1 = (ti % nt1) * 64;
+  if (t0 >= e0) return;
+  const T* __restrict__ src = (const T*)B->src_base;
+  T* __restrict__ dst = (T*)B->dst_base;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t i0 = t0 + r, i1 = t1 + tx;
+    if (i0 < e0 && i1 < e1) tile[r][tx] = src[i0 * B->src_stride[0] + i1 * B->src_stride[1]];
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t i1 = t1 + r, i0 = t0 + tx;
+    if (i0 < e0 && i1 < e1) dst[i0 * B->dst_stride[0] + i1 * B->dst_stride[1]] = tile[tx][r];
+  }
+}
+
+// Generic element gather (any strides, any itemsize); used for odd layouts.
+__global__ __launch_bounds__(kBlock) void k_copy_elems(const cubed_box_t* __restrict__ boxes,
+                                                       int64_t nboxes, int32_t ndim, int32_t isz,
+                                                       int64_t bpb) {
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t bi = g / bpb, blk = g % bpb;
+  if (bi >= nboxes) return;
+  const cubed_box_t* __restrict__ B = boxes + bi;
+  int64_t n = 1;
+  for (int d = 0; d < ndim; ++d) n *= B->extent[d];
+  for (int64_t i = blk * kBlock + threadIdx.x; i < n; i += bpb * kBlock) {
+    int64_t so = 0, dof = 0, rr = i;
+    for (int d = ndim - 1; d >= 0; --d) {
+      const int64_t e = B->extent[d];
+      const int64_t c = rr % e;
+      rr /= e;
+      so += c * B->src_stride[d];
+      dof += c * B->dst_stride[d];
+    }
+    const char* s = (const char*)B->src_base + so * isz;
+    char* dd = (char*)B->dst_base + dof * isz;
+    switch (isz) {
+      case 1: *(uint8_t*)dd = *(const uint8_t*)s; break;
+      case 2: *(uint16_t*)dd = *(const uint16_t*)s; break;
+      case 4: *(uint32_t*)dd = *(const uint32_t*)s; break;
+      case 8: *(uint64_t*)dd = *(const uint64_t*)s; break;
+      default: for (int j = 0; j < isz; ++j) dd[j] = s[j]; break;
+    }
+  }
+}
+
+static dim3 grid2(int64_t blocks) {
+  if (blocks <= 0x7fffffff) return dim3((unsigned)blocks, 1, 1);
+  return dim3(0x7fffffffu, (unsigned)((blocks + 0x7ffffffe) / 0x7fffffff), 1);
+}
+
+extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int32_t ndim,
+                                int32_t itemsize, int32_t path, int32_t lane_bytes,
+                                int64_t work, int64_t row_bytes, void* stream) {
+  if (nboxes == 0) return 0;
+  if (!d_boxes) return fail("cubed_copy_boxes: null box table");
+  hipStream_t st = (hipStream_t)stream;
+  const int isz = itemsize;
+  const int width = lane_bytes;
+  const int nd = ndim;
+  const int64_t max_box_elems = work;
+  if (nd < 1 || nd > CUBED_MAX_DIMS || isz < 1) return fail("cubed_copy_boxes: bad ndim/itemsize");
+  if (path == 2) {
+    if (nd != 2) return fail("cubed_copy_boxes: tile path needs 2-d boxes");
+    // max_box_elems carries tiles per box for this path
+    const int64_t tpb = max_box_elems;
+    const dim3 grid = grid2(nboxes * tpb);
+    switch (isz) {
+      case 1: hipLaunchKernelGGL(k_copy_tile<uint8_t>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, tpb); break;
+      case 2: hipLaunchKernelGGL(k_copy_tile<uint16_t>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, tpb); break;
+      case 4: hipLaunchKernelGGL(k_copy_tile<uint32_t>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, tpb); break;
+      case 8: hipLaunchKernelGGL(k_copy_tile<uint64_t>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, tpb); break;
+      default: return fail("cubed_copy_boxes: tile path itemsize");
+    }
+  } else if (path == 1) {
+    int64_t bpb = (max_box_elems + kBlock * 4 - 1) / (kBlock * 4);
+    if (bpb < 1) bpb = 1;
+    if (bpb > 65536) bpb = 65536;
+    hipLaunchKernelGGL(k_copy_elems, grid2(nboxes * bpb), dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb);
+  } else {
+    // rows: max_box_elems = max rows per box; aim ~64 KB per workgroup
+    const int64_t max_rows = max_box_elems;
+    int64_t rpb = row_bytes > 0 ? (65536 + row_bytes - 1) / row_bytes : 16;
+    if (rpb < 4) rpb = 4;
+    if (rpb > 4096) rpb = 4096;
+    int64_t bpb = (max_rows + rpb - 1) / rpb;
+    if (bpb < 1) bpb = 1;
+    const dim3 grid = grid2(nboxes * bpb);
+    switch (width) {
+      case 16: hipLaunchKernelGGL(k_copy_rows<16>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb, rpb); break;
+      case 8: hipLaunchKernelGGL(k_copy_rows<8>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb, rpb); break;
+      case 4: hipLaunchKernelGGL(k_copy_rows<4>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb, rpb); break;
+      default: hipLaunchKernelGGL(k_copy_rows<1>, grid, dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb, rpb); break;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}

@@ -1,0 +1,327 @@
+// vm.h -- the per-element program interpreter of the fused chunk kernels.
+//
+// A fused Cubed pipeline (elementwise chain -> optional reduction ->
+// epilogue, see DESIGN.md "Fused chunk programs") is lowered on the host to
+// a short two-address program over CUBED_NREGS registers, each holding VEC
+// consecutive elements of the thread.  The opcode and the register operands
+// are wave-uniform (they live in the kernel-argument segment and are read
+// with scalar loads), so every switch below is a scalar branch: the VALU
+// only executes the selected op on the VEC elements.  Register operands are
+// resolved by fetch/op/write-back switches so the register file stays in
+// VGPRs (a runtime-indexed array would be demoted to scratch).
+#pragma once
+#include "common.h"
+
+namespace cubed {
+
+template <typename V, int VEC>
+struct Regs {
+  V r0[VEC], r1[VEC], r2[VEC], r3[VEC], r4[VEC], r5[VEC];
+};
+
+#define CUBED_REG_SWITCH(idx, STMT) \
+  switch (idx) {                    \
+    case 0: { auto& R = regs.r0; STMT; } break; \
+    case 1: { auto& R = regs.r1; STMT; } break; \
+    case 2: { auto& R = regs.r2; STMT; } break; \
+    case 3: { auto& R = regs.r3; STMT; } break; \
+    case 4: { auto& R = regs.r4; STMT; } break; \
+    default: { auto& R = regs.r5; STMT; } break; \
+  }
+
+template <typename V, int VEC>
+CUBED_DEV void fetch(const Regs<V, VEC>& regs, int idx, V (&X)[VEC]) {
+  CUBED_REG_SWITCH(idx, { _Pragma("unroll") for (int j = 0; j < VEC; ++j) X[j] = R[j]; })
+}
+template <typename V, int VEC>
+CUBED_DEV void put(Regs<V, VEC>& regs, int idx, const V (&X)[VEC]) {
+  CUBED_REG_SWITCH(idx, { _Pragma("unroll") for (int j = 0; j < VEC; ++j) R[j] = X[j]; })
+}
+template <typename V, int VEC>
+CUBED_DEV V* reg_ptr(Regs<V, VEC>& regs, int idx) {
+  switch (idx) {
+    case 0: return regs.r0; case 1: return regs.r1; case 2: return regs.r2;
+    case 3: return regs.r3; case 4: return regs.r4; default: return regs.r5;
+  }
+}
+
+#define CUBED_EACH(EXPR) _Pragma("unroll") for (int j = 0; j < VEC; ++j) { const V x = X[j]; (void)x; X[j] = (EXPR); }
+#define CUBED_EACH2(EXPR) _Pragma("unroll") for (int j = 0; j < VEC; ++j) { const V x = X[j]; const V y = Y[j]; X[j] = (EXPR); }
+
+// CAST: round the value (of source dtype s) to dtype t, keeping it in V.
+template <typename V>
+CUBED_DEV V cast_val(V x, int t, int s) {
+  if (t == CUBED_BOOL) return (x != (V)0) ? (V)1 : (V)0;
+  if constexpr (std::is_same<V, int64_t>::value) {
+    switch (t) {
+      case CUBED_I8: return (int64_t)(int8_t)x;
+      case CUBED_I16: return (int64_t)(int16_t)x;
+      case CUBED_I32: return (int64_t)(int32_t)x;
+      case CUBED_U8: return (int64_t)(uint8_t)x;
+      case CUBED_U16: return (int64_t)(uint16_t)x;
+      case CUBED_U32: return (int64_t)(uint32_t)x;
+      default: return x;
+    }
+  } else {
+    switch (t) {
+      case CUBED_F32: return (V)(float)x;
+      case CUBED_F64: return x;
+      case CUBED_F16: return (V)(float)__half((float)x);
+      case CUBED_BF16: return (V)(float)__hip_bfloat16((float)x);
+      default: break;
+    }
+    // integer targets: float sources truncate toward zero, then wrap
+    int64_t i = dt_is_float(s) ? f2i64((double)x) : f2i64((double)x);
+    switch (t) {
+      case CUBED_I8: return (V)(int8_t)i;
+      case CUBED_I16: return (V)(int16_t)i;
+      case CUBED_I32: return (V)(int32_t)i;
+      case CUBED_U8: return (V)(uint8_t)i;
+      case CUBED_U16: return (V)(uint16_t)i;
+      case CUBED_U32: return (V)(uint32_t)i;
+      case CUBED_U64: return (V)(uint64_t)i;
+      default: return (V)i;
+    }
+  }
+}
+
+template <typename V, int VEC>
+CUBED_DEV void unary(int op, V (&X)[VEC]) {
+  if constexpr (std::is_same<V, int64_t>::value) {
+    switch (op) {
+      case CUBED_OP_NEG: CUBED_EACH((int64_t)(0ull - (uint64_t)x)); break;
+      case CUBED_OP_ABS: CUBED_EACH(x < 0 ? (int64_t)(0ull - (uint64_t)x) : x); break;
+      case CUBED_OP_LNOT: CUBED_EACH((int64_t)(x == 0)); break;
+      case CUBED_OP_BNOT: CUBED_EACH(~x); break;
+      case CUBED_OP_SIGN: CUBED_EACH((int64_t)((x > 0) - (x < 0))); break;
+      case CUBED_OP_SQUARE: CUBED_EACH((int64_t)((uint64_t)x * (uint64_t)x)); break;
+      case CUBED_OP_ISNAN: case CUBED_OP_ISINF: case CUBED_OP_SIGNBIT: CUBED_EACH((int64_t)(op == CUBED_OP_SIGNBIT ? (x < 0) : 0)); break;
+      case CUBED_OP_ISFINITE: CUBED_EACH((int64_t)1); break;
+      default: break;  // floor/ceil/trunc/rint/positive of ints are identities
+    }
+  } else {
+    switch (op) {
+      case CUBED_OP_NEG: CUBED_EACH(-x); break;
+      case CUBED_OP_ABS: CUBED_EACH(fabs(x)); break;
+      case CUBED_OP_SQRT: CUBED_EACH(sqrt(x)); break;
+      case CUBED_OP_EXP: CUBED_EACH(exp(x)); break;
+      case CUBED_OP_LOG: CUBED_EACH(log(x)); break;
+      case CUBED_OP_SIN: CUBED_EACH(sin(x)); break;
+      case CUBED_OP_COS: CUBED_EACH(cos(x)); break;
+      case CUBED_OP_TAN: CUBED_EACH(tan(x)); break;
+      case CUBED_OP_TANH: CUBED_EACH(tanh(x)); break;
+      case CUBED_OP_FLOOR: CUBED_EACH(floor(x)); break;
+      case CUBED_OP_CEIL: CUBED_EACH(ceil(x)); break;
+      case CUBED_OP_TRUNC: CUBED_EACH(trunc(x)); break;
+      case CUBED_OP_RINT: CUBED_EACH(rint(x)); break;
+      case CUBED_OP_ISNAN: CUBED_EACH((V)(x != x)); break;
+      case CUBED_OP_ISINF: CUBED_EACH((V)(isinf(x) ? 1 : 0)); break;
+      case CUBED_OP_ISFINITE: CUBED_EACH((V)(isfinite(x) ? 1 : 0)); break;
+      case CUBED_OP_LNOT: CUBED_EACH((V)(x == (V)0)); break;
+      case CUBED_OP_BNOT: CUBED_EACH((V)(~f2i64((double)x))); break;
+      case CUBED_OP_SIGN: CUBED_EACH(x > 0 ? (V)1 : (x < 0 ? (V)-1 : (x == 0 ? (V)0 : x))); break;
+      case CUBED_OP_SQUARE: CUBED_EACH(x * x); break;
+      case CUBED_OP_RECIP: CUBED_EACH((V)1 / x); break;
+      case CUBED_OP_LOG1P: CUBED_EACH(log1p(x)); break;
+      case CUBED_OP_EXPM1: CUBED_EACH(expm1(x)); break;
+      case CUBED_OP_LOG2: CUBED_EACH(log2(x)); break;
+      case CUBED_OP_LOG10: CUBED_EACH(log10(x)); break;
+      case CUBED_OP_SINH: CUBED_EACH(sinh(x)); break;
+      case CUBED_OP_COSH: CUBED_EACH(cosh(x)); break;
+      case CUBED_OP_ASIN: CUBED_EACH(asin(x)); break;
+      case CUBED_OP_ACOS: CUBED_EACH(acos(x)); break;
+      case CUBED_OP_ATAN: CUBED_EACH(atan(x)); break;
+      case CUBED_OP_ASINH: CUBED_EACH(asinh(x)); break;
+      case CUBED_OP_ACOSH: CUBED_EACH(acosh(x)); break;
+      case CUBED_OP_ATANH: CUBED_EACH(atanh(x)); break;
+      case CUBED_OP_EXP2: CUBED_EACH(exp2(x)); break;
+      case CUBED_OP_SIGNBIT: CUBED_EACH((V)(signbit(x) ? 1 : 0)); break;
+      default: break;
+    }
+  }
+}
+
+template <typename V, int VEC>
+CUBED_DEV void binary(int op, V (&X)[VEC], const V (&Y)[VEC]) {
+  if constexpr (std::is_same<V, int64_t>::value) {
+    switch (op) {
+      case CUBED_OP_ADD: CUBED_EACH2((int64_t)((uint64_t)x + (uint64_t)y)); break;
+      case CUBED_OP_SUB: CUBED_EACH2((int64_t)((uint64_t)x - (uint64_t)y)); break;
+      case CUBED_OP_MUL: CUBED_EACH2((int64_t)((uint64_t)x * (uint64_t)y)); break;
+      case CUBED_OP_FLOORDIV: CUBED_EACH2(ifloordiv(x, y)); break;
+      case CUBED_OP_MOD: CUBED_EACH2(imod(x, y)); break;
+      case CUBED_OP_POW: CUBED_EACH2(ipow(x, y)); break;
+      case CUBED_OP_MAX: case CUBED_OP_FMAX: CUBED_EACH2(x > y ? x : y); break;
+      case CUBED_OP_MIN: case CUBED_OP_FMIN: CUBED_EACH2(x < y ? x : y); break;
+      case CUBED_OP_EQ: CUBED_EACH2((int64_t)(x == y)); break;
+      case CUBED_OP_NE: CUBED_EACH2((int64_t)(x != y)); break;
+      case CUBED_OP_LT: CUBED_EACH2((int64_t)(x < y)); break;
+      case CUBED_OP_LE: CUBED_EACH2((int64_t)(x <= y)); break;
+      case CUBED_OP_GT: CUBED_EACH2((int64_t)(x > y)); break;
+      case CUBED_OP_GE: CUBED_EACH2((int64_t)(x >= y)); break;
+      case CUBED_OP_LAND: CUBED_EACH2((int64_t)((x != 0) && (y != 0))); break;
+      case CUBED_OP_LOR: CUBED_EACH2((int64_t)((x != 0) || (y != 0))); break;
+      case CUBED_OP_LXOR: CUBED_EACH2((int64_t)((x != 0) != (y != 0))); break;
+      case CUBED_OP_BAND: CUBED_EACH2(x & y); break;
+      case CUBED_OP_BOR: CUBED_EACH2(x | y); break;
+      case CUBED_OP_BXOR: CUBED_EACH2(x ^ y); break;
+      case CUBED_OP_SHL: CUBED_EACH2((y < 0 || y > 63) ? (int64_t)0 : (int64_t)((uint64_t)x << y)); break;
+      case CUBED_OP_SHR: CUBED_EACH2((y < 0 || y > 63) ? (x < 0 ? (int64_t)-1 : (int64_t)0) : (x >> y)); break;
+      default: break;
+    }
+  } else {
+    switch (op) {
+      case CUBED_OP_ADD: CUBED_EACH2(x + y); break;
+      case CUBED_OP_SUB: CUBED_EACH2(x - y); break;
+      case CUBED_OP_MUL: CUBED_EACH2(x * y); break;
+      case CUBED_OP_DIV: CUBED_EACH2(x / y); break;
+      case CUBED_OP_FLOORDIV: { _Pragma("unroll") for (int j = 0; j < VEC; ++j) { V m; X[j] = npy_divmod<V>(X[j], Y[j], &m); } } break;
+      case CUBED_OP_MOD: { _Pragma("unroll") for (int j = 0; j < VEC; ++j) { V m; npy_divmod<V>(X[j], Y[j], &m); X[j] = m; } } break;
+      case CUBED_OP_POW: CUBED_EACH2(pow(x, y)); break;
+      case CUBED_OP_MAX: CUBED_EACH2(npy_max<V>(x, y)); break;
+      case CUBED_OP_MIN: CUBED_EACH2(npy_min<V>(x, y)); break;
+      case CUBED_OP_FMAX: CUBED_EACH2(fmax(x, y)); break;
+      case CUBED_OP_FMIN: CUBED_EACH2(fmin(x, y)); break;
+      case CUBED_OP_EQ: CUBED_EACH2((V)(x == y)); break;
+      case CUBED_OP_NE: CUBED_EACH2((V)(x != y)); break;
+      case CUBED_OP_LT: CUBED_EACH2((V)(x < y)); break;
+      case CUBED_OP_LE: CUBED_EACH2((V)(x <= y)); break;
+      case CUBED_OP_GT: CUBED_EACH2((V)(x > y)); break;
+      case CUBED_OP_GE: CUBED_EACH2((V)(x >= y)); break;
+      case CUBED_OP_LAND: CUBED_EACH2((V)((x != 0) && (y != 0))); break;
+      case CUBED_OP_LOR: CUBED_EACH2((V)((x != 0) || (y != 0))); break;
+      case CUBED_OP_LXOR: CUBED_EACH2((V)((x != 0) != (y != 0))); break;
+      case CUBED_OP_BAND: CUBED_EACH2((V)(f2i64((double)x) & f2i64((double)y))); break;
+      case CUBED_OP_BOR: CUBED_EACH2((V)(f2i64((double)x) | f2i64((double)y))); break;
+      case CUBED_OP_BXOR: CUBED_EACH2((V)(f2i64((double)x) ^ f2i64((double)y))); break;
+      case CUBED_OP_ATAN2: CUBED_EACH2(atan2(x, y)); break;
+      case CUBED_OP_HYPOT: CUBED_EACH2(hypot(x, y)); break;
+      case CUBED_OP_COPYSIGN: CUBED_EACH2(copysign(x, y)); break;
+      case CUBED_OP_LOGADDEXP: CUBED_EACH2(npy_logaddexp<V>(x, y)); break;
+      case CUBED_OP_LOGADDEXP2: CUBED_EACH2(npy_logaddexp2<V>(x, y)); break;
+      default: break;
+    }
+  }
+}
+
+// Run `n` instructions.  consts: the program's constant pool.
+template <typename V, int VEC>
+CUBED_DEV void run_vm(Regs<V, VEC>& regs, const cubed_insn_t* ins, int n,
+                      const cubed_program_t& P) {
+  for (int i = 0; i < n; ++i) {
+    const cubed_insn_t I = ins[i];
+    const int op = I.op;
+    V X[VEC];
+    if (op == CUBED_OP_CONST) {
+      V c;
+      if constexpr (std::is_same<V, int64_t>::value) c = P.consts[I.imm].i;
+      else c = (V)P.consts[I.imm].f;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) X[j] = c;
+      put(regs, I.a, X);
+      continue;
+    }
+    if (op == CUBED_OP_MOV) {
+      fetch(regs, I.b, X);
+      put(regs, I.a, X);
+      continue;
+    }
+    fetch(regs, I.a, X);
+    if (op == CUBED_OP_CAST) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) X[j] = cast_val<V>(X[j], I.t, I.imm);
+    } else if (op == CUBED_OP_WHERE) {
+      V Y[VEC], C[VEC];
+      fetch(regs, I.b, Y);
+      fetch(regs, I.c, C);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) X[j] = (C[j] != (V)0) ? X[j] : Y[j];
+    } else if (op >= CUBED_OP_ADD) {
+      V Y[VEC];
+      fetch(regs, I.b, Y);
+      binary<V, VEC>(op, X, Y);
+    } else {
+      unary<V, VEC>(op, X);
+    }
+    put(regs, I.a, X);
+  }
+}
+
+// ---------------------------------------------------------------- reductions
+union Acc { double f; int64_t i; };
+
+CUBED_DEV Acc acc_init(int rop, int acc_i) {
+  Acc a;
+  switch (rop) {
+    case CUBED_R_MAX: if (acc_i) a.i = INT64_MIN; else a.f = -__builtin_inf(); break;
+    case CUBED_R_MIN: if (acc_i) a.i = INT64_MAX; else a.f = __builtin_inf(); break;
+    case CUBED_R_NANMAX: case CUBED_R_NANMIN: if (acc_i) a.i = (rop == CUBED_R_NANMAX ? INT64_MIN : INT64_MAX); else a.f = __builtin_nan(""); break;
+    case CUBED_R_PROD: case CUBED_R_NANPROD: if (acc_i) a.i = 1; else a.f = 1.0; break;
+    case CUBED_R_ALL: a.i = 1; break;
+    case CUBED_R_SUM: case CUBED_R_NANSUM: if (acc_i) a.i = 0; else a.f = -0.0; break;
+    default: a.i = 0; break;
+  }
+  return a;
+}
+
+// fold one value into an accumulator
+template <typename V>
+CUBED_DEV void acc_add(Acc& a, int rop, int acc_i, V v) {
+  switch (rop) {
+    case CUBED_R_SUM:
+      if (acc_i) a.i = (int64_t)((uint64_t)a.i + (uint64_t)to_i64(v)); else a.f += (double)v; break;
+    case CUBED_R_NANSUM:
+      if (acc_i) a.i += to_i64(v); else if (v == v) a.f += (double)v; break;
+    case CUBED_R_COUNT: a.i += 1; break;
+    case CUBED_R_COUNT_NONNAN: a.i += (v == v) ? 1 : 0; break;
+    case CUBED_R_MAX:
+      if (acc_i) { int64_t w = to_i64(v); a.i = w > a.i ? w : a.i; } else a.f = npy_max<double>(a.f, (double)v); break;
+    case CUBED_R_MIN:
+      if (acc_i) { int64_t w = to_i64(v); a.i = w < a.i ? w : a.i; } else a.f = npy_min<double>(a.f, (double)v); break;
+    case CUBED_R_NANMAX:
+      if (acc_i) { int64_t w = to_i64(v); a.i = w > a.i ? w : a.i; }
+      else if (v == v) a.f = (a.f != a.f || (double)v > a.f) ? (double)v : a.f; break;
+    case CUBED_R_NANMIN:
+      if (acc_i) { int64_t w = to_i64(v); a.i = w < a.i ? w : a.i; }
+      else if (v == v) a.f = (a.f != a.f || (double)v < a.f) ? (double)v : a.f; break;
+    case CUBED_R_PROD:
+      if (acc_i) a.i = (int64_t)((uint64_t)a.i * (uint64_t)to_i64(v)); else a.f *= (double)v; break;
+    case CUBED_R_NANPROD:
+      if (acc_i) a.i = (int64_t)((uint64_t)a.i * (uint64_t)to_i64(v)); else if (v == v) a.f *= (double)v; break;
+    case CUBED_R_ANY: a.i |= (v != (V)0) ? 1 : 0; break;
+    case CUBED_R_ALL: a.i &= (v != (V)0) ? 1 : 0; break;
+    default: break;
+  }
+}
+
+// combine two partial accumulators
+CUBED_DEV Acc acc_combine(Acc a, Acc b, int rop, int acc_i) {
+  Acc r;
+  switch (rop) {
+    case CUBED_R_SUM: case CUBED_R_NANSUM:
+      if (acc_i) r.i = (int64_t)((uint64_t)a.i + (uint64_t)b.i); else r.f = a.f + b.f; break;
+    case CUBED_R_COUNT: case CUBED_R_COUNT_NONNAN: r.i = a.i + b.i; break;
+    case CUBED_R_MAX: if (acc_i) r.i = a.i > b.i ? a.i : b.i; else r.f = npy_max<double>(a.f, b.f); break;
+    case CUBED_R_MIN: if (acc_i) r.i = a.i < b.i ? a.i : b.i; else r.f = npy_min<double>(a.f, b.f); break;
+    case CUBED_R_NANMAX:
+      if (acc_i) r.i = a.i > b.i ? a.i : b.i;
+      else r.f = (a.f != a.f) ? b.f : ((b.f != b.f) ? a.f : (a.f > b.f ? a.f : b.f)); break;
+    case CUBED_R_NANMIN:
+      if (acc_i) r.i = a.i < b.i ? a.i : b.i;
+      else r.f = (a.f != a.f) ? b.f : ((b.f != b.f) ? a.f : (a.f < b.f ? a.f : b.f)); break;
+    case CUBED_R_PROD: case CUBED_R_NANPROD:
+      if (acc_i) r.i = (int64_t)((uint64_t)a.i * (uint64_t)b.i); else r.f = a.f * b.f; break;
+    case CUBED_R_ANY: r.i = a.i | b.i; break;
+    case CUBED_R_ALL: r.i = a.i & b.i; break;
+    default: r = a; break;
+  }
+  return r;
+}
+
+CUBED_DEV Acc shfl_xor_acc(Acc a, int m) {
+  Acc r;
+  r.i = __shfl_xor((long long)a.i, m, 64);
+  return r;
+}
+
+}  // namespace cubed

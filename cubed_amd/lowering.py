@@ -1,0 +1,1119 @@
+"""Lowering of fused Cubed pipelines to libcubed_amd launches.
+
+For one pipeline (an op node of the finalized DAG) this builds, once, every
+device-side table its launch needs:
+
+* ``FusedLaunch``: an IR ``ExprProgram`` -> ``cubed_program_t`` (register
+  allocation of the two-address VM, constant pool, CAST insertion for the
+  program's value type) + a ``cubed_task_t`` row per output chunk (the leaf
+  and output views of that chunk, in a canonical dim order shared by all
+  tasks: unit dims dropped, reduced dims ordered for kernel A or B, adjacent
+  dims coalesced when every view allows it).
+* ``CopyLaunch``: rechunk / merge_chunks / index / pure copies as a table of
+  (source chunk x target chunk) boxes.
+* ``GemmLaunch``: matmul / tensordot chunk products.
+
+The task key resolution follows apply_blockwise (primitive/blockwise.py:61-84):
+``block_function(('out',) + out_key)`` gives each argument's chunk key(s).
+A leaf reads either one chunk (a strided sub-box), a run of unit-extent
+chunks (partials being merged: one stride = the slot stride), or -- for any
+other multi-chunk read -- a per-task gather into a contiguous scratch buffer.
+"""
+
+from __future__ import annotations
+
+import itertools
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as nat
+from . import ir
+from .storage import (
+    DeviceArray,
+    HostArray,
+    VirtualEmptyArray,
+    VirtualFullArray,
+    VirtualInMemoryArray,
+    VirtualOffsetsArray,
+    c_strides,
+)
+from .utils import block_id_to_offset, flatten_keys
+
+
+class LoweringError(RuntimeError):
+    pass
+
+
+LEAF_ARRAY, LEAF_PHILOX, LEAF_OFFSET, LEAF_IOTA = 0, 1, 2, 3
+V_F32, V_F64, V_I64 = 0, 1, 2
+
+
+# ------------------------------------------------------------------ views
+
+
+@dataclass
+class ArrView:
+    """A strided view: base byte address + per-dim (extent, stride) in
+    elements of ``dtype`` (array-dim order)."""
+    base: int
+    extent: List[int]
+    stride: List[int]
+    dtype: np.dtype
+
+
+def chunk_view(arr: DeviceArray, coords, field=None) -> ArrView:
+    ext = list(arr.chunk_extent(coords))
+    return ArrView(arr.chunk_addr(coords, field), ext, list(c_strides(ext)),
+                   arr.field_dtype(field))
+
+
+def merged_view(arr: DeviceArray, keys, field=None) -> Optional[ArrView]:
+    """One view over a set of chunk keys, or None if irregular.  Regular =
+    along each dim either one chunk, or a contiguous run of chunks that all
+    have extent 1 there (reduction partials): that dim's stride is the slot
+    stride, since every chunk occupies one fixed-size slot."""
+    coords = [k[1:] for k in keys]
+    nd = arr.ndim
+    if nd == 0:
+        return chunk_view(arr, coords[0], field)
+    per_dim = [sorted({c[d] for c in coords}) for d in range(nd)]
+    if math.prod(len(p) for p in per_dim) != len(set(map(tuple, coords))):
+        return None
+    if arr.world != 1:
+        return None
+    first = tuple(p[0] for p in per_dim)
+    base_ext = arr.chunk_extent(first)
+    ext, stride = [], []
+    inner = c_strides(base_ext)
+    slot_elems = arr.slot_stride_elems(field)
+    for d in range(nd):
+        p = per_dim[d]
+        if len(p) == 1:
+            ext.append(base_ext[d])
+            stride.append(inner[d])
+            continue
+        if p != list(range(p[0], p[-1] + 1)):
+            return None
+        if any(arr.chunk_extent(tuple(p2 if dd == d else first[dd] for dd in range(nd)))[d] != 1
+               for p2 in p):
+            return None
+        slot_step = math.prod(arr.numblocks[d + 1:])
+        ext.append(len(p))
+        stride.append(slot_step * slot_elems)
+    return ArrView(arr.chunk_addr(first, field), ext, stride, arr.field_dtype(field))
+
+
+def region_pieces(arr, region) -> List[Tuple[Tuple[int, ...], List[Tuple[int, int, int]], List[int]]]:
+    """Split a region (per dim: slice with step, int, or list) of ``arr``
+    into per-chunk pieces: (chunk coords, per-dim (in-chunk start, count,
+    step), per-region-dim output offsets).  Int dims produce no region dim."""
+    per_dim = []
+    for d, s in enumerate(region):
+        n = arr.shape[d]
+        pieces = []  # (chunk, local_start, count, step, out_offset)
+        if isinstance(s, slice):
+            start, stop, step = s.start or 0, s.stop if s.stop is not None else n, s.step or 1
+            i, out = start, 0
+            while i < stop:
+                c = arr.chunk_of(d, i)
+                cst = arr.chunk_start(tuple(c if dd == d else 0 for dd in range(arr.ndim)))[d]
+                cend = cst + arr.chunk_extent(tuple(c if dd == d else 0 for dd in range(arr.ndim)))[d]
+                last = min(stop, cend)
+                cnt = (last - i + step - 1) // step
+                pieces.append((c, i - cst, cnt, step, out))
+                out += cnt
+                i += cnt * step
+            per_dim.append((pieces, True))
+        elif isinstance(s, list):
+            for j, v in enumerate(s):
+                c = arr.chunk_of(d, v)
+                cst = arr.chunk_start(tuple(c if dd == d else 0 for dd in range(arr.ndim)))[d]
+                pieces.append((c, v - cst, 1, 1, j))
+            per_dim.append((pieces, True))
+        else:
+            v = int(s)
+            c = arr.chunk_of(d, v)
+            cst = arr.chunk_start(tuple(c if dd == d else 0 for dd in range(arr.ndim)))[d]
+            per_dim.append(([(c, v - cst, 1, 1, 0)], False))
+    out = []
+    for combo in itertools.product(*[p for p, _ in per_dim]):
+        coords = tuple(c for c, *_ in combo)
+        local = [(ls, cnt, st) for _, ls, cnt, st, _ in combo]
+        offs = [o for (_, _, _, _, o), (_, keep) in zip(combo, per_dim) if keep]
+        out.append((coords, local, offs))
+    return out
+
+
+def region_view(arr: DeviceArray, region, field=None) -> Optional[ArrView]:
+    """View of a region that lies inside one chunk (None otherwise)."""
+    pieces = region_pieces(arr, region)
+    if len(pieces) != 1:
+        return None
+    coords, local, _ = pieces[0]
+    ext = arr.chunk_extent(coords)
+    inner = c_strides(ext)
+    off = sum(ls * inner[d] for d, (ls, _, _) in enumerate(local))
+    isz = arr.field_dtype(field).itemsize
+    # int-indexed dims keep extent 1 (the leaf maps them to no space dim)
+    return ArrView(arr.chunk_addr(coords, field) + off * isz,
+                   [cnt for (_, cnt, _) in local],
+                   [inner[d] * st for d, (_, _, st) in enumerate(local)],
+                   arr.field_dtype(field))
+
+
+# ------------------------------------------------------------------ box copies
+
+
+@dataclass
+class Box:
+    src: int
+    dst: int
+    extent: List[int]
+    sstride: List[int]
+    dstride: List[int]
+
+
+def boxes_for_region(src: DeviceArray, region, dst_base: int, dst_strides: Sequence[int],
+                     field=None) -> List[Box]:
+    """Boxes copying ``src[region]`` into a destination view whose dims are
+    the region's non-int dims."""
+    isz = src.field_dtype(field).itemsize
+    out = []
+    for coords, local, offs in region_pieces(src, region):
+        ext = src.chunk_extent(coords)
+        inner = c_strides(ext)
+        base = src.chunk_addr(coords, field) + sum(ls * inner[d] for d, (ls, _, _) in enumerate(local)) * isz
+        keep = [d for d, s in enumerate(region) if not _is_int_sel(s)]
+        extent = [local[d][1] for d in keep]
+        sstr = [inner[d] * local[d][2] for d in keep]
+        dbase = dst_base + sum(o * s for o, s in zip(offs, dst_strides)) * isz
+        out.append(Box(base, dbase, extent, sstr, list(dst_strides)))
+    return out
+
+
+def _is_int_sel(s):
+    return not isinstance(s, (slice, list))
+
+
+def canonical_boxes(boxes: List[Box]):
+    """Drop unit dims, coalesce dims contiguous on both sides; returns
+    (ndim, boxes) with every box padded to the same ndim."""
+    canon = []
+    for b in boxes:
+        dims = [(e, s, d) for e, s, d in zip(b.extent, b.sstride, b.dstride) if e != 1]
+        if not dims:
+            dims = [(1, 1, 1)]
+        merged = [list(dims[0])]
+        for e, s, d in dims[1:]:
+            pe, ps, pd = merged[-1]
+            if ps == s * e and pd == d * e:
+                merged[-1] = [pe * e, s, d]
+            else:
+                merged.append([e, s, d])
+        canon.append((b, merged))
+    nd = max(len(m) for _, m in canon)
+    if nd > nat.MAX_DIMS:
+        raise LoweringError(f"box with {nd} dims after coalescing")
+    out = []
+    for b, m in canon:
+        m = [[1, 0, 0]] * (nd - len(m)) + m
+        out.append(Box(b.src, b.dst, [x[0] for x in m], [x[1] for x in m], [x[2] for x in m]))
+    return nd, out
+
+
+class CopyLaunch:
+    """One cubed_copy_boxes launch."""
+
+    def __init__(self, boxes: List[Box], itemsize: int, device):
+        import torch
+
+        self.nboxes = len(boxes)
+        if not boxes:
+            return
+        nd, boxes = canonical_boxes(boxes)
+        self.ndim = nd
+        self.itemsize = itemsize
+        inner_contig = all(b.sstride[-1] == 1 and b.dstride[-1] == 1 for b in boxes)
+        if inner_contig:
+            self.path = nat.COPY_ROWS
+            lane = 16
+            for b in boxes:
+                vals = [b.extent[-1] * itemsize, b.src, b.dst]
+                vals += [s * itemsize for s in b.sstride[:-1]] + [s * itemsize for s in b.dstride[:-1]]
+                while lane > 1 and any(v % lane for v in vals):
+                    lane //= 2
+            self.lane = lane
+            self.work = max(math.prod(b.extent[:-1]) for b in boxes)
+            self.row_bytes = max(b.extent[-1] for b in boxes) * itemsize
+        elif nd == 2 and all(b.sstride[1] == 1 and b.dstride[0] == 1 for b in boxes):
+            self.path = nat.COPY_TILE
+            self.lane = 0
+            self.work = max(((b.extent[0] + 63) // 64) * ((b.extent[1] + 63) // 64) for b in boxes)
+            self.row_bytes = 0
+        else:
+            self.path = nat.COPY_ELEMS
+            self.lane = 0
+            self.work = max(math.prod(b.extent) for b in boxes)
+            self.row_bytes = 0
+        rows = np.zeros(len(boxes), dtype=nat.BOX_DTYPE)
+        for i, b in enumerate(boxes):
+            rows[i]["src_base"] = b.src
+            rows[i]["dst_base"] = b.dst
+            ext = [1] * nat.MAX_DIMS
+            ss = [0] * nat.MAX_DIMS
+            ds = [0] * nat.MAX_DIMS
+            ext[:nd] = b.extent
+            ss[:nd] = b.sstride
+            ds[:nd] = b.dstride
+            rows[i]["extent"] = ext
+            rows[i]["src_stride"] = ss
+            rows[i]["dst_stride"] = ds
+        self.table = torch.from_numpy(rows.view(np.uint8).copy()).to(device)
+
+    def run(self, stream):
+        if self.nboxes == 0:
+            return
+        L = nat.lib()
+        nat.check(L.cubed_copy_boxes(self.table.data_ptr(), self.nboxes, self.ndim, self.itemsize,
+                                     self.path, self.lane, self.work, self.row_bytes, stream),
+                  "cubed_copy_boxes")
+
+
+# ------------------------------------------------------------------ programs
+
+
+class Codegen:
+    """IR expressions -> two-address VM code for cubed_program_t."""
+
+    def __init__(self, vtype: int, leaf_regs: Dict[int, int], nregs: int = nat.NREGS):
+        self.vtype = vtype
+        self.leaf_regs = leaf_regs       # id(leaf expr) -> register
+        self.reserved = set(leaf_regs.values())
+        self.free = [r for r in range(nregs) if r not in self.reserved]
+        self.code: List[Tuple] = []
+        self.consts: List[Tuple[str, Any]] = []
+        self.cache: Dict[int, int] = {}
+        self.uses: Dict[int, int] = {}
+
+    # -- helpers --------------------------------------------------------------
+    def count_uses(self, exprs):
+        seen = set()
+
+        def walk(e):
+            self.uses[id(e)] = self.uses.get(id(e), 0) + 1
+            if id(e) in seen:
+                return
+            seen.add(id(e))
+            for c in e.children():
+                walk(c)
+
+        for e in exprs:
+            walk(e)
+
+    def alloc(self) -> int:
+        if not self.free:
+            raise LoweringError("fused expression needs more than 6 VM registers")
+        return self.free.pop(0)
+
+    def release(self, r):
+        if r not in self.reserved and r not in self.free and r not in self.cache.values():
+            self.free.append(r)
+            self.free.sort()
+
+    def const_index(self, value, dtype) -> int:
+        dtype = np.dtype(dtype)
+        if self.vtype == V_I64:
+            item = ("i", int(np.array(value).astype(np.int64)))
+        else:
+            v = float(np.array(value).astype(np.float64))
+            if self.vtype == V_F32 or dtype == np.float32:
+                v = float(np.float32(v)) if dtype.kind == "f" and dtype.itemsize <= 4 else v
+            item = ("f", v)
+        for i, c in enumerate(self.consts):
+            if c == item and not (isinstance(c[1], float) and math.isnan(c[1])):
+                return i
+        if len(self.consts) >= nat.MAX_CONSTS:
+            raise LoweringError("too many constants in one fused program")
+        self.consts.append(item)
+        return len(self.consts) - 1
+
+    def natural(self, dtype) -> bool:
+        """True if a value of ``dtype`` needs no re-rounding in V."""
+        dtype = np.dtype(dtype)
+        if dtype.kind == "b":
+            return True
+        if self.vtype == V_F64:
+            return dtype in (np.dtype(np.float64), np.dtype(np.int64), np.dtype(np.uint64))
+        if self.vtype == V_F32:
+            return dtype == np.dtype(np.float32)
+        return dtype in (np.dtype(np.int64), np.dtype(np.uint64))
+
+    # -- expression codegen --------------------------------------------------
+    def gen(self, e) -> Tuple[int, bool]:
+        """Return (register, owned) holding the value of ``e``."""
+        key = id(e)
+        if key in self.leaf_regs:
+            return self.leaf_regs[key], False
+        if key in self.cache:
+            return self.cache[key], False
+        if isinstance(e, ir.Const):
+            r = self.alloc()
+            self.code.append((ir_op("CONST"), r, 0, 0, 0, self.const_index(e.value, e.dtype)))
+            return self._finish(e, r)
+        if isinstance(e, (ir.Arg, ir.Region, ir.Philox, ir.BlockOffset, ir.Iota, ir.Field)):
+            raise LoweringError(f"leaf {e} has no register")
+        if isinstance(e, ir.Cast):
+            r = self.owned(*self.gen(e.x))
+            self.code.append((ir_op("CAST"), r, 0, 0, ir.dtype_code(e.dtype), ir.dtype_code(e.x.dtype)))
+            return self._finish(e, r, rounded=True)
+        if isinstance(e, ir.Unary):
+            r = self.owned(*self.gen(e.x))
+            self.code.append((ir.UNARY_OPS[e.op], r, 0, 0, 0, 0))
+            return self._finish(e, r)
+        if isinstance(e, ir.Binary):
+            ra, oa = self.gen(e.a)
+            ra = self.owned(ra, oa)
+            rb, ob = self.gen(e.b)
+            self.code.append((ir.BINARY_OPS[e.op], ra, rb, 0, 0, 0))
+            if ob:
+                self.release(rb)
+            return self._finish(e, ra)
+        if isinstance(e, ir.Where):
+            ra = self.owned(*self.gen(e.a))
+            rb, ob = self.gen(e.b)
+            rc, oc = self.gen(e.c)
+            self.code.append((ir_op("WHERE"), ra, rb, rc, 0, 0))
+            if ob:
+                self.release(rb)
+            if oc:
+                self.release(rc)
+            return self._finish(e, ra)
+        raise LoweringError(f"cannot generate code for {type(e).__name__}")
+
+    def owned(self, r, owned) -> int:
+        if owned:
+            return r
+        t = self.alloc()
+        self.code.append((ir_op("MOV"), t, r, 0, 0, 0))
+        return t
+
+    def _finish(self, e, r, rounded=False):
+        if not rounded and not self.natural(e.dtype):
+            self.code.append((ir_op("CAST"), r, 0, 0, ir.dtype_code(e.dtype), ir.dtype_code(e.dtype)))
+        if self.uses.get(id(e), 0) > 1:
+            self.cache[id(e)] = r
+            return r, False
+        return r, True
+
+
+_OPCODES = {"NOP": 0, "CONST": 1, "MOV": 2, "CAST": 3, "WHERE": 4}
+
+
+def ir_op(name):
+    return _OPCODES[name]
+
+
+def choose_vtype(exprs, leaves) -> int:
+    """Register value type: I64 for all-integer programs, F32 when every
+    computed node is f32-or-narrower (f64 leaves only feed casts to f32), else
+    F64 (f32 nodes are then re-rounded by CAST, exact for + - * / sqrt)."""
+    nodes = []
+    seen = set()
+    parents: Dict[int, List[Any]] = {}
+
+    def walk(e, parent=None):
+        if parent is not None:
+            parents.setdefault(id(e), []).append(parent)
+        if id(e) in seen:
+            return
+        seen.add(id(e))
+        nodes.append(e)
+        for c in e.children():
+            walk(c, e)
+
+    for e in exprs:
+        walk(e)
+    dts = [np.dtype(n.dtype) for n in nodes if not isinstance(n, ir.Field)]
+    if all(d.kind in "biu" for d in dts):
+        return V_I64
+    small = {np.dtype(np.float32), np.dtype(np.float16), np.dtype(np.bool_), np.dtype(np.int8),
+             np.dtype(np.uint8), np.dtype(np.int16), np.dtype(np.uint16)}
+    ok = True
+    for n in nodes:
+        d = np.dtype(n.dtype)
+        if isinstance(n, (ir.Arg, ir.Region, ir.Philox)):
+            if d not in small and not all(isinstance(p, ir.Cast) and np.dtype(p.dtype) in small
+                                          for p in parents.get(id(n), [None])):
+                ok = False
+        elif isinstance(n, (ir.BlockOffset, ir.Iota)):
+            ok = False
+        elif isinstance(n, ir.Const):
+            continue
+        elif d not in small:
+            ok = False
+    return V_F32 if ok else V_F64
+
+
+def collect_leaves(exprs) -> List[Any]:
+    out, seen = [], set()
+    for e in exprs:
+        for leaf in ir.leaves(e):
+            if isinstance(leaf, (ir.Const, ir.Field)):
+                continue
+            k = _leaf_key(leaf)
+            if k not in seen:
+                seen.add(k)
+                out.append(leaf)
+    return out
+
+
+def _leaf_key(leaf):
+    if isinstance(leaf, ir.Arg):
+        return ("arg", leaf.index, leaf.field, leaf.axes)
+    if isinstance(leaf, ir.Region):
+        return ("region", leaf.array_name, leaf.field, leaf.axes, id(leaf.region), leaf.block_arg)
+    if isinstance(leaf, ir.Philox):
+        return ("philox", leaf.root_seed, leaf.block_arg, leaf.axes)
+    if isinstance(leaf, ir.BlockOffset):
+        return ("offset", leaf.block_arg)
+    if isinstance(leaf, ir.Iota):
+        return ("iota", leaf.dim, leaf.arg, leaf.axes)
+    return ("other", id(leaf))
+
+
+def dedupe_leaves(exprs):
+    """Rewrite expressions so equal leaves are one object (one register)."""
+    canon: Dict[Any, Any] = {}
+
+    def fn(leaf):
+        if isinstance(leaf, (ir.Const, ir.Field)):
+            return None
+        k = _leaf_key(leaf)
+        if k in canon:
+            return canon[k]
+        canon[k] = leaf
+        return leaf
+
+    memo: Dict[int, Any] = {}
+    return [ir.transform(e, fn, memo) for e in exprs]
+
+
+def program_exprs(p: ir.ExprProgram):
+    outs = [e for _, e in p.output_items()]
+    fields = [f.expr for f in p.reduce.fields] if p.reduce else []
+    return outs, fields
+
+
+def is_pure_copy(p: ir.ExprProgram, out_dtype) -> bool:
+    """A program that only moves one leaf's values (merge/index/squeeze)."""
+    if p.reduce is not None or p.structured:
+        return False
+    e = p.outputs
+    return isinstance(e, (ir.Arg, ir.Region)) and np.dtype(e.dtype) == np.dtype(out_dtype)
+
+
+# ------------------------------------------------------------------ fused launch
+
+
+class FusedLaunch:
+    """One cubed_fused_chunks launch (+ optional scratch gathers)."""
+
+    def __init__(self, prog_struct, table, ntasks, max_kept, max_red, ws_bytes, gathers, device):
+        import torch
+
+        self.prog = prog_struct
+        self.table = table
+        self.ntasks = ntasks
+        self.max_kept = max_kept
+        self.max_red = max_red
+        self.gathers = gathers
+        self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device) if ws_bytes else None
+        self.ws_bytes = ws_bytes
+
+    def run(self, stream):
+        for g in self.gathers:
+            g.run(stream)
+        L = nat.lib()
+        nat.check(L.cubed_fused_chunks(self.prog, self.table.data_ptr(), self.ntasks, self.max_kept,
+                                       self.max_red, self.ws.data_ptr() if self.ws is not None else None,
+                                       self.ws_bytes, stream), "cubed_fused_chunks")
+
+
+class GemmLaunch:
+    def __init__(self, rows, dtype_code, max_m, max_n, device, zero_targets=()):
+        import torch
+
+        self.n = len(rows)
+        self.dtype_code = dtype_code
+        self.max_m, self.max_n = max_m, max_n
+        self.table = torch.from_numpy(rows.view(np.uint8).copy()).to(device) if self.n else None
+
+    def run(self, stream):
+        if not self.n:
+            return
+        L = nat.lib()
+        nat.check(L.cubed_gemm_chunks(self.table.data_ptr(), self.n, self.dtype_code, self.max_m,
+                                      self.max_n, stream), "cubed_gemm_chunks")
+
+
+class Lowerer:
+    """Lowers pipelines for one executor context (device, scratch buffers,
+    uploaded small arrays)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    # -- argument resolution ---------------------------------------------------
+    def resolve_target(self, name, reads_map):
+        proxy = reads_map.get(name)
+        if proxy is None:
+            raise LoweringError(f"array {name} is not an input of this pipeline")
+        return self.ctx.device_source(proxy.array)
+
+    def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys):
+        """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline."""
+        outs, field_exprs = program_exprs(program)
+        exprs = dedupe_leaves(outs + field_exprs)
+        outs2, fields2 = exprs[:len(outs)], exprs[len(outs):]
+        out_items = [(n, e) for (n, _), e in zip(program.output_items(), outs2)]
+        rfields = []
+        if program.reduce is not None:
+            rfields = [ir.ReduceField(f.name, f.rop, e, f.dtype) for f, e in zip(program.reduce.fields, fields2)]
+
+        # pure copies go through the box-copy kernel
+        if program.reduce is None and not program.structured and is_pure_copy(program, target.dtype):
+            return self.lower_copy_program(program, spec, target, task_keys)
+
+        pre_exprs = [e for _, e in out_items] if program.reduce is None else [f.expr for f in rfields]
+        leaves = collect_leaves(pre_exprs)
+        if len(leaves) > nat.MAX_LEAVES:
+            raise LoweringError(f"fused program reads {len(leaves)} inputs (max {nat.MAX_LEAVES})")
+
+        # constant-fold leaves that resolve to constants (virtual full / scalars)
+        sample_args = spec.block_function(("out",) + tuple(task_keys[0]))
+        const_leaves = {}
+        for leaf in leaves:
+            c = self.constant_value(leaf, sample_args, spec.reads_map)
+            if c is not None:
+                const_leaves[_leaf_key(leaf)] = c
+        if const_leaves:
+            def fold(leaf):
+                k = _leaf_key(leaf) if not isinstance(leaf, (ir.Const, ir.Field)) else None
+                if k in const_leaves:
+                    return ir.Const(const_leaves[k], leaf.dtype)
+                return None
+            memo = {}
+            pre_exprs = [ir.transform(e, fold, memo) for e in pre_exprs]
+            if program.reduce is None:
+                out_items = [(n, e) for (n, _), e in zip(out_items, pre_exprs)]
+            else:
+                rfields = [ir.ReduceField(f.name, f.rop, e, f.dtype) for f, e in zip(rfields, pre_exprs)]
+            leaves = collect_leaves(pre_exprs)
+
+        vtype = choose_vtype(pre_exprs, leaves)
+        leaf_regs = {}
+        by_key = {_leaf_key(l): i for i, l in enumerate(leaves)}
+
+        def index_leaves(e):
+            for lf in ir.leaves(e):
+                if not isinstance(lf, (ir.Const, ir.Field)):
+                    leaf_regs[id(lf)] = by_key[_leaf_key(lf)]
+
+        for e in pre_exprs:
+            index_leaves(e)
+        cg = Codegen(vtype, leaf_regs)
+        cg.count_uses(pre_exprs)
+
+        P = nat.Program()
+        P.vtype = vtype
+        P.nleaves = len(leaves)
+        structured_out = program.structured
+        out_fields = [n for n, _ in out_items]
+        if program.reduce is None:
+            srcs = []
+            for _, e in out_items:
+                r, _ = cg.gen(e)
+                srcs.append(r)
+            P.nfields = 0
+            P.nepi = -1
+            out_regs = srcs
+        else:
+            P.nfields = len(rfields)
+            if P.nfields > nat.MAX_FIELDS:
+                raise LoweringError("too many reduced fields")
+            for i, f in enumerate(rfields):
+                r, _ = cg.gen(f.expr)
+                P.field_src[i] = r
+                P.field_rop[i] = ir.ROPS[f.rop]
+                P.field_acc[i] = 1 if ir.acc_is_int(f.rop, f.dtype) else 0
+            # epilogue over fields (double registers 0..nf-1)
+            fidx = {f.name: i for i, f in enumerate(rfields)}
+            direct = all(isinstance(e, ir.Field) for _, e in out_items)
+            if direct:
+                P.nepi = -1
+                out_regs = [fidx[e.name] for _, e in out_items]
+            else:
+                ecg = Codegen(V_F64, {}, nregs=nat.NREGS)
+                ecg.reserved = set(range(len(rfields)))
+                ecg.free = [r for r in range(nat.NREGS) if r not in ecg.reserved]
+                ecg.consts = cg.consts  # shared pool
+                ecg.count_uses([e for _, e in out_items])
+                field_regs = {}
+
+                def bind_fields(e):
+                    for lf in ir.leaves(e):
+                        if isinstance(lf, ir.Field):
+                            field_regs[id(lf)] = fidx[lf.name]
+
+                for _, e in out_items:
+                    bind_fields(e)
+                ecg.leaf_regs = field_regs
+                out_regs = []
+                for _, e in out_items:
+                    r, _ = ecg.gen(e)
+                    out_regs.append(r)
+                if len(ecg.code) > nat.MAX_EPI:
+                    raise LoweringError("epilogue too long")
+                P.nepi = len(ecg.code)
+                for i, ins in enumerate(ecg.code):
+                    _set_insn(P.epi[i], ins)
+                cg.consts = ecg.consts
+        if len(cg.code) > nat.MAX_INSNS:
+            raise LoweringError("fused program too long")
+        P.ninsns = len(cg.code)
+        for i, ins in enumerate(cg.code):
+            _set_insn(P.insns[i], ins)
+        for i, (kind, v) in enumerate(cg.consts):
+            if kind == "i":
+                P.consts[i].i = v
+            else:
+                P.consts[i].f = v
+
+        # outputs
+        fields_of_target = target.fields
+        P.nouts = len(out_items)
+        for o, (name, _) in enumerate(out_items):
+            fname = name if structured_out else None
+            if fname is not None and fname not in fields_of_target:
+                raise LoweringError(f"output field {fname} missing in target")
+            P.out_dtype[o] = ir.dtype_code(target.field_dtype(fname))
+            P.out_src[o] = out_regs[o]
+
+        for i, leaf in enumerate(leaves):
+            P.leaf_kind[i] = self.leaf_kind(leaf)
+            P.leaf_dtype[i] = ir.dtype_code(leaf.dtype) if P.leaf_kind[i] == LEAF_ARRAY else 0
+
+        # ---- per-task views
+        red_axes = set(program.reduce.axes) if program.reduce is not None else set()
+        n = program.ndim
+        rows = []
+        gathers = []
+        for key in task_keys:
+            rows.append(self.task_layout(program, spec, target, key, leaves, out_items,
+                                         structured_out, gathers))
+        layout = canonicalize(rows, n, red_axes, leaves, [self.leaf_kind(l) for l in leaves])
+        P.ndim = layout.ndim
+        P.nred = layout.nred
+        P.mode = layout.mode
+        table = layout.table(self.ctx.device)
+        ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
+        return FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
+                           gathers, self.ctx.device)
+
+    def leaf_kind(self, leaf) -> int:
+        if isinstance(leaf, ir.Philox):
+            return LEAF_PHILOX
+        if isinstance(leaf, ir.BlockOffset):
+            return LEAF_OFFSET
+        if isinstance(leaf, ir.Iota):
+            return LEAF_IOTA
+        return LEAF_ARRAY
+
+    def constant_value(self, leaf, args, reads_map):
+        """Value of a leaf that reads a constant (virtual full array, 1-element
+        in-memory array), else None."""
+        if isinstance(leaf, ir.Arg):
+            spec = args[leaf.index]
+            if not isinstance(spec, tuple):
+                return None
+            arr = reads_map[spec[0]].array
+        elif isinstance(leaf, ir.Region):
+            arr = leaf.target
+        else:
+            return None
+        if isinstance(arr, VirtualFullArray):
+            return arr.fill_value
+        if isinstance(arr, VirtualInMemoryArray) and arr.array.size == 1:
+            v = arr.array.reshape(-1)[0]
+            if leaf.field is not None:
+                v = v[leaf.field]
+            return v.item()
+        return None
+
+    # -- one task's views (program space order) --------------------------------
+    def task_layout(self, program, spec, target, key, leaves, out_items, structured_out, gathers):
+        n = program.ndim
+        key = tuple(key)
+        args = spec.block_function(("out",) + key)
+        args = [list(a) if not isinstance(a, (tuple, list, str)) else a for a in args]
+        extent = [None] * n
+        leaf_views = []
+        for leaf in leaves:
+            leaf_views.append(self.leaf_view(leaf, args, spec, gathers, key))
+        # output views
+        out_views = []
+        out_ext = target.chunk_extent(key) if target.ndim else ()
+        for name, _ in out_items:
+            fname = name if structured_out else None
+            out_views.append(chunk_view(target, key, fname) if target.ndim else
+                             ArrView(target.chunk_addr((), fname), [], [], target.field_dtype(fname)))
+        for j, s in enumerate(program.out_axes):
+            if s is not None:
+                extent[s] = out_ext[j]
+        # leaf extents fill / check the space
+        for leaf, (kind, v) in zip(leaves, leaf_views):
+            axes = getattr(leaf, "axes", None)
+            if axes is None or v is None:
+                continue
+            for d, s in enumerate(axes):
+                e = v.extent[d]
+                if s is None:
+                    if e != 1:
+                        raise LoweringError(f"leaf dim {d} of extent {e} has no space dim")
+                    continue
+                if extent[s] is None or extent[s] == 1:
+                    extent[s] = e if extent[s] is None or e != 1 else extent[s]
+                elif e != 1 and e != extent[s]:
+                    raise LoweringError(f"extent mismatch on space dim {s}: {e} vs {extent[s]}")
+        extent = [1 if e is None else e for e in extent]
+        # strides per space dim
+        lstrides, bases = [], []
+        for leaf, (kind, v) in zip(leaves, leaf_views):
+            st = [0] * n
+            axes = getattr(leaf, "axes", ())
+            if v is not None:
+                for d, s in enumerate(axes):
+                    if s is not None and v.extent[d] != 1:
+                        st[s] = v.stride[d]
+                    elif s is not None and v.extent[d] == 1 and extent[s] != 1:
+                        st[s] = 0
+                bases.append(v.base)
+            else:
+                bases.append(0)
+            lstrides.append(st)
+        ostrides = []
+        for (name, _), v in zip(out_items, out_views):
+            st = [0] * n
+            for j, s in enumerate(program.out_axes):
+                if s is not None and j < len(v.stride):
+                    st[s] = v.stride[j] if extent[s] != 1 else 0
+            ostrides.append(st)
+        obases = [v.base for v in out_views]
+        key_lo = key_hi = 0
+        block_offset = 0
+        for leaf, (kind, v) in zip(leaves, leaf_views):
+            if kind == LEAF_PHILOX:
+                key_lo, key_hi = v.key
+            if kind in (LEAF_PHILOX, LEAF_OFFSET):
+                block_offset = v.block_offset
+        return TaskRow(extent, bases, lstrides, obases, ostrides, key_lo, key_hi, block_offset)
+
+    def leaf_view(self, leaf, args, spec, gathers, out_key):
+        """(kind, view) for one leaf of one task."""
+        if isinstance(leaf, ir.Arg):
+            a = args[leaf.index]
+            if isinstance(a, tuple):
+                arr = self.resolve_target(a[0], spec.reads_map)
+                if isinstance(arr, _OffsetsSource):
+                    return LEAF_OFFSET, _Scalar(block_id_to_offset(a[1:], arr.shape))
+                return LEAF_ARRAY, (chunk_view(arr, a[1:], leaf.field) if arr.ndim else
+                                    ArrView(arr.chunk_addr((), leaf.field), [], [], arr.field_dtype(leaf.field)))
+            keys = flatten_keys(a)
+            arr = self.resolve_target(keys[0][0], spec.reads_map)
+            v = merged_view(arr, keys, leaf.field)
+            if v is None:
+                v = self.ctx.gather_keys(arr, keys, leaf.field, gathers)
+            return LEAF_ARRAY, v
+        if isinstance(leaf, ir.Region):
+            block_id = tuple(args[leaf.block_arg][1:])
+            region = leaf.region(block_id)
+            arr = self.ctx.device_source(leaf.target)
+            v = region_view(arr, region, leaf.field)
+            if v is None:
+                v = self.ctx.gather_region(arr, region, leaf.field, gathers)
+            else:
+                # int-indexed dims are already extent 1
+                pass
+            return LEAF_ARRAY, v
+        if isinstance(leaf, ir.Philox):
+            block_id = tuple(args[leaf.block_arg][1:])
+            off = block_id_to_offset(block_id, leaf.numblocks)
+            from .random import philox_key
+
+            ext = [leaf.chunks[d][b] for d, b in enumerate(block_id)]
+            v = ArrView(0, ext, list(c_strides(ext)), np.dtype(np.float64))
+            v.key = philox_key(leaf.root_seed, off)
+            v.block_offset = off
+            return LEAF_PHILOX, v
+        if isinstance(leaf, ir.BlockOffset):
+            block_id = tuple(args[leaf.block_arg][1:])
+            return LEAF_OFFSET, _Scalar(block_id_to_offset(block_id, leaf.numblocks))
+        if isinstance(leaf, ir.Iota):
+            block_id = tuple(args[leaf.arg][1:])
+            nd = len(leaf.chunks)
+            ext = [leaf.chunks[d][b] for d, b in enumerate(block_id)]
+            start = sum(leaf.chunks[leaf.dim][:block_id[leaf.dim]])
+            st = [1 if d == leaf.dim else 0 for d in range(nd)]
+            return LEAF_IOTA, ArrView(start, ext, st, np.dtype(np.int64))
+        raise LoweringError(f"unsupported leaf {type(leaf).__name__}")
+
+    # -- copies ---------------------------------------------------------------
+    def lower_copy_program(self, program, spec, target, task_keys):
+        """merge_chunks / index / identity maps as box copies."""
+        leaf = program.outputs
+        boxes = []
+        for key in task_keys:
+            key = tuple(key)
+            args = spec.block_function(("out",) + key)
+            dst = chunk_view(target, key) if target.ndim else ArrView(target.chunk_addr(()), [], [], target.dtype)
+            if isinstance(leaf, ir.Region):
+                block_id = tuple(args[leaf.block_arg][1:])
+                region = leaf.region(block_id)
+                src = self.ctx.device_source(leaf.target)
+                if isinstance(src, _ConstSource):
+                    raise LoweringError("copy from a constant")
+                # destination strides for the region's kept dims (space = out dims)
+                dstr = _dst_strides_for(leaf.axes, program.out_axes, dst)
+                boxes += boxes_for_region(src, region, dst.base, dstr, leaf.field)
+            else:
+                a = args[leaf.index]
+                keys = [a] if isinstance(a, tuple) else flatten_keys(a)
+                src = self.resolve_target(keys[0][0], spec.reads_map)
+                dstr = _dst_strides_for(leaf.axes, program.out_axes, dst)
+                for k in keys:
+                    sv = chunk_view(src, k[1:], leaf.field) if src.ndim else \
+                        ArrView(src.chunk_addr((), leaf.field), [], [], src.dtype)
+                    # position of this chunk inside the merged destination
+                    boxes.append(Box(sv.base, dst.base + _merged_offset(src, keys, k, dstr) * target.dtype.itemsize,
+                                     sv.extent, sv.stride, dstr[:len(sv.extent)]))
+        return CopyLaunch(boxes, target.dtype.itemsize, self.ctx.device)
+
+
+def _merged_offset(src, keys, k, dstr):
+    if len(keys) == 1:
+        return 0
+    first = [min(kk[d + 1] for kk in keys) for d in range(src.ndim)]
+    off = 0
+    for d in range(src.ndim):
+        pos = sum(src._norm_chunks[d][first[d]:k[d + 1]])
+        off += pos * dstr[d]
+    return off
+
+
+def _dst_strides_for(leaf_axes, out_axes, dst: ArrView):
+    """Destination element strides for each leaf dim (0 for unit dims)."""
+    space_to_out = {s: j for j, s in enumerate(out_axes) if s is not None}
+    out = []
+    for s in leaf_axes:
+        if s is None or s not in space_to_out:
+            out.append(0)
+        else:
+            out.append(dst.stride[space_to_out[s]] if dst.stride else 0)
+    return out
+
+
+class _Scalar:
+    def __init__(self, offset):
+        self.block_offset = offset
+        self.base = 0
+        self.extent = []
+        self.stride = []
+
+
+class _ConstSource:
+    def __init__(self, value, arr):
+        self.value = value
+        self.array = arr
+
+
+class _OffsetsSource:
+    def __init__(self, arr):
+        self.shape = arr.shape
+        self.ndim = arr.ndim
+
+
+def _set_insn(slot, ins):
+    op, a, b, c, t, imm = ins
+    slot.op, slot.a, slot.b, slot.c, slot.t, slot.imm = op, a, b, c, t, imm
+
+
+# ------------------------------------------------------------------ canonical layout
+
+
+@dataclass
+class TaskRow:
+    extent: List[int]
+    bases: List[int]
+    lstrides: List[List[int]]
+    obases: List[int]
+    ostrides: List[List[int]]
+    key_lo: int
+    key_hi: int
+    block_offset: int
+
+
+@dataclass
+class Layout:
+    order: List[int]          # groups of program dims (after coalescing) in kernel order
+    groups: List[List[int]]
+    ndim: int
+    nred: int
+    mode: int
+    rows: List[TaskRow]
+    max_kept: int
+    max_red: int
+
+    def table(self, device):
+        import torch
+
+        arr = np.zeros(len(self.rows), dtype=nat.TASK_DTYPE)
+        for i, r in enumerate(self.rows):
+            ext, ls, os_ = _apply_groups(r, self.groups)
+            e = [1] * nat.MAX_DIMS
+            e[:len(ext)] = ext
+            arr[i]["extent"] = e
+            for l in range(len(r.bases)):
+                arr[i]["leaf_base"][l] = r.bases[l]
+                s = [0] * nat.MAX_DIMS
+                s[:len(ext)] = ls[l]
+                arr[i]["leaf_stride"][l] = s
+            for o in range(len(r.obases)):
+                arr[i]["out_base"][o] = r.obases[o]
+                s = [0] * nat.MAX_DIMS
+                s[:len(ext)] = os_[o]
+                arr[i]["out_stride"][o] = s
+            arr[i]["key_lo"] = np.uint64(r.key_lo)
+            arr[i]["key_hi"] = np.uint64(r.key_hi)
+            arr[i]["block_offset"] = r.block_offset
+        return torch.from_numpy(arr.view(np.uint8).copy()).to(device)
+
+
+def _apply_groups(r: TaskRow, groups):
+    """Coalesce program dims into kernel dims (each group = contiguous run,
+    outermost first; the group's stride is its innermost dim's)."""
+    ext = [math.prod(r.extent[d] for d in g) for g in groups]
+    ls = [[st[g[-1]] for g in groups] for st in r.lstrides]
+    os_ = [[st[g[-1]] for g in groups] for st in r.ostrides]
+    return ext, ls, os_
+
+
+def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout:
+    if n == 0:
+        groups = []
+    else:
+        groups = None
+    # 1. dims of extent 1 in every task are dropped
+    live = [d for d in range(n) if any(r.extent[d] != 1 for r in rows)]
+    if not live:
+        live = [n - 1] if n else []
+    kept = [d for d in live if d not in red_axes]
+    red = [d for d in live if d in red_axes]
+    innermost = live[-1] if live else None
+    use_b = False
+    if red and innermost is not None and innermost in red_axes:
+        inner_ext = max(r.extent[innermost] for r in rows)
+        contig = all(st[innermost] in (0, 1) for r in rows for st in r.lstrides)
+        use_b = inner_ext >= 64 and contig
+    order = (kept + red) if use_b else (red + kept)
+
+    def can_merge(a, b):
+        # a then b adjacent in `order`, same reduced status
+        if (a in red_axes) != (b in red_axes):
+            return False
+        for r in rows:
+            for st in r.lstrides + r.ostrides:
+                if st[a] != st[b] * r.extent[b]:
+                    return False
+        return True
+
+    groups = []
+    for d in order:
+        if groups and can_merge(groups[-1][-1], d) and _groups_contiguous(groups[-1], d, order):
+            groups[-1].append(d)
+        else:
+            groups.append([d])
+    if not groups:
+        groups = [[0]] if n else []
+    nred = sum(1 for g in groups if g[0] in red_axes)
+    ndim = len(groups)
+    if ndim > nat.MAX_DIMS:
+        raise LoweringError(f"task needs {ndim} iteration dims after coalescing (max {nat.MAX_DIMS})")
+    if ndim == 0:
+        # 0-d program: one element per task
+        groups = [[]]
+        ndim = 1
+
+    def gext(r, g):
+        return math.prod(r.extent[d] for d in g) if g else 1
+
+    kept_groups = [g for g in groups if not (g and g[0] in red_axes)]
+    red_groups = [g for g in groups if g and g[0] in red_axes]
+    max_kept = max(math.prod(gext(r, g) for g in kept_groups) for r in rows) if rows else 1
+    max_red = max(math.prod(gext(r, g) for g in red_groups) for r in rows) if rows else 1
+    # vectorisation (VEC=4) along the innermost kernel dim
+    inner = groups[-1]
+    mode = 1 if use_b else 0
+    if inner and _vec_ok(rows, inner, kinds, leaves, use_b):
+        mode |= 4
+    rows2 = []
+    for r in rows:
+        if not groups[0]:
+            rows2.append(TaskRow([1], r.bases, [[0] for _ in r.lstrides], r.obases,
+                                 [[0] for _ in r.ostrides], r.key_lo, r.key_hi, r.block_offset))
+        else:
+            rows2.append(r)
+    lay = Layout(order, groups if groups[0] else [[0]], ndim, nred, mode, rows2,
+                 max(1, max_kept), max(1, max_red))
+    if not groups[0]:
+        lay.groups = [[0]]
+        for r in rows2:
+            r.extent = [1]
+    return lay
+
+
+def _groups_contiguous(group, d, order):
+    return order.index(d) == order.index(group[-1]) + 1
+
+
+def _vec_ok(rows, inner, kinds, leaves, use_b) -> bool:
+    for r in rows:
+        e = math.prod(r.extent[d] for d in inner)
+        if e % 4:
+            return False
+        d_in = inner[-1]
+        for l, (st, kind) in enumerate(zip(r.lstrides, kinds)):
+            s_in = st[d_in]
+            if kind == LEAF_ARRAY:
+                if s_in not in (0, 1):
+                    return False
+                if s_in == 1:
+                    isz = np.dtype(leaves[l].dtype).itemsize
+                    if r.bases[l] % (4 * isz):
+                        return False
+                    if any(st[d] % 4 for d in range(len(st)) if d not in inner and r.extent[d] != 1):
+                        return False
+            elif kind == LEAF_PHILOX:
+                if s_in != 1:
+                    return False
+        if not use_b:
+            for o, st in enumerate(r.ostrides):
+                if st[d_in] != 1:
+                    return False
+                if r.obases[o] % 32:
+                    return False
+                if any(st[d] % 4 for d in range(len(st)) if d not in inner and r.extent[d] != 1):
+                    return False
+    return True

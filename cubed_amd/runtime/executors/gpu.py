@@ -1,0 +1,354 @@
+"""The MI355X DAG executor.
+
+Replaces the reference's task loop (``PythonDagExecutor``,
+runtime/executors/python.py:14-32, and the thread-pool
+``AsyncPythonDagExecutor``, python_async.py:121-142) behind the same plug-in
+interface ``execute_dag(dag, callbacks, array_names, resume, spec)``:
+
+* each op node of the finalized DAG (one fused pipeline) is lowered once to
+  one or two kernel launches over ALL its tasks (cubed_amd/lowering.py) and
+  cached on the executor, so re-executing a plan replays the launches;
+* launches are stream-ordered on one HIP stream (torch's current stream by
+  default); nothing synchronises inside ``execute_dag`` -- reading a result
+  back (``compute()``) or the caller's ``torch.cuda.synchronize()`` does;
+* intermediates stay resident in HBM (``DeviceArray`` slabs allocated by the
+  create-arrays node); ``resume=True`` skips ops whose targets were already
+  written by an earlier compute (the reference's resume, runtime/pipeline.py
+  :8-35);
+* one ``TaskEndEvent(array_name, num_tasks)`` per pipeline, so the
+  reference's callbacks (task counters, history, progress) keep working.
+
+There is no CPU path: a pipeline whose chunk function cannot be lowered
+raises ``LoweringError`` instead of running host code.
+"""
+
+from __future__ import annotations
+
+import itertools
+import math
+import time
+import weakref
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ... import _native as nat
+from ... import ir
+from ...core.ops import UploadSpec, upload_stage
+from ...core.plan import create_arrays_stage
+from ...lowering import (
+    ArrView,
+    Box,
+    CopyLaunch,
+    GemmLaunch,
+    LoweringError,
+    Lowerer,
+    _OffsetsSource,
+    boxes_for_region,
+    chunk_view,
+)
+from ...primitive.blockwise import apply_blockwise
+from ...primitive.rechunk import copy_read_to_write
+from ...storage import (
+    DeviceArray,
+    HostArray,
+    VirtualEmptyArray,
+    VirtualFullArray,
+    VirtualInMemoryArray,
+    VirtualOffsetsArray,
+    c_strides,
+)
+from ..pipeline import visit_nodes
+from ..types import DagExecutor, TaskEndEvent
+
+HBM_BYTES_PER_GPU = 288 * 10**9
+
+
+def gather_to_host(arr: DeviceArray) -> np.ndarray:
+    import torch
+
+    torch.cuda.synchronize(arr.device)
+    return arr.to_numpy()
+
+
+class _Alloc:
+    def __init__(self, ctx, targets):
+        self.ctx = ctx
+        self.targets = list(targets)
+
+    def run(self, stream):
+        for t in self.targets:
+            self.ctx.allocate(t)
+
+
+class _Upload:
+    def __init__(self, ctx, cfg: UploadSpec):
+        self.ctx = ctx
+        self.cfg = cfg
+
+    def run(self, stream):
+        self.ctx.allocate(self.cfg.target)
+        self.cfg.target.from_numpy(np.asarray(self.cfg.source.array))
+
+
+class GpuDagExecutor(DagExecutor):
+    """Runs Cubed plans on one MI355X (one process per GPU)."""
+
+    def __init__(self, device=None, stream=None, check_memory: bool = True):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise nat.NativeError("GpuDagExecutor needs a visible GPU (cubed_amd has no CPU path)")
+        nat.lib()
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self._stream = stream
+        self.check_memory = check_memory
+        self._cache: Dict[int, tuple] = {}
+        self._uploads: Dict[int, DeviceArray] = {}
+        self._scratch: List = []
+        self.lowerer = Lowerer(self)
+        self.rank, self.world = 0, 1
+
+    # -- plumbing used by the lowerer ------------------------------------------
+    @property
+    def stream(self) -> int:
+        import torch
+
+        if self._stream is not None:
+            return self._stream.cuda_stream if hasattr(self._stream, "cuda_stream") else int(self._stream)
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def allocate(self, t: DeviceArray):
+        if not t.allocated:
+            t.allocate(self.device, self.rank, self.world)
+
+    def device_source(self, arr):
+        """A readable device-side representation of an input array."""
+        if isinstance(arr, DeviceArray):
+            if not arr.allocated:
+                self.allocate(arr)
+            return arr
+        if isinstance(arr, VirtualOffsetsArray):
+            return _OffsetsSource(arr)
+        if isinstance(arr, (VirtualInMemoryArray, VirtualFullArray, HostArray)):
+            key = id(arr)
+            d = self._uploads.get(key)
+            if d is None:
+                d = DeviceArray(arr.shape, arr.dtype, arr.chunks if arr.ndim else (),
+                                name=f"virtual-{key}")
+                self.allocate(d)
+                if isinstance(arr, VirtualFullArray):
+                    self._fill(d, arr.fill_value)
+                else:
+                    d.from_numpy(np.asarray(arr.array))
+                d.written = True
+                self._uploads[key] = d
+                self._keepalive = getattr(self, "_keepalive", [])
+                self._keepalive.append(arr)
+            return d
+        if isinstance(arr, VirtualEmptyArray):
+            raise LoweringError("a chunk function reads an empty (template) array")
+        raise LoweringError(f"unsupported source array {type(arr).__name__}")
+
+    def _fill(self, d: DeviceArray, value):
+        import torch
+
+        tdt = {np.dtype(np.float64): torch.float64, np.dtype(np.float32): torch.float32,
+               np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
+               np.dtype(np.int16): torch.int16, np.dtype(np.int8): torch.int8,
+               np.dtype(np.uint8): torch.uint8, np.dtype(np.bool_): torch.bool}
+        for f in d.fields:
+            dt = d.field_dtype(f)
+            if dt in tdt:
+                d.slabs[f].view(tdt[dt]).fill_(value if f is None else value[f])
+            else:
+                raw = np.full(d.slabs[f].numel() // dt.itemsize, value, dtype=dt)
+                d.slabs[f].copy_(torch.from_numpy(raw.view(np.uint8)))
+
+    def scratch(self, nbytes: int) -> int:
+        import torch
+
+        buf = torch.empty(max(nbytes, 16) + 256, dtype=torch.uint8, device=self.device)
+        self._scratch.append(buf)
+        p = buf.data_ptr()
+        return (p + 255) // 256 * 256
+
+    def gather_region(self, arr: DeviceArray, region, field, gathers) -> ArrView:
+        """Copy a multi-chunk region into contiguous scratch; return its view
+        in array-dim order (int-indexed dims as extent 1)."""
+        ext_all, keep_ext = [], []
+        for d, s in enumerate(region):
+            if isinstance(s, slice):
+                start, stop, step = s.start or 0, s.stop, s.step or 1
+                e = max(0, (stop - start + step - 1) // step)
+                ext_all.append(e)
+                keep_ext.append(e)
+            elif isinstance(s, list):
+                ext_all.append(len(s))
+                keep_ext.append(len(s))
+            else:
+                ext_all.append(1)
+        dt = arr.field_dtype(field)
+        base = self.scratch(math.prod(keep_ext) * dt.itemsize)
+        dstr = list(c_strides(keep_ext))
+        gathers.append((boxes_for_region(arr, region, base, dstr, field), dt.itemsize))
+        strides_all, k = [], 0
+        for d, s in enumerate(region):
+            if isinstance(s, (slice, list)):
+                strides_all.append(dstr[k])
+                k += 1
+            else:
+                strides_all.append(0)
+        return ArrView(base, ext_all, strides_all, dt)
+
+    def gather_keys(self, arr: DeviceArray, keys, field, gathers) -> ArrView:
+        coords = [k[1:] for k in keys]
+        region = []
+        for d in range(arr.ndim):
+            lo = min(c[d] for c in coords)
+            hi = max(c[d] for c in coords)
+            start = arr.chunk_start(tuple(lo if dd == d else 0 for dd in range(arr.ndim)))[d]
+            stop_c = tuple(hi if dd == d else 0 for dd in range(arr.ndim))
+            stop = arr.chunk_start(stop_c)[d] + arr.chunk_extent(stop_c)[d]
+            region.append(slice(start, stop, 1))
+        return self.gather_region(arr, tuple(region), field, gathers)
+
+    # -- lowering --------------------------------------------------------------
+    def _task_keys(self, target: DeviceArray):
+        if target.ndim == 0:
+            return [()]
+        return list(itertools.product(*[range(n) for n in target.numblocks]))
+
+    def lower_node(self, name, node) -> list:
+        pipeline = node["pipeline"]
+        fn = pipeline.function
+        cfg = pipeline.config
+        if fn is create_arrays_stage:
+            return [_Alloc(self, pipeline.mappable)]
+        if fn is upload_stage:
+            return [_Upload(self, cfg)]
+        if fn is copy_read_to_write:
+            return [self._lower_rechunk(cfg)]
+        if fn is apply_blockwise:
+            target = cfg.write.array
+            self.allocate(target)
+            program = cfg.function
+            keys = self._task_keys(target)
+            if isinstance(program, ir.OpaqueProgram):
+                raise LoweringError(
+                    f"op {name}: {program.func!r} cannot run on the MI355X executor "
+                    "(not expressible as a fused chunk program)")
+            if isinstance(program, ir.ExprProgram):
+                launch = self.lowerer.lower_expr_pipeline(program, cfg, target, keys)
+                return _with_gathers(launch, self.device)
+            if isinstance(program, (ir.MatmulProgram, ir.TensordotProgram)):
+                return [self._lower_gemm(program, cfg, target, keys)]
+            if isinstance(program, ir.GemmThenProgram):
+                from types import SimpleNamespace
+
+                from ...primitive.types import CubedArrayProxy
+
+                gt = program.gemm_target
+                self.allocate(gt)
+                gcfg = SimpleNamespace(block_function=program.gemm_block_function,
+                                       reads_map=program.gemm_reads)
+                launches = [self._lower_gemm(program.gemm, gcfg, gt, self._task_keys(gt))]
+                if not isinstance(program.then, ir.ExprProgram):
+                    raise LoweringError(f"op {name}: GEMM consumer {program.then!r} is not lowerable")
+                tcfg = SimpleNamespace(block_function=program.then_block_function,
+                                       reads_map={gt.name: CubedArrayProxy(gt, gt.chunks)},
+                                       write=cfg.write)
+                launch = self.lowerer.lower_expr_pipeline(program.then, tcfg, target, keys)
+                return launches + _with_gathers(launch, self.device)
+            raise LoweringError(f"op {name}: unsupported program {type(program).__name__}")
+        raise LoweringError(f"op {name}: unknown stage function {getattr(fn, '__name__', fn)}")
+
+    def _lower_rechunk(self, cfg):
+        src = self.device_source(cfg.read.array)
+        dst = cfg.write.array
+        self.allocate(dst)
+        boxes: List[Box] = []
+        for key in self._task_keys(dst):
+            region = tuple(slice(s, s + e) for s, e in zip(dst.chunk_start(key), dst.chunk_extent(key)))
+            dv = chunk_view(dst, key)
+            boxes += boxes_for_region(src, region, dv.base, dv.stride)
+        return CopyLaunch(boxes, dst.dtype.itemsize, self.device)
+
+    def _lower_gemm(self, program, cfg, target, keys):
+        rows = np.zeros(len(keys), dtype=nat.GEMM_DTYPE)
+        max_m = max_n = 1
+        f32 = (program.out_dtype == np.float32)
+        for i, key in enumerate(keys):
+            args = cfg.block_function(("out",) + tuple(key))
+            a_key, b_key = args[0], args[1]
+            A = self.device_source(cfg.reads_map[a_key[0]].array)
+            B = self.device_source(cfg.reads_map[b_key[0]].array)
+            if A.ndim != 2 or B.ndim != 2:
+                raise LoweringError("batched matmul chunks are not lowered yet")
+            if f32 and not (A.dtype == np.float32 and B.dtype == np.float32):
+                raise LoweringError("f32 matmul with non-f32 inputs")
+            if not f32 and (A.dtype != np.float64 or B.dtype != np.float64 or target.dtype != np.float64):
+                raise LoweringError(f"matmul of {A.dtype} x {B.dtype} -> {target.dtype} is not lowered "
+                                    "(f32 and f64 only)")
+            am, ak = A.chunk_extent(a_key[1:])
+            bk, bn = B.chunk_extent(b_key[1:])
+            if ak != bk:
+                raise LoweringError("contracted chunk extents differ")
+            rows[i] = (A.chunk_addr(a_key[1:]), B.chunk_addr(b_key[1:]), target.chunk_addr(key),
+                       am, bn, ak, ak, bn, bn, 0)
+            max_m, max_n = max(max_m, am), max(max_n, bn)
+        code = ir.dtype_code(np.float32 if f32 else np.float64)
+        return GemmLaunch(rows, code, max_m, max_n, self.device)
+
+    # -- execution -------------------------------------------------------------
+    def compiled(self, name, node):
+        pipeline = node["pipeline"]
+        entry = self._cache.get(id(pipeline))
+        if entry is not None and entry[0]() is pipeline:
+            return entry[1]
+        launches = self.lower_node(name, node)
+        self._cache[id(pipeline)] = (weakref.ref(pipeline), launches)
+        return launches
+
+    def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
+        stream = self.stream
+        nodes = dict(dag.nodes(data=True))
+        if self.check_memory:
+            self._check_hbm(dag)
+        for name, node in visit_nodes(dag, resume=resume):
+            t0 = time.time()
+            for launch in self.compiled(name, node):
+                launch.run(stream)
+            for out in dag.successors(name):
+                target = nodes[out].get("target")
+                if isinstance(target, DeviceArray):
+                    target.written = True
+            if callbacks is not None:
+                op = node.get("primitive_op")
+                ev = TaskEndEvent(array_name=name, num_tasks=op.num_tasks if op is not None else 1,
+                                  function_start_tstamp=t0, function_end_tstamp=time.time())
+                ev.task_result_tstamp = time.time()
+                for cb in callbacks:
+                    cb.on_task_end(ev)
+
+    def _check_hbm(self, dag):
+        total = 0
+        for _, d in dag.nodes(data=True):
+            t = d.get("target")
+            if isinstance(t, DeviceArray):
+                total += t.device_bytes()
+        if total > HBM_BYTES_PER_GPU:
+            raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
+                              f"MI355X holds ({HBM_BYTES_PER_GPU})")
+
+
+def _with_gathers(launch, device):
+    """Turn collected scratch gathers into CopyLaunches run before ``launch``."""
+    gathers = getattr(launch, "gathers", None)
+    if not gathers:
+        return [launch]
+    by_size: Dict[int, List[Box]] = {}
+    for boxes, isz in gathers:
+        by_size.setdefault(isz, []).extend(boxes)
+    launch.gathers = [CopyLaunch(b, isz, device) for isz, b in by_size.items()]
+    return [launch]

@@ -1,0 +1,234 @@
+/*
+ * cubed_amd.h -- C ABI of the MI355X execution path for Cubed's blockwise /
+ * reduction / rechunk primitives (libcubed_amd.so).
+ *
+ * Plain C: fixed-size structs, raw device pointers, element counts and a
+ * hipStream_t passed as void*.  No torch or C++ types cross this boundary.
+ * The caller owns every buffer (arrays, task tables, workspace); the library
+ * never allocates or frees persistent memory and never synchronises the
+ * device.  Every entry point returns 0 on success, a positive hipError_t
+ * value on a HIP failure, or a negative CUBED_E_* code on a bad argument;
+ * cubed_last_error() gives a message for the calling thread.
+ *
+ * Which reference interface each entry point replaces (paths relative to the
+ * reference tree, rsignell/cubed v0.12.0):
+ *
+ *   cubed_fused_chunks   -> apply_blockwise(out_key, config=BlockwiseSpec)
+ *                           cubed/primitive/blockwise.py:61-84, running the
+ *                           fused chunk function built by fuse/fuse_multiple
+ *                           (:368-508): elementwise chains (array_object.py
+ *                           :121-348, elementwise_functions.py), per-chunk
+ *                           reductions (_mean_func/_mean_combine/
+ *                           _mean_aggregate statistical_functions.py:54-100,
+ *                           nan_functions.py:37-59, sum/max/min/prod) and the
+ *                           merge_chunks+combine rounds of core/ops.py:849-889.
+ *   cubed_random_chunks  -> _random(x, numblocks, root_seed, block_id)
+ *                           cubed/random.py:31-36 (numpy Philox4x64-10 +
+ *                           Generator.random), bit-exact.
+ *   cubed_copy_boxes     -> copy_read_to_write(chunk_key, config=CubedCopySpec)
+ *                           cubed/primitive/rechunk.py:187-192, and the
+ *                           map_direct region reads _copy_chunk
+ *                           (core/ops.py:784-787) / _read_index_chunk
+ *                           (core/ops.py:481-486).
+ *   cubed_gemm_chunks    -> _matmul / _tensordot chunk products
+ *                           cubed/array_api/linear_algebra_functions.py:62-64,
+ *                           :139-149 (numpy BLAS sgemm/dgemm per task).
+ */
+#ifndef CUBED_AMD_H
+#define CUBED_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CUBED_ABI_VERSION 1
+
+#define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
+#define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
+#define CUBED_MAX_FIELDS 2 /* reduced fields (e.g. mean's n and total)      */
+#define CUBED_MAX_OUTS 2   /* output arrays written per task                */
+#define CUBED_MAX_INSNS 48 /* VM instructions in the prologue program       */
+#define CUBED_MAX_EPI 16   /* VM instructions in the epilogue program       */
+#define CUBED_MAX_CONSTS 16
+#define CUBED_NREGS 6      /* VM registers; leaf i is preloaded into reg i  */
+
+/* error codes (negative); positive values are hipError_t */
+#define CUBED_E_ARG (-1)
+#define CUBED_E_DTYPE (-2)
+#define CUBED_E_LAYOUT (-3)
+#define CUBED_E_WORKSPACE (-4)
+
+/* element dtypes (numpy kinds); bool is 1 byte 0/1 */
+enum cubed_dtype {
+  CUBED_BOOL = 0, CUBED_I8, CUBED_I16, CUBED_I32, CUBED_I64,
+  CUBED_U8, CUBED_U16, CUBED_U32, CUBED_U64,
+  CUBED_F32, CUBED_F64, CUBED_F16, CUBED_BF16
+};
+
+/* register value type of a program (all arithmetic happens in it; narrower
+ * node dtypes are re-rounded by CAST instructions) */
+enum cubed_vtype { CUBED_V_F32 = 0, CUBED_V_F64 = 1, CUBED_V_I64 = 2 };
+
+/* leaf kinds */
+enum cubed_leaf_kind {
+  CUBED_LEAF_ARRAY = 0,  /* strided view of a chunk (or of merged chunks)  */
+  CUBED_LEAF_PHILOX = 1, /* numpy Generator(Philox(key)).random() stream,  */
+                         /* element = C-order position in the task's box   */
+  CUBED_LEAF_OFFSET = 2, /* the task's block offset (int64), for block_id  */
+  CUBED_LEAF_IOTA = 3    /* int64 value leaf_base + sum(coord*stride): the  */
+                         /* global index along an axis (arange/eye/tril)    */
+};
+
+/* reduction ops of a field; accumulators are f64 or i64 (acc_type) */
+enum cubed_rop {
+  CUBED_R_NONE = 0, CUBED_R_SUM, CUBED_R_NANSUM, CUBED_R_COUNT,
+  CUBED_R_COUNT_NONNAN, CUBED_R_MAX, CUBED_R_MIN, CUBED_R_PROD,
+  CUBED_R_NANMAX, CUBED_R_NANMIN, CUBED_R_ANY, CUBED_R_ALL, CUBED_R_NANPROD
+};
+
+/* VM opcodes (two-address: r[a] = op(r[a], r[b]); where: r[a] = r[c] ? r[a] : r[b]) */
+enum cubed_op {
+  CUBED_OP_NOP = 0,
+  CUBED_OP_CONST,   /* r[a] = consts[imm]                                  */
+  CUBED_OP_MOV,     /* r[a] = r[b]                                         */
+  CUBED_OP_CAST,    /* r[a] = round r[a] to dtype t (from dtype imm)       */
+  CUBED_OP_WHERE,   /* r[a] = r[c] ? r[a] : r[b]                           */
+  /* unary */
+  CUBED_OP_NEG = 16, CUBED_OP_ABS, CUBED_OP_SQRT, CUBED_OP_EXP, CUBED_OP_LOG,
+  CUBED_OP_SIN, CUBED_OP_COS, CUBED_OP_TAN, CUBED_OP_TANH, CUBED_OP_FLOOR,
+  CUBED_OP_CEIL, CUBED_OP_TRUNC, CUBED_OP_RINT, CUBED_OP_ISNAN, CUBED_OP_ISINF,
+  CUBED_OP_ISFINITE, CUBED_OP_LNOT, CUBED_OP_BNOT, CUBED_OP_SIGN,
+  CUBED_OP_SQUARE, CUBED_OP_RECIP, CUBED_OP_LOG1P, CUBED_OP_EXPM1,
+  CUBED_OP_LOG2, CUBED_OP_LOG10, CUBED_OP_SINH, CUBED_OP_COSH, CUBED_OP_ASIN,
+  CUBED_OP_ACOS, CUBED_OP_ATAN, CUBED_OP_ASINH, CUBED_OP_ACOSH,
+  CUBED_OP_ATANH, CUBED_OP_EXP2, CUBED_OP_SIGNBIT,
+  /* binary */
+  CUBED_OP_ADD = 64, CUBED_OP_SUB, CUBED_OP_MUL, CUBED_OP_DIV,
+  CUBED_OP_FLOORDIV, CUBED_OP_MOD, CUBED_OP_POW, CUBED_OP_MAX, CUBED_OP_MIN,
+  CUBED_OP_EQ, CUBED_OP_NE, CUBED_OP_LT, CUBED_OP_LE, CUBED_OP_GT,
+  CUBED_OP_GE, CUBED_OP_LAND, CUBED_OP_LOR, CUBED_OP_LXOR, CUBED_OP_BAND,
+  CUBED_OP_BOR, CUBED_OP_BXOR, CUBED_OP_SHL, CUBED_OP_SHR, CUBED_OP_ATAN2,
+  CUBED_OP_HYPOT, CUBED_OP_LOGADDEXP, CUBED_OP_COPYSIGN, CUBED_OP_FMAX,
+  CUBED_OP_FMIN, CUBED_OP_LOGADDEXP2
+};
+
+typedef struct {
+  uint8_t op, a, b, c; /* opcode and register operands                      */
+  uint8_t t;           /* CAST target dtype                                 */
+  uint8_t pad;
+  uint16_t imm;        /* CONST index / CAST source dtype                   */
+} cubed_insn_t;
+
+/* A fused chunk program: leaves -> prologue -> (per-field reduce) ->
+ * epilogue -> outputs.  Passed by value as the kernel argument. */
+typedef struct {
+  int32_t vtype;                 /* enum cubed_vtype                        */
+  int32_t ndim;                  /* iteration dims (<= CUBED_MAX_DIMS)      */
+  int32_t nred;                  /* dims [0,nred) are reduced (kernel A) or */
+                                 /* dims [ndim-nred,ndim) (kernel B)        */
+  int32_t mode;                  /* kernel shape: 0 = A (reduced dims first,*/
+                                 /* or a map), 1 = B (reduced dims last);   */
+                                 /* +4 when the innermost dim is packed     */
+                                 /* (VEC=4 loads/stores; host-checked)      */
+  int32_t nleaves;
+  uint8_t leaf_kind[CUBED_MAX_LEAVES];
+  uint8_t leaf_dtype[CUBED_MAX_LEAVES];
+  int32_t nfields;               /* 0 = map (no reduction)                  */
+  uint8_t field_rop[CUBED_MAX_FIELDS];
+  uint8_t field_acc[CUBED_MAX_FIELDS]; /* 0 = f64 accumulator, 1 = i64     */
+  uint8_t field_src[CUBED_MAX_FIELDS]; /* register holding the field value  */
+  uint8_t pad0[2];
+  int32_t nouts;
+  uint8_t out_dtype[CUBED_MAX_OUTS];
+  uint8_t out_src[CUBED_MAX_OUTS]; /* register (or field when no epilogue)  */
+  int32_t ninsns;
+  int32_t nepi;                  /* -1 = store fields directly              */
+  cubed_insn_t insns[CUBED_MAX_INSNS];
+  cubed_insn_t epi[CUBED_MAX_EPI];
+  union { double f; int64_t i; } consts[CUBED_MAX_CONSTS];
+} cubed_program_t;
+
+/* One task (= one output chunk of the pipeline, or one sub-box of it).
+ * Strides are in elements; a broadcast dim has stride 0; an output has
+ * stride 0 on reduced dims.  Bases are device byte addresses. */
+typedef struct {
+  int64_t extent[CUBED_MAX_DIMS];
+  int64_t leaf_base[CUBED_MAX_LEAVES];
+  int64_t leaf_stride[CUBED_MAX_LEAVES][CUBED_MAX_DIMS];
+  int64_t out_base[CUBED_MAX_OUTS];
+  int64_t out_stride[CUBED_MAX_OUTS][CUBED_MAX_DIMS];
+  uint64_t key_lo, key_hi; /* Philox key of this task's random leaf          */
+  int64_t block_offset;    /* C-order block offset (block_id_to_offset)      */
+  int64_t pad;
+} cubed_task_t;
+
+/* Run a fused chunk program over ntasks tasks (task table in device memory).
+ * All tasks share the dim structure of `prog` (ndim, nred) but may differ in
+ * extents (edge chunks).  max_kept / max_red bound the per-task kept and
+ * reduced element counts (the library sizes its grid from them).
+ * workspace may be NULL when cubed_fused_workspace_bytes() returns 0. */
+int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_t* d_tasks,
+                       int64_t ntasks, int64_t max_kept, int64_t max_red,
+                       void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Workspace the call above needs (split reductions keep partial
+ * accumulators there).  Pure host function. */
+int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
+                                    int64_t max_kept, int64_t max_red);
+
+/* Fill ntasks chunks with numpy Generator(Philox(key)).random() doubles:
+ * d_out[i] (device pointers) gets counts[i] doubles from key (lo,hi)[i].
+ * All three tables are device arrays of ntasks entries. */
+int cubed_random_chunks(const int64_t* d_out_ptrs, const int64_t* d_counts,
+                        const uint64_t* d_keys /* 2*ntasks: lo,hi */,
+                        int64_t ntasks, int64_t max_count, void* stream);
+
+/* Strided N-d box copies (rechunk, merge_chunks, index).  Each box moves
+ * extent[0..ndim) elements of `itemsize` bytes from src to dst views. */
+typedef struct {
+  int64_t src_base, dst_base;      /* device byte addresses                 */
+  int64_t extent[CUBED_MAX_DIMS];  /* innermost last; unused dims = 1       */
+  int64_t src_stride[CUBED_MAX_DIMS];
+  int64_t dst_stride[CUBED_MAX_DIMS];
+} cubed_box_t;
+
+/* path: CUBED_COPY_ROWS   -- innermost dim contiguous on both sides; rows are
+ *                            moved with lane_bytes-wide lanes (16/8/4/1, must
+ *                            divide every row's byte count and offset);
+ *                            work = max rows per box, row_bytes = max row size
+ *       CUBED_COPY_ELEMS  -- any strides, element at a time; work = max elems
+ *       CUBED_COPY_TILE   -- 2-d boxes, src contiguous along dim 1 and dst
+ *                            along dim 0 (64x64 LDS tile); work = tiles/box */
+#define CUBED_COPY_ROWS 0
+#define CUBED_COPY_ELEMS 1
+#define CUBED_COPY_TILE 2
+int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int32_t ndim,
+                     int32_t itemsize, int32_t path, int32_t lane_bytes,
+                     int64_t work, int64_t row_bytes, void* stream);
+
+/* Batched chunk GEMM on MFMA: for each task t, C_t = A_t @ B_t (+ C_t when
+ * accumulate) with row-major views (lda/ldb/ldc in elements).  dtype is
+ * CUBED_F32 (f32-input MFMA, exact f32 products), CUBED_BF16 (bf16 inputs,
+ * f32 accumulate/out) or CUBED_F64 (f64 vector FMA). */
+typedef struct {
+  int64_t a, b, c;        /* device byte addresses                          */
+  int64_t m, n, k;
+  int64_t lda, ldb, ldc;
+  int64_t accumulate;     /* 1: C += A@B, 0: C = A@B                         */
+} cubed_gemm_task_t;
+
+int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntasks,
+                      int32_t dtype, int64_t max_m, int64_t max_n,
+                      void* stream);
+
+/* library info */
+int cubed_abi_version(void);
+const char* cubed_last_error(void);
+int cubed_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CUBED_AMD_H */
