@@ -1,0 +1,284 @@
+"""Reduction-chain fusion (an executor-side optimization of the plan).
+
+The reference runs a reduction as separate pipelines: the per-chunk reduce
+(``blockwise(func, keepdims=True)``, core/ops.py:838-847), then rounds of
+merge_chunks + combine (:849-889) and the aggregate (:891-892), every round
+writing and re-reading its partials through storage.  On the MI355X all of
+those rounds read/write HBM for nothing: this pass recognises such a chain in
+the finalized DAG and lowers it to ONE fused-kernel launch that reads the
+chain's inputs once and writes only the final output.
+
+Legality: the rounds only regroup partials of associative per-field reductions
+(sum of sums, sum of counts, max of maxes, ...), so the single pass computes
+the same fields with a different summation order (within the fp tolerances of
+DESIGN.md; integer/count/max/min fields are bit-exact).  The chain's
+intermediate arrays must be consumed only by the next round and must not be
+requested outputs.  Task bookkeeping (TaskEndEvents per original pipeline) is
+unchanged.
+
+Layout: the fused task for final output block K iterates the first
+pipeline's space plus one "chunk" dim per reduced axis; each leaf's stride
+along that dim is derived from the first pipeline's own per-task views and
+checked to be affine in the chunk index (else the chain is not fused).
+"""
+
+from __future__ import annotations
+
+import itertools
+import math
+from dataclasses import dataclass, replace
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from . import ir
+from .lowering import (
+    LEAF_ARRAY,
+    LEAF_IOTA,
+    LoweringError,
+    TaskRow,
+    chunk_view,
+    region_chunk_keys,
+)
+from .primitive.blockwise import apply_blockwise
+from .storage import DeviceArray
+
+# (initial rop, combine rop) -> rop of the single pass
+COMPOSE = {
+    ("sum", "sum"): "sum", ("sum", "nansum"): "sum", ("nansum", "nansum"): "nansum",
+    ("nansum", "sum"): "nansum", ("count", "sum"): "count", ("count", "nansum"): "count",
+    ("count_nonnan", "sum"): "count_nonnan", ("count_nonnan", "nansum"): "count_nonnan",
+    ("max", "max"): "max", ("min", "min"): "min", ("prod", "prod"): "prod",
+    ("nanmax", "nanmax"): "nanmax", ("nanmin", "nanmin"): "nanmin",
+    ("nanprod", "nanprod"): "nanprod", ("any", "any"): "any", ("all", "all"): "all",
+}
+
+
+@dataclass
+class Chain:
+    nodes: List[str]          # op nodes, first = per-chunk reduce
+    program: ir.ExprProgram   # composite program over the first node's leaves
+    first_spec: object        # BlockwiseSpec of the first node
+    first_target: DeviceArray
+    final_spec: object
+    final_target: DeviceArray
+    levels: List[Tuple[object, object]]  # (spec, program) of each combine node
+
+
+def _reduce_leaf(f: ir.ReduceField):
+    e = f.expr
+    if isinstance(e, (ir.Region, ir.Arg)):
+        return e
+    return None
+
+
+def _field_map(p: ir.ExprProgram) -> Dict[Optional[str], ir.ReduceField]:
+    """Output name -> reduced field producing it (outputs must be bare Fields)."""
+    out = {}
+    fields = {f.name: f for f in p.reduce.fields}
+    for name, e in p.output_items():
+        if not isinstance(e, ir.Field):
+            return None
+        out[name] = fields[e.name]
+    return out
+
+
+def find_chains(dag, array_names) -> Dict[str, Chain]:
+    """{first node name: Chain} for every fusable reduction chain."""
+    nodes = dict(dag.nodes(data=True))
+    requested = set(array_names or ())
+    chains = {}
+    claimed = set()
+    for n in dag.nodes():
+        d = nodes[n]
+        if n in claimed or "pipeline" not in d or d["pipeline"].function is not apply_blockwise:
+            continue
+        p1 = d["pipeline"].config.function
+        if not isinstance(p1, ir.ExprProgram) or p1.reduce is None:
+            continue
+        if any(isinstance(l, ir.Region) for f in p1.reduce.fields for l in ir.leaves(f.expr)):
+            continue
+        fmap = _field_map(p1)
+        if fmap is None:
+            continue
+        # composite fields: output name of the current level -> (rop, expr, dtype)
+        comp = {name: (f.rop, f.expr, f.dtype) for name, f in fmap.items()}
+        cur = n
+        members = [n]
+        levels = []
+        final_prog = None
+        while True:
+            outs = list(dag.successors(cur))
+            if len(outs) != 1:
+                break
+            arr = outs[0]
+            if arr in requested or dag.out_degree(arr) != 1:
+                break
+            nxt = next(iter(dag.successors(arr)))
+            nd = nodes[nxt]
+            if "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
+                break
+            p2 = nd["pipeline"].config.function
+            if not isinstance(p2, ir.ExprProgram) or p2.reduce is None:
+                break
+            if tuple(p2.reduce.axes) != tuple(p1.reduce.axes) or p2.ndim != p1.ndim:
+                break
+            target = nodes[arr].get("target")
+            ok = True
+            newcomp = {}
+            fields2 = {}
+            for f in p2.reduce.fields:
+                leaf = _reduce_leaf(f)
+                if not isinstance(leaf, ir.Region) or leaf.target is not target:
+                    ok = False
+                    break
+                src = comp.get(leaf.field) if leaf.field is not None else comp.get(None)
+                if src is None:
+                    ok = False
+                    break
+                rop = COMPOSE.get((src[0], f.rop))
+                if rop is None:
+                    ok = False
+                    break
+                fields2[f.name] = (rop, src[1], f.dtype)
+            if not ok:
+                break
+            members.append(nxt)
+            levels.append((nd["pipeline"].config, p2))
+            final_prog = p2
+            fm2 = _field_map(p2)
+            # next level sees p2's outputs; if p2 has an epilogue the chain ends here
+            if fm2 is None:
+                comp = None
+                break
+            comp = {name: fields2[f.name] for name, f in fm2.items()}
+            cur = nxt
+        if len(members) < 2:
+            continue
+        # composite program: p1's leaves, composed fields, final outputs
+        comp_final = _compose_fields(p1, [lv[1] for lv in levels])
+        if comp_final is None:
+            continue
+        rfields = tuple(ir.ReduceField(name, rop, expr, dt) for name, (rop, expr, dt) in comp_final.items())
+        program = ir.ExprProgram(ndim=p1.ndim, nargs=p1.nargs, outputs=final_prog.outputs,
+                                 out_axes=final_prog.out_axes,
+                                 reduce=ir.ReduceStage(p1.reduce.axes, rfields),
+                                 name=f"chain({p1.name}x{len(members)})")
+        first_cfg = d["pipeline"].config
+        final_node = nodes[members[-1]]
+        chains[n] = Chain(members, program, first_cfg, first_cfg.write.array,
+                          final_node["pipeline"].config, final_node["pipeline"].config.write.array,
+                          levels)
+        claimed.update(members)
+    return chains
+
+
+def _compose_fields(p1, combine_programs):
+    """Field name of the last level -> (rop, expr over p1's leaves, dtype)."""
+    fmap = _field_map(p1)
+    comp = {name: (f.rop, f.expr, f.dtype) for name, f in fmap.items()}
+    result = None
+    for k, p2 in enumerate(combine_programs):
+        fields2 = {}
+        for f in p2.reduce.fields:
+            leaf = _reduce_leaf(f)
+            src = comp.get(leaf.field) if leaf.field is not None else comp.get(None)
+            if src is None:
+                return None
+            rop = COMPOSE.get((src[0], f.rop))
+            if rop is None:
+                return None
+            fields2[f.name] = (rop, src[1], f.dtype)
+        result = fields2
+        fm2 = _field_map(p2)
+        if fm2 is None:
+            break
+        comp = {name: fields2[f.name] for name, f in fm2.items()}
+    return result
+
+
+def contributing_keys(chain: Chain, final_key) -> List[Tuple[int, ...]]:
+    """First-node task keys feeding one final output block, by walking the
+    merge regions of the combine levels backwards."""
+    keys = [tuple(final_key)]
+    for cfg, prog in reversed(chain.levels):
+        nxt = []
+        leaf = _reduce_leaf(prog.reduce.fields[0])
+        for k in keys:
+            args = cfg.block_function(("out",) + k)
+            block_id = tuple(args[leaf.block_arg][1:])
+            region = leaf.region(block_id)
+            ck = region_chunk_keys(leaf.target, region)
+            if ck is None:
+                raise LoweringError("combine region is not made of whole chunks")
+            nxt += [c[1:] for c in ck]
+        keys = nxt
+    return sorted(set(keys))
+
+
+def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys) -> Tuple[List[TaskRow], set]:
+    """Fused task rows (space = [one chunk dim per reduced axis] + first
+    node's dims) and the reduced dim set."""
+    p1 = chain.first_spec.function
+    axes = tuple(chain.program.reduce.axes)
+    na = len(axes)
+    n = chain.program.ndim
+    red = set(range(na)) | {na + a for a in axes}
+    rows = []
+    final = chain.final_target
+    outs = chain.program.output_items()
+    for K in final_keys:
+        tkeys = contributing_keys(chain, K)
+        layouts = {}
+        for t in tkeys:
+            layouts[t] = lowerer.task_layout(p1, chain.first_spec, chain.first_target, t, leaves,
+                                             [], p1.structured, [])
+        t0 = tkeys[0]
+        r0 = layouts[t0]
+        for t in tkeys:
+            r = layouts[t]
+            if r.extent != r0.extent or r.lstrides != r0.lstrides:
+                raise LoweringError("chain tasks are not uniform (edge chunk along the reduced axis)")
+        coords = {a: sorted({t[a] for t in tkeys}) for a in axes}
+        nq = [len(coords[a]) for a in axes]
+        if math.prod(nq) != len(tkeys):
+            raise LoweringError("chain tasks do not form a grid")
+        # per-leaf chunk-dim strides from neighbours, verified for every task
+        qstr = []
+        for l, kind in enumerate(kinds):
+            isz = np.dtype(leaves[l].dtype).itemsize if kind == LEAF_ARRAY else 1
+            s_l = []
+            for i, a in enumerate(axes):
+                if nq[i] == 1:
+                    s_l.append(0)
+                    continue
+                t1 = tuple(coords[a][1] if d == a else t0[d] for d in range(len(t0)))
+                diff = layouts[t1].bases[l] - r0.bases[l]
+                if diff % isz:
+                    raise LoweringError("chunk stride is not a whole number of elements")
+                s_l.append(diff // isz)
+            for t in tkeys:
+                pos = [coords[a].index(t[a]) for a in axes]
+                exp = r0.bases[l] + sum(p * s * isz for p, s in zip(pos, s_l))
+                if layouts[t].bases[l] != exp:
+                    raise LoweringError("leaf chunks are not at an affine stride")
+            qstr.append(s_l)
+        # output: the final target chunk K, mapped through the final out_axes
+        extent = nq + list(r0.extent)
+        lstrides = [qs + list(st) for qs, st in zip(qstr, r0.lstrides)]
+        ostr, obases = [], []
+        for name, _ in outs:
+            fname = name if chain.program.structured else None
+            v = chunk_view(final, K, fname) if final.ndim else None
+            st = [0] * (na + n)
+            if v is not None:
+                for j, s in enumerate(chain.program.out_axes):
+                    if s is not None and j < len(v.stride) and s not in axes:
+                        st[na + s] = v.stride[j] if extent[na + s] != 1 else 0
+                obases.append(v.base)
+            else:
+                obases.append(final.chunk_addr((), fname))
+            ostr.append(st)
+        rows.append(TaskRow(extent, list(r0.bases), lstrides, obases, ostr,
+                            r0.key_lo, r0.key_hi, r0.block_offset))
+    return rows, red

@@ -13,6 +13,21 @@
 
 #define CUBED_DEV __device__ __forceinline__
 
+// Device addresses arrive as int64 in the task tables; casting them to
+// address_space(1) pointers makes the compiler emit global_load/store
+// (SGPR base + offset addressing) instead of flat accesses.
+#define CUBED_G __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef int64_t i64x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+CUBED_DEV const CUBED_G T* gload_ptr(const char* p) { return (const CUBED_G T*)(uintptr_t)p; }
+template <typename T>
+CUBED_DEV CUBED_G T* gstore_ptr(char* p) { return (CUBED_G T*)(uintptr_t)p; }
+
 namespace cubed {
 
 static constexpr int kBlock = 256;  // 4 waves of 64
@@ -31,23 +46,33 @@ __host__ __device__ inline int dt_size(int dt) {
 }
 
 // ---------------------------------------------------------------- scalar I/O
+CUBED_DEV float bf16_to_f32(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// float -> bfloat16, round to nearest even (NaN stays a quiet NaN)
+CUBED_DEV uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
 // Read one element of dtype dt at p and convert to V.
 template <typename V>
 CUBED_DEV V ld1(const char* p, int dt) {
   switch (dt) {
-    case CUBED_BOOL: return (V)(*(const uint8_t*)p != 0);
-    case CUBED_I8: return (V)(*(const int8_t*)p);
-    case CUBED_I16: return (V)(*(const int16_t*)p);
-    case CUBED_I32: return (V)(*(const int32_t*)p);
-    case CUBED_I64: return (V)(*(const int64_t*)p);
-    case CUBED_U8: return (V)(*(const uint8_t*)p);
-    case CUBED_U16: return (V)(*(const uint16_t*)p);
-    case CUBED_U32: return (V)(*(const uint32_t*)p);
-    case CUBED_U64: return (V)(*(const uint64_t*)p);
-    case CUBED_F32: return (V)(*(const float*)p);
-    case CUBED_F64: return (V)(*(const double*)p);
-    case CUBED_F16: return (V)(float)(*(const __half*)p);
-    case CUBED_BF16: return (V)(float)(*(const __hip_bfloat16*)p);
+    case CUBED_BOOL: return (V)(*gload_ptr<uint8_t>(p) != 0);
+    case CUBED_I8: return (V)(*gload_ptr<int8_t>(p));
+    case CUBED_I16: return (V)(*gload_ptr<int16_t>(p));
+    case CUBED_I32: return (V)(*gload_ptr<int32_t>(p));
+    case CUBED_I64: return (V)(*gload_ptr<int64_t>(p));
+    case CUBED_U8: return (V)(*gload_ptr<uint8_t>(p));
+    case CUBED_U16: return (V)(*gload_ptr<uint16_t>(p));
+    case CUBED_U32: return (V)(*gload_ptr<uint32_t>(p));
+    case CUBED_U64: return (V)(*gload_ptr<uint64_t>(p));
+    case CUBED_F32: return (V)(*gload_ptr<float>(p));
+    case CUBED_F64: return (V)(*gload_ptr<double>(p));
+    case CUBED_F16: return (V)(float)(*gload_ptr<_Float16>(p));
+    case CUBED_BF16: return (V)bf16_to_f32(*gload_ptr<uint16_t>(p));
   }
   return (V)0;
 }
@@ -69,24 +94,24 @@ CUBED_DEV int64_t to_i64(V x) {
 template <typename V>
 CUBED_DEV void st1(char* p, int dt, V v) {
   switch (dt) {
-    case CUBED_BOOL: *(uint8_t*)p = (v != (V)0) ? 1 : 0; return;
-    case CUBED_I8: *(int8_t*)p = (int8_t)to_i64(v); return;
-    case CUBED_I16: *(int16_t*)p = (int16_t)to_i64(v); return;
-    case CUBED_I32: *(int32_t*)p = (int32_t)to_i64(v); return;
-    case CUBED_I64: *(int64_t*)p = to_i64(v); return;
-    case CUBED_U8: *(uint8_t*)p = (uint8_t)to_i64(v); return;
-    case CUBED_U16: *(uint16_t*)p = (uint16_t)to_i64(v); return;
-    case CUBED_U32: *(uint32_t*)p = (uint32_t)to_i64(v); return;
+    case CUBED_BOOL: *gstore_ptr<uint8_t>(p) = (v != (V)0) ? 1 : 0; return;
+    case CUBED_I8: *gstore_ptr<int8_t>(p) = (int8_t)to_i64(v); return;
+    case CUBED_I16: *gstore_ptr<int16_t>(p) = (int16_t)to_i64(v); return;
+    case CUBED_I32: *gstore_ptr<int32_t>(p) = (int32_t)to_i64(v); return;
+    case CUBED_I64: *gstore_ptr<int64_t>(p) = to_i64(v); return;
+    case CUBED_U8: *gstore_ptr<uint8_t>(p) = (uint8_t)to_i64(v); return;
+    case CUBED_U16: *gstore_ptr<uint16_t>(p) = (uint16_t)to_i64(v); return;
+    case CUBED_U32: *gstore_ptr<uint32_t>(p) = (uint32_t)to_i64(v); return;
     case CUBED_U64:
-      if constexpr (std::is_same<V, int64_t>::value) *(uint64_t*)p = (uint64_t)v;
-      else *(uint64_t*)p = ((double)v >= 9223372036854775808.0)
+      if constexpr (std::is_same<V, int64_t>::value) *gstore_ptr<uint64_t>(p) = (uint64_t)v;
+      else *gstore_ptr<uint64_t>(p) = ((double)v >= 9223372036854775808.0)
                                ? (uint64_t)((double)v)
                                : (uint64_t)to_i64(v);
       return;
-    case CUBED_F32: *(float*)p = (float)v; return;
-    case CUBED_F64: *(double*)p = (double)v; return;
-    case CUBED_F16: *(__half*)p = __half((float)v); return;
-    case CUBED_BF16: *(__hip_bfloat16*)p = __hip_bfloat16((float)v); return;
+    case CUBED_F32: *gstore_ptr<float>(p) = (float)v; return;
+    case CUBED_F64: *gstore_ptr<double>(p) = (double)v; return;
+    case CUBED_F16: *gstore_ptr<_Float16>(p) = (_Float16)v; return;
+    case CUBED_BF16: *gstore_ptr<uint16_t>(p) = f32_to_bf16((float)v); return;
   }
 }
 
@@ -101,25 +126,25 @@ CUBED_DEV void ldv(V (&o)[VEC], const char* base, int64_t off, int dt) {
     static_assert(VEC == 4, "VEC is 1 or 4");
     switch (dt) {
       case CUBED_F32: {
-        float4 v = *(const float4*)(base + off * 4);
+        f32x4 v = *gload_ptr<f32x4>(base + off * 4);
         o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
       }
       case CUBED_F64: {
-        const double2* q = (const double2*)(base + off * 8);
-        double2 a = q[0], b = q[1];
+        const CUBED_G f64x2* q = gload_ptr<f64x2>(base + off * 8);
+        f64x2 a = q[0], b = q[1];
         o[0] = (V)a.x; o[1] = (V)a.y; o[2] = (V)b.x; o[3] = (V)b.y; return;
       }
       case CUBED_I32: {
-        int4 v = *(const int4*)(base + off * 4);
+        i32x4 v = *gload_ptr<i32x4>(base + off * 4);
         o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
       }
       case CUBED_U32: {
-        uint4 v = *(const uint4*)(base + off * 4);
+        u32x4 v = *gload_ptr<u32x4>(base + off * 4);
         o[0] = (V)v.x; o[1] = (V)v.y; o[2] = (V)v.z; o[3] = (V)v.w; return;
       }
       case CUBED_I64: case CUBED_U64: {
-        const longlong2* q = (const longlong2*)(base + off * 8);
-        longlong2 a = q[0], b = q[1];
+        const CUBED_G i64x2* q = gload_ptr<i64x2>(base + off * 8);
+        i64x2 a = q[0], b = q[1];
         if (dt == CUBED_I64) { o[0] = (V)a.x; o[1] = (V)a.y; o[2] = (V)b.x; o[3] = (V)b.y; }
         else { o[0] = (V)(uint64_t)a.x; o[1] = (V)(uint64_t)a.y; o[2] = (V)(uint64_t)b.x; o[3] = (V)(uint64_t)b.y; }
         return;
@@ -141,12 +166,12 @@ CUBED_DEV void stv(char* base, int64_t off, int dt, const V (&v)[VEC]) {
   } else {
     switch (dt) {
       case CUBED_F32: {
-        float4 w; w.x = (float)v[0]; w.y = (float)v[1]; w.z = (float)v[2]; w.w = (float)v[3];
-        *(float4*)(base + off * 4) = w; return;
+        f32x4 w; w.x = (float)v[0]; w.y = (float)v[1]; w.z = (float)v[2]; w.w = (float)v[3];
+        *gstore_ptr<f32x4>(base + off * 4) = w; return;
       }
       case CUBED_F64: {
-        double2* q = (double2*)(base + off * 8);
-        double2 a, b; a.x = (double)v[0]; a.y = (double)v[1]; b.x = (double)v[2]; b.y = (double)v[3];
+        CUBED_G f64x2* q = gstore_ptr<f64x2>(base + off * 8);
+        f64x2 a, b; a.x = (double)v[0]; a.y = (double)v[1]; b.x = (double)v[2]; b.y = (double)v[3];
         q[0] = a; q[1] = b; return;
       }
       default: {
@@ -190,7 +215,9 @@ CUBED_DEV double u64_to_unit(uint64_t u) {
 CUBED_DEV double philox_at(uint64_t k0, uint64_t k1, int64_t e) {
   const uint64_t b = (uint64_t)(e >> 2) + 1ull;
   P4 r = philox4x64_10(b, b == 0 ? 1ull : 0ull, k0, k1);
-  return u64_to_unit(r.x[e & 3]);
+  const int w = (int)(e & 3);
+  const uint64_t u = w == 0 ? r.x[0] : (w == 1 ? r.x[1] : (w == 2 ? r.x[2] : r.x[3]));
+  return u64_to_unit(u);
 }
 
 // ---------------------------------------------------------------- numpy ops

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(kBlock) void k_random(const int64_t* __restrict__ o
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int64_t t = g / bpt, b = g % bpt;
   if (t >= ntasks) return;
-  double* __restrict__ out = (double*)outs[t];
+  CUBED_G double* __restrict__ out = (CUBED_G double*)(uintptr_t)outs[t];
   const int64_t n = counts[t];
   const uint64_t k0 = keys[2 * t], k1 = keys[2 * t + 1];
   const int64_t nblk = (n + 3) >> 2;
@@ -38,11 +38,11 @@ __global__ __launch_bounds__(kBlock) void k_random(const int64_t* __restrict__ o
     P4 r = philox4x64_10((uint64_t)i + 1ull, 0ull, k0, k1);
     const int64_t e = i << 2;
     if (e + 4 <= n && (((uintptr_t)(out + e)) & 15) == 0) {
-      double2 a, c;
+      f64x2 a, c;
       a.x = u64_to_unit(r.x[0]); a.y = u64_to_unit(r.x[1]);
       c.x = u64_to_unit(r.x[2]); c.y = u64_to_unit(r.x[3]);
-      ((double2*)(out + e))[0] = a;
-      ((double2*)(out + e))[1] = c;
+      ((CUBED_G f64x2*)(out + e))[0] = a;
+      ((CUBED_G f64x2*)(out + e))[1] = c;
     } else {
       for (int j = 0; j < 4 && e + j < n; ++j) out[e + j] = u64_to_unit(r.x[j]);
     }
@@ -75,8 +75,8 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restrict__ boxes,
                                                       int64_t nboxes, int32_t ndim, int32_t isz,
                                                       int64_t bpb, int64_t rows_per_block) {
-  using T = typename std::conditional<W == 16, uint4,
-            typename std::conditional<W == 8, uint2,
+  using T = typename std::conditional<W == 16, u32x4,
+            typename std::conditional<W == 8, uint64_t,
             typename std::conditional<W == 4, uint32_t, uint8_t>::type>::type>::type;
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int64_t bi = g / bpb, blk = g % bpb;
@@ -101,8 +101,8 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restr
       so += c * B->src_stride[d];
       dof += c * B->dst_stride[d];
     }
-    const T* __restrict__ src = (const T*)((const char*)B->src_base + so * isz);
-    T* __restrict__ dst = (T*)((char*)B->dst_base + dof * isz);
+    const CUBED_G T* __restrict__ src = (const CUBED_G T*)(uintptr_t)(B->src_base + so * isz);
+    CUBED_G T* __restrict__ dst = (CUBED_G T*)(uintptr_t)(B->dst_base + dof * isz);
     for (int64_t i = lane; i < nw; i += 64) dst[i] = src[i];
   }
 }
@@ -121,8 +121,8 @@ __global__ __launch_bounds__(kBlock) void k_copy_tile(const cubed_box_t* __restr
   const int64_t nt1 = (e1 + 63) / 64;
   const int64_t t0 = (ti / nt1) * 64, t1 = (ti % nt1) * 64;
   if (t0 >= e0) return;
-  const T* __restrict__ src = (const T*)B->src_base;
-  T* __restrict__ dst = (T*)B->dst_base;
+  const CUBED_G T* __restrict__ src = (const CUBED_G T*)(uintptr_t)B->src_base;
+  CUBED_G T* __restrict__ dst = (CUBED_G T*)(uintptr_t)B->dst_base;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   for (int r = ty; r < 64; r += 4) {
     const int64_t i0 = t0 + r, i1 = t1 + tx;

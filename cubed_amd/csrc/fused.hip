@@ -93,7 +93,8 @@ CUBED_DEV void accumulate(Acc (&acc)[CUBED_MAX_FIELDS][VEC], Regs<V, VEC>& regs,
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
     if (f < P.nfields) {
-      const V* src = reg_ptr(regs, P.field_src[f]);
+      V src[VEC];
+      fetch(regs, P.field_src[f], src);
       const int rop = P.field_rop[f], ai = P.field_acc[f];
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
@@ -197,10 +198,8 @@ __global__ __launch_bounds__(kBlock) void k_fused_a(
 #pragma unroll
       for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
         if (o < P.nouts) {
-          const V* src = reg_ptr(regs, P.out_src[o]);
           V X[VEC];
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) X[j] = src[j];
+          fetch(regs, P.out_src[o], X);
           stv<V, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
         }
       }

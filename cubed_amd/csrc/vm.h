@@ -37,14 +37,6 @@ template <typename V, int VEC>
 CUBED_DEV void put(Regs<V, VEC>& regs, int idx, const V (&X)[VEC]) {
   CUBED_REG_SWITCH(idx, { _Pragma("unroll") for (int j = 0; j < VEC; ++j) R[j] = X[j]; })
 }
-template <typename V, int VEC>
-CUBED_DEV V* reg_ptr(Regs<V, VEC>& regs, int idx) {
-  switch (idx) {
-    case 0: return regs.r0; case 1: return regs.r1; case 2: return regs.r2;
-    case 3: return regs.r3; case 4: return regs.r4; default: return regs.r5;
-  }
-}
-
 #define CUBED_EACH(EXPR) _Pragma("unroll") for (int j = 0; j < VEC; ++j) { const V x = X[j]; (void)x; X[j] = (EXPR); }
 #define CUBED_EACH2(EXPR) _Pragma("unroll") for (int j = 0; j < VEC; ++j) { const V x = X[j]; const V y = Y[j]; X[j] = (EXPR); }
 
@@ -66,8 +58,8 @@ CUBED_DEV V cast_val(V x, int t, int s) {
     switch (t) {
       case CUBED_F32: return (V)(float)x;
       case CUBED_F64: return x;
-      case CUBED_F16: return (V)(float)__half((float)x);
-      case CUBED_BF16: return (V)(float)__hip_bfloat16((float)x);
+      case CUBED_F16: return (V)(float)(_Float16)x;
+      case CUBED_BF16: return (V)bf16_to_f32(f32_to_bf16((float)x));
       default: break;
     }
     // integer targets: float sources truncate toward zero, then wrap

@@ -147,6 +147,21 @@ def region_pieces(arr, region) -> List[Tuple[Tuple[int, ...], List[Tuple[int, in
     return out
 
 
+def region_chunk_keys(arr: DeviceArray, region):
+    """Chunk keys of a region made of whole chunks (unit-step slices aligned
+    to chunk boundaries), else None."""
+    ranges = []
+    for d, s in enumerate(region):
+        if not isinstance(s, slice) or (s.step or 1) != 1:
+            return None
+        start, stop = s.start or 0, s.stop if s.stop is not None else arr.shape[d]
+        st = arr._starts[d]
+        if start not in st or stop not in st:
+            return None
+        ranges.append(range(st.index(start), st.index(stop)))
+    return [(arr.name,) + c for c in itertools.product(*ranges)]
+
+
 def region_view(arr: DeviceArray, region, field=None) -> Optional[ArrView]:
     """View of a region that lies inside one chunk (None otherwise)."""
     pieces = region_pieces(arr, region)
@@ -295,18 +310,39 @@ class Codegen:
         self.free = [r for r in range(nregs) if r not in self.reserved]
         self.code: List[Tuple] = []
         self.consts: List[Tuple[str, Any]] = []
-        self.cache: Dict[int, int] = {}
-        self.uses: Dict[int, int] = {}
+        self.cache: Dict[Any, int] = {}
+        self.uses: Dict[Any, int] = {}
+        self._skeys: Dict[int, Any] = {}
+        self._keep: List[Any] = []
 
     # -- helpers --------------------------------------------------------------
+    def skey(self, e):
+        """Structural key (common-subexpression identity) of an expression."""
+        k = self._skeys.get(id(e))
+        if k is not None:
+            return k
+        if isinstance(e, ir.Const):
+            k = ("const", repr(e.value), str(e.dtype))
+        elif isinstance(e, (ir.Arg, ir.Region, ir.Philox, ir.BlockOffset, ir.Iota)):
+            k = ("leaf",) + _leaf_key(e)
+        elif isinstance(e, ir.Field):
+            k = ("field", e.name)
+        else:
+            k = (type(e).__name__, getattr(e, "op", None), str(e.dtype)) + \
+                tuple(self.skey(c) for c in e.children())
+        self._skeys[id(e)] = k
+        self._keep.append(e)
+        return k
+
     def count_uses(self, exprs):
         seen = set()
 
         def walk(e):
-            self.uses[id(e)] = self.uses.get(id(e), 0) + 1
-            if id(e) in seen:
+            k = self.skey(e)
+            self.uses[k] = self.uses.get(k, 0) + 1
+            if k in seen:
                 return
-            seen.add(id(e))
+            seen.add(k)
             for c in e.children():
                 walk(c)
 
@@ -354,9 +390,9 @@ class Codegen:
     # -- expression codegen --------------------------------------------------
     def gen(self, e) -> Tuple[int, bool]:
         """Return (register, owned) holding the value of ``e``."""
-        key = id(e)
-        if key in self.leaf_regs:
-            return self.leaf_regs[key], False
+        if id(e) in self.leaf_regs:
+            return self.leaf_regs[id(e)], False
+        key = self.skey(e)
         if key in self.cache:
             return self.cache[key], False
         if isinstance(e, ir.Const):
@@ -403,8 +439,9 @@ class Codegen:
     def _finish(self, e, r, rounded=False):
         if not rounded and not self.natural(e.dtype):
             self.code.append((ir_op("CAST"), r, 0, 0, ir.dtype_code(e.dtype), ir.dtype_code(e.dtype)))
-        if self.uses.get(id(e), 0) > 1:
-            self.cache[id(e)] = r
+        k = self.skey(e)
+        if self.uses.get(k, 0) > 1:
+            self.cache[k] = r
             return r, False
         return r, True
 
@@ -573,8 +610,11 @@ class Lowerer:
             raise LoweringError(f"array {name} is not an input of this pipeline")
         return self.ctx.device_source(proxy.array)
 
-    def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys):
-        """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline."""
+    def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
+                            rows_fn=None):
+        """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
+        ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
+        per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
         outs, field_exprs = program_exprs(program)
         exprs = dedupe_leaves(outs + field_exprs)
         outs2, fields2 = exprs[:len(outs)], exprs[len(outs):]
@@ -584,7 +624,8 @@ class Lowerer:
             rfields = [ir.ReduceField(f.name, f.rop, e, f.dtype) for f, e in zip(program.reduce.fields, fields2)]
 
         # pure copies go through the box-copy kernel
-        if program.reduce is None and not program.structured and is_pure_copy(program, target.dtype):
+        if rows_fn is None and program.reduce is None and not program.structured and \
+                is_pure_copy(program, target.dtype):
             return self.lower_copy_program(program, spec, target, task_keys)
 
         pre_exprs = [e for _, e in out_items] if program.reduce is None else [f.expr for f in rfields]
@@ -707,14 +748,19 @@ class Lowerer:
             P.leaf_dtype[i] = ir.dtype_code(leaf.dtype) if P.leaf_kind[i] == LEAF_ARRAY else 0
 
         # ---- per-task views
-        red_axes = set(program.reduce.axes) if program.reduce is not None else set()
-        n = program.ndim
-        rows = []
+        kinds = [self.leaf_kind(l) for l in leaves]
         gathers = []
-        for key in task_keys:
-            rows.append(self.task_layout(program, spec, target, key, leaves, out_items,
-                                         structured_out, gathers))
-        layout = canonicalize(rows, n, red_axes, leaves, [self.leaf_kind(l) for l in leaves])
+        if rows_fn is not None:
+            rows, red_axes = rows_fn(leaves, kinds)
+            n = len(rows[0].extent)
+        else:
+            red_axes = set(program.reduce.axes) if program.reduce is not None else set()
+            n = program.ndim
+            rows = []
+            for key in task_keys:
+                rows.append(self.task_layout(program, spec, target, key, leaves, out_items,
+                                             structured_out, gathers))
+        layout = canonicalize(rows, n, red_axes, leaves, kinds)
         P.ndim = layout.ndim
         P.nred = layout.nred
         P.mode = layout.mode
@@ -843,10 +889,11 @@ class Lowerer:
             arr = self.ctx.device_source(leaf.target)
             v = region_view(arr, region, leaf.field)
             if v is None:
+                keys = region_chunk_keys(arr, region)
+                if keys is not None:
+                    v = merged_view(arr, keys, leaf.field)
+            if v is None:
                 v = self.ctx.gather_region(arr, region, leaf.field, gathers)
-            else:
-                # int-indexed dims are already extent 1
-                pass
             return LEAF_ARRAY, v
         if isinstance(leaf, ir.Philox):
             block_id = tuple(args[leaf.block_arg][1:])

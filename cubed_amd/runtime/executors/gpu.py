@@ -71,6 +71,30 @@ def gather_to_host(arr: DeviceArray) -> np.ndarray:
     return arr.to_numpy()
 
 
+class LaunchTimer:
+    """Per-launch HIP events recorded on the executor's stream (torch's
+    current stream), for bench.py's live roofline figure."""
+
+    def __init__(self):
+        self.records = []
+
+    def events(self):
+        import torch
+
+        return torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def add(self, key, ev0, ev1):
+        self.records.append((key, ev0, ev1))
+
+    def summary(self):
+        """{launch key: (count, mean ms)} after a device synchronize."""
+        out = {}
+        for key, a, b in self.records:
+            c, s = out.get(key, (0, 0.0))
+            out[key] = (c + 1, s + a.elapsed_time(b))
+        return {k: (c, s / c) for k, (c, s) in out.items()}
+
+
 class _Alloc:
     def __init__(self, ctx, targets):
         self.ctx = ctx
@@ -78,7 +102,8 @@ class _Alloc:
 
     def run(self, stream):
         for t in self.targets:
-            self.ctx.allocate(t)
+            if id(t) not in self.ctx.elided:
+                self.ctx.allocate(t)
 
 
 class _Upload:
@@ -100,7 +125,11 @@ class GpuDagExecutor(DagExecutor):
         if not torch.cuda.is_available():
             raise nat.NativeError("GpuDagExecutor needs a visible GPU (cubed_amd has no CPU path)")
         nat.lib()
-        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self._init_state(torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}"),
+                         stream, check_memory)
+
+    def _init_state(self, device, stream, check_memory):
+        self.device = device
         self._stream = stream
         self.check_memory = check_memory
         self._cache: Dict[int, tuple] = {}
@@ -108,6 +137,10 @@ class GpuDagExecutor(DagExecutor):
         self._scratch: List = []
         self.lowerer = Lowerer(self)
         self.rank, self.world = 0, 1
+        self.timing: Optional[LaunchTimer] = None
+        self.fuse_reductions = True
+        self._chains: Dict = {}
+        self.elided = set()
 
     # -- plumbing used by the lowerer ------------------------------------------
     @property
@@ -310,19 +343,91 @@ class GpuDagExecutor(DagExecutor):
         self._cache[id(pipeline)] = (weakref.ref(pipeline), launches)
         return launches
 
+    def chains_of(self, dag, array_names):
+        """Reduction chains of this DAG (cubed_amd/chains.py), cached."""
+        key = (id(dag), tuple(array_names or ()))
+        entry = self._chains.get(key)
+        if entry is not None and entry[0]() is dag:
+            return entry[1]
+        from ...chains import find_chains
+
+        chains = find_chains(dag, array_names) if self.fuse_reductions else {}
+        members = {}
+        nodes = dict(dag.nodes(data=True))
+        for first, ch in chains.items():
+            for m in ch.nodes[1:]:
+                members[m] = first
+            # partials of all but the last level are never materialised
+            for m in ch.nodes[:-1]:
+                for out in dag.successors(m):
+                    t = nodes[out].get("target")
+                    if isinstance(t, DeviceArray):
+                        self.elided.add(id(t))
+        self._chains[key] = (weakref.ref(dag), (chains, members))
+        return chains, members
+
+    def compiled_chain(self, chain):
+        entry = self._cache.get(("chain", id(chain.first_spec)))
+        if entry is not None and entry[0]() is chain.first_spec:
+            return entry[1]
+        from ...chains import chain_rows
+
+        target = chain.final_target
+        self.allocate(target)
+        keys = self._task_keys(target)
+        launch = self.lowerer.lower_expr_pipeline(
+            chain.program, chain.first_spec, target, keys,
+            rows_fn=lambda leaves, kinds: chain_rows(self.lowerer, chain, leaves, kinds, keys))
+        launches = _with_gathers(launch, self.device)
+        self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
+        return launches
+
     def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
         stream = self.stream
         nodes = dict(dag.nodes(data=True))
         if self.check_memory:
             self._check_hbm(dag)
+        timing = self.timing
+        chains, members = self.chains_of(dag, array_names)
         for name, node in visit_nodes(dag, resume=resume):
             t0 = time.time()
-            for launch in self.compiled(name, node):
-                launch.run(stream)
-            for out in dag.successors(name):
-                target = nodes[out].get("target")
-                if isinstance(target, DeviceArray):
-                    target.written = True
+            if name in members:
+                launches = []  # ran as part of its chain's fused launch
+            elif name in chains:
+                ch = chains[name]
+                if resume and ch.final_target.written:
+                    launches = []
+                else:
+                    try:
+                        launches = self.compiled_chain(ch)
+                    except LoweringError:
+                        # not fusable after all: run the chain's pipelines one by one
+                        chains.pop(name)
+                        for m in ch.nodes[1:]:
+                            members.pop(m, None)
+                        for m in ch.nodes[:-1]:
+                            for out in dag.successors(m):
+                                t = nodes[out].get("target")
+                                if isinstance(t, DeviceArray):
+                                    self.elided.discard(id(t))
+                                    self.allocate(t)
+                        launches = self.compiled(name, node)
+            else:
+                launches = self.compiled(name, node)
+            for i, launch in enumerate(launches):
+                if timing is not None:
+                    ev0, ev1 = timing.events()
+                    ev0.record()
+                    launch.run(stream)
+                    ev1.record()
+                    timing.add((name, i, type(launch).__name__), ev0, ev1)
+                else:
+                    launch.run(stream)
+            if name not in chains:  # a chain head's partials are never materialised
+                for out in dag.successors(name):
+                    target = nodes[out].get("target")
+                    if isinstance(target, DeviceArray):
+                        target.written = True
             if callbacks is not None:
                 op = node.get("primitive_op")
                 ev = TaskEndEvent(array_name=name, num_tasks=op.num_tasks if op is not None else 1,

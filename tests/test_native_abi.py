@@ -1,0 +1,120 @@
+"""The C-ABI library (include/cubed_amd.h) loads and matches its header (CPU).
+
+No compute entry point is called here (there is no GPU in the build
+container); the struct layouts the host writes into the task tables are
+checked against the C compiler's view of the header, and every function the
+header declares must be exported by libcubed_amd.so.
+"""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "cubed_amd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    return sorted(set(re.findall(r"\b(cubed_\w+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    fns = header_functions()
+    for f in ("cubed_fused_chunks", "cubed_copy_boxes", "cubed_random_chunks", "cubed_gemm_chunks"):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol(built):
+    from cubed_amd import _native as nat
+
+    lib = ctypes.CDLL(nat.LIB_PATH)
+    for f in header_functions():
+        assert hasattr(lib, f), f"{f} declared in include/cubed_amd.h but not exported"
+    assert set(nat.EXPORTED_SYMBOLS) <= set(header_functions())
+
+
+def test_library_loads_through_binding(built):
+    from cubed_amd import _native as nat
+
+    L = nat.lib()
+    assert L.cubed_abi_version() == 1
+
+
+def test_workspace_query_is_host_only(built):
+    """cubed_fused_workspace_bytes is pure host logic: callable without a GPU."""
+    from cubed_amd import _native as nat
+
+    P = nat.Program()
+    P.ndim, P.nred, P.mode, P.nleaves, P.nfields, P.nouts = 2, 1, 0, 1, 1, 1
+    n = nat.lib().cubed_fused_workspace_bytes(ctypes.byref(P), 1, 1 << 20, 1 << 12)
+    assert n >= 0
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "cubed_amd.h"
+#define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F))
+#define S(T) printf(#T " %zu\n", sizeof(T))
+int main(void) {
+  S(cubed_insn_t); S(cubed_program_t); S(cubed_task_t); S(cubed_box_t); S(cubed_gemm_task_t);
+  P(cubed_program_t, insns); P(cubed_program_t, epi); P(cubed_program_t, consts);
+  P(cubed_program_t, leaf_kind); P(cubed_program_t, out_dtype); P(cubed_program_t, ninsns);
+  P(cubed_task_t, leaf_base); P(cubed_task_t, leaf_stride); P(cubed_task_t, out_base);
+  P(cubed_task_t, out_stride); P(cubed_task_t, key_lo); P(cubed_task_t, block_offset);
+  P(cubed_box_t, src_stride); P(cubed_box_t, dst_stride);
+  P(cubed_gemm_task_t, ldc); P(cubed_gemm_task_t, accumulate);
+  return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def c_layout(tmp_path_factory):
+    d = tmp_path_factory.mktemp("abi")
+    src = d / "layout.c"
+    src.write_text(LAYOUT_C)
+    exe = d / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    return {k: int(v) for k, v in (line.split() for line in out.splitlines())}
+
+
+def test_header_is_plain_c(c_layout):
+    assert c_layout["cubed_task_t"] > 0
+
+
+def test_struct_layouts_match_binding(c_layout):
+    from cubed_amd import _native as nat
+
+    assert ctypes.sizeof(nat.Insn) == c_layout["cubed_insn_t"]
+    assert ctypes.sizeof(nat.Program) == c_layout["cubed_program_t"]
+    for f in ("insns", "epi", "consts", "leaf_kind", "out_dtype", "ninsns"):
+        assert getattr(nat.Program, f).offset == c_layout[f"cubed_program_t.{f}"], f
+    assert nat.TASK_DTYPE.itemsize == c_layout["cubed_task_t"]
+    for f in ("leaf_base", "leaf_stride", "out_base", "out_stride", "key_lo", "block_offset"):
+        assert nat.TASK_DTYPE.fields[f][1] == c_layout[f"cubed_task_t.{f}"], f
+    assert nat.BOX_DTYPE.itemsize == c_layout["cubed_box_t"]
+    for f in ("src_stride", "dst_stride"):
+        assert nat.BOX_DTYPE.fields[f][1] == c_layout[f"cubed_box_t.{f}"], f
+    assert nat.GEMM_DTYPE.itemsize == c_layout["cubed_gemm_task_t"]
+    for f in ("ldc", "accumulate"):
+        assert nat.GEMM_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_task_t.{f}"], f
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: a missing extension is an error, not a silent path."""
+    from cubed_amd import _native as nat
+
+    monkeypatch.setattr(nat, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(nat, "_lib", None)
+    with pytest.raises(nat.NativeError):
+        nat.lib()
