@@ -37,6 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
+ABI_VERSION = 2  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -112,7 +113,7 @@ def lib():
             f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()); "
             "cubed_amd has no CPU fallback")
     L = ctypes.CDLL(LIB_PATH)
-    L.cubed_fused_chunks.argtypes = [POINTER(Program), c_void_p, c_int64, c_int64, c_int64,
+    L.cubed_fused_chunks.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_int64,
                                      c_void_p, c_int64, c_void_p]
     L.cubed_fused_chunks.restype = c_int
     L.cubed_fused_workspace_bytes.argtypes = [POINTER(Program), c_int64, c_int64, c_int64]
@@ -127,7 +128,7 @@ def lib():
     L.cubed_abi_version.restype = c_int
     L.cubed_last_error.restype = c_char_p
     L.cubed_device_count.restype = c_int
-    if L.cubed_abi_version() != 1:
+    if L.cubed_abi_version() != ABI_VERSION:
         raise NativeError("libcubed_amd.so ABI version mismatch; rebuild it")
     _lib = L
     return L

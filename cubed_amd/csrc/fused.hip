@@ -17,7 +17,7 @@
 //   split: when a launch would not fill 256 CUs, the reduced range is split
 //      over workgroups that write partial accumulators to the workspace;
 //      k_finalize combines them in split order and runs the epilogue.
-#include "vm.h"
+#include "fused_common.h"
 #include <stdio.h>
 #include <string.h>
 
@@ -25,15 +25,6 @@ namespace cubed {
 
 thread_local char g_err[512];
 static void set_err(const char* m) { snprintf(g_err, sizeof(g_err), "%s", m); }
-
-CUBED_DEV void divmod64(int64_t a, int64_t b, int64_t& q, int64_t& r) {
-  if (((uint64_t)a | (uint64_t)b) < 0x100000000ull) {
-    const uint32_t qa = (uint32_t)a / (uint32_t)b;
-    q = qa; r = a - (int64_t)qa * b;
-  } else {
-    q = a / b; r = a - q * b;
-  }
-}
 
 // Load leaf l (VEC elements) at element offset `off`; `inner` is the leaf's
 // stride along the dim the VEC elements run on (0 = broadcast, 1 = packed).
@@ -87,74 +78,12 @@ CUBED_DEV void load_leaves(Regs<V, VEC>& regs, const cubed_program_t& P,
   if (nl > 3) load_leaf<V, VEC>(regs.r3, P, T, 3, off[3], inner[3]);
 }
 
-template <typename V, int VEC>
-CUBED_DEV void accumulate(Acc (&acc)[CUBED_MAX_FIELDS][VEC], Regs<V, VEC>& regs,
-                          const cubed_program_t& P) {
-#pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    if (f < P.nfields) {
-      V src[VEC];
-      fetch(regs, P.field_src[f], src);
-      const int rop = P.field_rop[f], ai = P.field_acc[f];
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
-    }
-  }
-}
-
-// Epilogue + store of VEC reduced elements.
-template <int VEC>
-CUBED_DEV void finish(const cubed_program_t& P, const cubed_task_t* T,
-                      const Acc (&acc)[CUBED_MAX_FIELDS][VEC],
-                      const int64_t (&ooff)[CUBED_MAX_OUTS]) {
-  if (P.nepi >= 0) {
-    Regs<double, VEC> er;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) { er.r0[j] = 0; er.r1[j] = 0; er.r2[j] = 0; er.r3[j] = 0; er.r4[j] = 0; er.r5[j] = 0; }
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-      if (f < P.nfields) {
-        double X[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) X[j] = P.field_acc[f] ? (double)acc[f][j].i : acc[f][j].f;
-        put(er, f, X);
-      }
-    }
-    run_vm<double, VEC>(er, P.epi, P.nepi, P);
-#pragma unroll
-    for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
-      if (o < P.nouts) {
-        double X[VEC];
-        fetch(er, P.out_src[o], X);
-        stv<double, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
-      if (o < P.nouts) {
-        const int f = P.out_src[o];
-        if (P.field_acc[f]) {
-          int64_t X[VEC];
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) X[j] = acc[f][j].i;
-          stv<int64_t, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
-        } else {
-          double X[VEC];
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) X[j] = acc[f][j].f;
-          stv<double, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
-        }
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ kernel A
 template <typename V, int VEC>
 __global__ __launch_bounds__(kBlock) void k_fused_a(
-    const cubed_program_t P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
+  const cubed_program_t& P = *Pd;
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int64_t b = g % bpt;
   const int64_t rest = g / bpt;
@@ -269,8 +198,9 @@ __global__ __launch_bounds__(kBlock) void k_fused_a(
 // ------------------------------------------------------------------ kernel B
 template <typename V, int VEC>
 __global__ __launch_bounds__(kBlock) void k_fused_b(
-    const cubed_program_t P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, int32_t nsplit, Acc* __restrict__ ws) {
+  const cubed_program_t& P = *Pd;
   __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int s = (int)(g % nsplit);
@@ -376,8 +306,9 @@ __global__ __launch_bounds__(kBlock) void k_fused_b(
 // Combine nsplit partial accumulators (in split order) for every kept
 // element and run the epilogue.  kept dims are [kd0, kd1) of the task.
 __global__ __launch_bounds__(kBlock) void k_finalize(
-    const cubed_program_t P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, int kd0, int kd1) {
+  const cubed_program_t& P = *Pd;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t t = i / max_kept, k = i % max_kept;
   if (t >= ntasks) return;
@@ -403,16 +334,6 @@ __global__ __launch_bounds__(kBlock) void k_finalize(
   }
   finish<1>(P, T, fin, ooff);
 }
-
-// ---------------------------------------------------------------- launch plan
-struct LaunchPlan {
-  int kernel;     // 0 = A, 1 = B
-  int vec;        // 1 or 4
-  int64_t bpt;    // A: blocks per task per split
-  int32_t nsplit;
-  int64_t ws_bytes;
-  int64_t blocks;
-};
 
 static LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red) {
@@ -449,26 +370,28 @@ static LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t 
   return L;
 }
 
-static dim3 grid_of(int64_t blocks) {
+dim3 grid_of(int64_t blocks) {
   if (blocks <= 0x7fffffff) return dim3((unsigned)blocks, 1, 1);
   const int64_t y = (blocks + 0x7fffffff - 1) / 0x7fffffff;
   return dim3(0x7fffffffu, (unsigned)y, 1);
 }
 
 template <typename V>
-static void launch_fused(const cubed_program_t& P, const LaunchPlan& L, const cubed_task_t* d_tasks,
+static void launch_fused(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L, const cubed_task_t* d_tasks,
                          int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
   const dim3 grid = grid_of(L.blocks);
-  if (L.kernel == 0) {
+  if (P.mode & CUBED_MODE_STREAM) {
+    launch_stream<V>(P, dP, L, d_tasks, ntasks, max_kept, ws, st);
+  } else if (L.kernel == 0) {
     if (L.vec == 4)
-      hipLaunchKernelGGL((k_fused_a<V, 4>), grid, dim3(kBlock), 0, st, P, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept);
+      hipLaunchKernelGGL((k_fused_a<V, 4>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept);
     else
-      hipLaunchKernelGGL((k_fused_a<V, 1>), grid, dim3(kBlock), 0, st, P, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept);
+      hipLaunchKernelGGL((k_fused_a<V, 1>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept);
   } else {
     if (L.vec == 4)
-      hipLaunchKernelGGL((k_fused_b<V, 4>), grid, dim3(kBlock), 0, st, P, d_tasks, ntasks, max_kept, L.nsplit, ws);
+      hipLaunchKernelGGL((k_fused_b<V, 4>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, max_kept, L.nsplit, ws);
     else
-      hipLaunchKernelGGL((k_fused_b<V, 1>), grid, dim3(kBlock), 0, st, P, d_tasks, ntasks, max_kept, L.nsplit, ws);
+      hipLaunchKernelGGL((k_fused_b<V, 1>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, max_kept, L.nsplit, ws);
   }
 }
 
@@ -482,10 +405,11 @@ extern "C" int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int6
   return plan_launch(prog, ntasks, max_kept, max_red).ws_bytes;
 }
 
-extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_t* d_tasks,
+extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                  const cubed_task_t* d_tasks,
                                   int64_t ntasks, int64_t max_kept, int64_t max_red,
                                   void* d_workspace, int64_t workspace_bytes, void* stream) {
-  if (!prog || (!d_tasks && ntasks > 0)) { set_err("cubed_fused_chunks: null argument"); return CUBED_E_ARG; }
+  if (!prog || !d_prog || (!d_tasks && ntasks > 0)) { set_err("cubed_fused_chunks: null argument"); return CUBED_E_ARG; }
   if (ntasks == 0) return 0;
   const cubed_program_t& P = *prog;
   if (P.ndim < 1 || P.ndim > CUBED_MAX_DIMS || P.nred < 0 || P.nred > P.ndim ||
@@ -496,6 +420,19 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_
     return CUBED_E_ARG;
   }
   if ((P.mode & 3) == 1 && P.nfields == 0) { set_err("cubed_fused_chunks: kernel B needs a reduction"); return CUBED_E_ARG; }
+  if ((P.mode & CUBED_MODE_STREAM) &&
+      ((P.mode & 3) != 0 || !(P.mode & 4) || P.nred > 1 || P.ndim != P.nred + 1 || P.nleaves < 1)) {
+    set_err("cubed_fused_chunks: stream mode needs kernel A, VEC=4, one kept dim and <= 1 reduced dim");
+    return CUBED_E_LAYOUT;
+  }
+  if (P.mode & CUBED_MODE_STREAM) {
+    const int want = P.vtype == CUBED_V_F32 ? CUBED_F32 : P.vtype == CUBED_V_F64 ? CUBED_F64 : CUBED_I64;
+    for (int l = 0; l < P.nleaves; ++l)
+      if (P.leaf_kind[l] != CUBED_LEAF_ARRAY || P.leaf_dtype[l] != want) {
+        set_err("cubed_fused_chunks: stream mode needs array leaves in the vtype's dtype");
+        return CUBED_E_LAYOUT;
+      }
+  }
   if (max_kept <= 0 || max_red <= 0) { set_err("cubed_fused_chunks: empty task bounds"); return CUBED_E_ARG; }
   const LaunchPlan L = plan_launch(&P, ntasks, max_kept, max_red);
   if (L.ws_bytes > 0 && (d_workspace == nullptr || workspace_bytes < L.ws_bytes)) {
@@ -505,9 +442,9 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_
   hipStream_t st = (hipStream_t)stream;
   Acc* ws = (Acc*)d_workspace;
   switch (P.vtype) {
-    case CUBED_V_F32: launch_fused<float>(P, L, d_tasks, ntasks, max_kept, ws, st); break;
-    case CUBED_V_F64: launch_fused<double>(P, L, d_tasks, ntasks, max_kept, ws, st); break;
-    case CUBED_V_I64: launch_fused<int64_t>(P, L, d_tasks, ntasks, max_kept, ws, st); break;
+    case CUBED_V_F32: launch_fused<float>(P, d_prog, L, d_tasks, ntasks, max_kept, ws, st); break;
+    case CUBED_V_F64: launch_fused<double>(P, d_prog, L, d_tasks, ntasks, max_kept, ws, st); break;
+    case CUBED_V_I64: launch_fused<int64_t>(P, d_prog, L, d_tasks, ntasks, max_kept, ws, st); break;
     default: set_err("cubed_fused_chunks: bad vtype"); return CUBED_E_DTYPE;
   }
   hipError_t e = hipGetLastError();
@@ -517,7 +454,7 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_
     const int kd1 = (L.kernel == 0) ? P.ndim : P.ndim - P.nred;
     const int64_t n = ntasks * max_kept;
     hipLaunchKernelGGL(k_finalize, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st,
-                       P, d_tasks, ntasks, max_kept, L.nsplit, (const Acc*)ws, kd0, kd1);
+                       d_prog, d_tasks, ntasks, max_kept, L.nsplit, (const Acc*)ws, kd0, kd1);
     e = hipGetLastError();
     if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   }

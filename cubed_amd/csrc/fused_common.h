@@ -1,0 +1,97 @@
+// fused_common.h -- pieces shared by the generic fused kernels (fused.hip)
+// and the streaming fast path (stream.hip).
+#pragma once
+#include "vm.h"
+
+namespace cubed {
+
+CUBED_DEV void divmod64(int64_t a, int64_t b, int64_t& q, int64_t& r) {
+  if (((uint64_t)a | (uint64_t)b) < 0x100000000ull) {
+    const uint32_t qa = (uint32_t)a / (uint32_t)b;
+    q = qa; r = a - (int64_t)qa * b;
+  } else {
+    q = a / b; r = a - q * b;
+  }
+}
+
+template <typename V, int VEC>
+CUBED_DEV void accumulate(Acc (&acc)[CUBED_MAX_FIELDS][VEC], Regs<V, VEC>& regs,
+                          const cubed_program_t& P) {
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+    if (f < P.nfields) {
+      V src[VEC];
+      fetch(regs, P.field_src[f], src);
+      const int rop = P.field_rop[f], ai = P.field_acc[f];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
+    }
+  }
+}
+
+// Epilogue + store of VEC reduced elements.
+template <int VEC>
+CUBED_DEV void finish(const cubed_program_t& P, const cubed_task_t* T,
+                      const Acc (&acc)[CUBED_MAX_FIELDS][VEC],
+                      const int64_t (&ooff)[CUBED_MAX_OUTS]) {
+  if (P.nepi >= 0) {
+    Regs<double, VEC> er;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { er.r0[j] = 0; er.r1[j] = 0; er.r2[j] = 0; er.r3[j] = 0; er.r4[j] = 0; er.r5[j] = 0; }
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+      if (f < P.nfields) {
+        double X[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) X[j] = P.field_acc[f] ? (double)acc[f][j].i : acc[f][j].f;
+        put(er, f, X);
+      }
+    }
+    run_vm<double, VEC>(er, P.epi, P.nepi, P);
+#pragma unroll
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
+      if (o < P.nouts) {
+        double X[VEC];
+        fetch(er, P.out_src[o], X);
+        stv<double, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
+      if (o < P.nouts) {
+        const int f = P.out_src[o];
+        if (P.field_acc[f]) {
+          int64_t X[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) X[j] = acc[f][j].i;
+          stv<int64_t, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+        } else {
+          double X[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) X[j] = acc[f][j].f;
+          stv<double, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launch plan
+struct LaunchPlan {
+  int kernel;     // 0 = A, 1 = B
+  int vec;        // 1 or 4
+  int64_t bpt;    // A: blocks per task per split
+  int32_t nsplit;
+  int64_t ws_bytes;
+  int64_t blocks;
+};
+
+// stream.hip: the streaming fast path (mode bit CUBED_MODE_STREAM)
+template <typename V>
+void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L, const cubed_task_t* d_tasks,
+                   int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st);
+
+dim3 grid_of(int64_t blocks);
+
+}  // namespace cubed

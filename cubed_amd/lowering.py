@@ -22,6 +22,7 @@ other multi-chunk read -- a per-task gather into a contiguous scratch buffer.
 
 from __future__ import annotations
 
+import ctypes
 import itertools
 import math
 from dataclasses import dataclass, field
@@ -249,6 +250,7 @@ class CopyLaunch:
         if not boxes:
             return
         nd, boxes = canonical_boxes(boxes)
+        self.boxes = boxes
         self.ndim = nd
         self.itemsize = itemsize
         inner_contig = all(b.sstride[-1] == 1 and b.dstride[-1] == 1 for b in boxes)
@@ -562,6 +564,9 @@ class FusedLaunch:
         import torch
 
         self.prog = prog_struct
+        raw = np.frombuffer(ctypes.string_at(ctypes.addressof(prog_struct), ctypes.sizeof(prog_struct)),
+                            dtype=np.uint8)
+        self.d_prog = torch.from_numpy(raw.copy()).to(device)  # read by the kernels
         self.table = table
         self.ntasks = ntasks
         self.max_kept = max_kept
@@ -574,7 +579,8 @@ class FusedLaunch:
         for g in self.gathers:
             g.run(stream)
         L = nat.lib()
-        nat.check(L.cubed_fused_chunks(self.prog, self.table.data_ptr(), self.ntasks, self.max_kept,
+        nat.check(L.cubed_fused_chunks(self.prog, self.d_prog.data_ptr(), self.table.data_ptr(),
+                                       self.ntasks, self.max_kept,
                                        self.max_red, self.ws.data_ptr() if self.ws is not None else None,
                                        self.ws_bytes, stream), "cubed_fused_chunks")
 
@@ -611,7 +617,7 @@ class Lowerer:
         return self.ctx.device_source(proxy.array)
 
     def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
-                            rows_fn=None):
+                            rows_fn=None, sample_key=None):
         """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
         ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
         per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
@@ -634,7 +640,7 @@ class Lowerer:
             raise LoweringError(f"fused program reads {len(leaves)} inputs (max {nat.MAX_LEAVES})")
 
         # constant-fold leaves that resolve to constants (virtual full / scalars)
-        sample_args = spec.block_function(("out",) + tuple(task_keys[0]))
+        sample_args = spec.block_function(("out",) + tuple(task_keys[0] if sample_key is None else sample_key))
         const_leaves = {}
         for leaf in leaves:
             c = self.constant_value(leaf, sample_args, spec.reads_map)
@@ -764,6 +770,8 @@ class Lowerer:
         P.ndim = layout.ndim
         P.nred = layout.nred
         P.mode = layout.mode
+        if _stream_ok(layout, leaves, kinds, P.vtype):
+            P.mode |= MODE_STREAM
         table = layout.table(self.ctx.device)
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
         return FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
@@ -1129,6 +1137,33 @@ def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout
         for r in rows2:
             r.extent = [1]
     return lay
+
+
+MODE_STREAM = 8  # include/cubed_amd.h CUBED_MODE_STREAM
+_VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64: np.dtype(np.int64)}
+
+
+def _stream_ok(layout: Layout, leaves, kinds, vtype) -> bool:
+    """Geometry of the streaming fast path (stream.hip): kernel A with VEC=4,
+    one kept kernel dim (packed in every leaf and output) after at most one
+    reduced dim, every leaf an array chunk in the VM's own dtype."""
+    if layout.mode != 4 or layout.nred > 1 or layout.ndim != layout.nred + 1 or not leaves:
+        return False
+    want = _VTYPE_DTYPE.get(vtype)
+    for l, kind in enumerate(kinds):
+        if kind != LEAF_ARRAY or np.dtype(leaves[l].dtype) != want:
+            return False
+    for r in layout.rows:
+        ext, ls, os_ = _apply_groups(r, layout.groups)
+        for l, st in enumerate(ls):
+            if st[-1] != 1 or r.bases[l] % 16:
+                return False
+            if layout.nred and ext[0] != 1 and st[0] % 4:
+                return False
+        for st in os_:
+            if st[-1] != 1:
+                return False
+    return True
 
 
 def _groups_contiguous(group, d, order):

@@ -370,14 +370,15 @@ class GpuDagExecutor(DagExecutor):
         entry = self._cache.get(("chain", id(chain.first_spec)))
         if entry is not None and entry[0]() is chain.first_spec:
             return entry[1]
-        from ...chains import chain_rows
+        from ...chains import chain_rows, contributing_keys
 
         target = chain.final_target
         self.allocate(target)
         keys = self._task_keys(target)
         launch = self.lowerer.lower_expr_pipeline(
             chain.program, chain.first_spec, target, keys,
-            rows_fn=lambda leaves, kinds: chain_rows(self.lowerer, chain, leaves, kinds, keys))
+            rows_fn=lambda leaves, kinds: chain_rows(self.lowerer, chain, leaves, kinds, keys),
+            sample_key=contributing_keys(chain, keys[0])[0])
         launches = _with_gathers(launch, self.device)
         self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
         return launches

@@ -191,7 +191,7 @@ class DeviceArray(ChunkGrid):
 
         ext = self.chunk_extent(coords)
         dt = self.field_dtype(field)
-        arr = np.ascontiguousarray(np.broadcast_to(np.asarray(value, dtype=dt), ext))
+        arr = np.array(np.broadcast_to(np.asarray(value, dtype=dt), ext), order="C", copy=True)
         raw, _ = self._slab_view(field, self.local_slot(coords), ext)
         raw.copy_(torch.from_numpy(arr.reshape(-1).view(np.uint8)))
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 1
+#define CUBED_ABI_VERSION 2
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -55,6 +55,8 @@ extern "C" {
 #define CUBED_NREGS 6      /* VM registers; leaf i is preloaded into reg i  */
 
 /* error codes (negative); positive values are hipError_t */
+#define CUBED_MODE_STREAM 8
+
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)
 #define CUBED_E_LAYOUT (-3)
@@ -132,6 +134,12 @@ typedef struct {
                                  /* or a map), 1 = B (reduced dims last);   */
                                  /* +4 when the innermost dim is packed     */
                                  /* (VEC=4 loads/stores; host-checked)      */
+                                 /* +8 (CUBED_MODE_STREAM): streaming fast  */
+                                 /* path, host-checked: kernel A, VEC=4,    */
+                                 /* ndim == nred + 1, nred <= 1, every leaf */
+                                 /* an ARRAY in the vtype's own dtype       */
+                                 /* (f32/f64/i64) with packed kept dim and  */
+                                 /* reduced strides that are multiples of 4 */
   int32_t nleaves;
   uint8_t leaf_kind[CUBED_MAX_LEAVES];
   uint8_t leaf_dtype[CUBED_MAX_LEAVES];
@@ -168,8 +176,13 @@ typedef struct {
  * All tasks share the dim structure of `prog` (ndim, nred) but may differ in
  * extents (edge chunks).  max_kept / max_red bound the per-task kept and
  * reduced element counts (the library sizes its grid from them).
+ * `prog` is read on the host (launch shape, argument checks); `d_prog` is a
+ * byte-identical copy in device memory that the kernels read through the
+ * scalar cache (a by-value kernel argument indexed by the interpreter loop
+ * would be demoted to scratch).
  * workspace may be NULL when cubed_fused_workspace_bytes() returns 0. */
-int cubed_fused_chunks(const cubed_program_t* prog, const cubed_task_t* d_tasks,
+int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                       const cubed_task_t* d_tasks,
                        int64_t ntasks, int64_t max_kept, int64_t max_red,
                        void* d_workspace, int64_t workspace_bytes, void* stream);
 

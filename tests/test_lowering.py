@@ -1,0 +1,94 @@
+"""Lowering decisions of the MI355X executor, checked on CPU (no launches).
+
+``DryExecutor`` (tests/dryrun.py) lowers plans to the exact kernel-argument
+tables the GPU path launches; these tests pin the decisions that decide
+performance: how many launches a pipeline becomes, whether the streaming
+fast path is taken, and that reduction chains are fused into one pass.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.random as crandom
+from cubed_amd import _native as nat
+from cubed_amd.core.plan import arrays_to_plan
+from cubed_amd.lowering import MODE_STREAM, CopyLaunch, FusedLaunch
+
+
+def _fused(ex):
+    return [l for l in ex.launched if isinstance(l, FusedLaunch)]
+
+
+def test_quad_means_is_one_streaming_launch(built, dry):
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(1)
+    u = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=dry, array_names=[u.name, v.name])
+    dry.launched.clear()
+    m = xp.mean(u * v, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    assert len(fused) == 1, [type(l).__name__ for l in dry.launched]
+    L = fused[0]
+    assert not L.gathers
+    P = L.prog
+    assert P.mode & MODE_STREAM and P.mode & 4
+    assert (P.ndim, P.nred, P.nleaves, P.nfields) == (2, 1, 2, 2)
+    assert L.max_red == 200 and L.max_kept == 16 * 32
+    assert P.ninsns == 2  # MOV + MUL: the product is shared by the n and total fields
+
+
+def test_chain_fusion_can_be_disabled(built, dry):
+    dry.fuse_reductions = False
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(1)
+    u = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    arrays_to_plan(u).execute(executor=dry, array_names=[u.name])
+    dry.launched.clear()
+    m = xp.mean(u, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    assert len(_fused(dry)) >= 2  # per-chunk reduce + merge/combine/aggregate rounds
+
+
+def test_elementwise_map_is_streaming(built, dry):
+    spec = cubed.Spec(allowed_mem=10**8, executor=dry)
+    a = cubed.from_array(np.arange(4096, dtype=np.float64).reshape(64, 64), chunks=(16, 64), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    b = (a + 1) * 2
+    arrays_to_plan(b).execute(executor=dry, resume=True, array_names=[b.name])
+    fused = _fused(dry)
+    assert len(fused) >= 1
+    assert fused[-1].prog.nfields == 0
+
+
+def test_rechunk_lowers_to_one_copy_launch(built, dry):
+    spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+    x = cubed.from_array(np.arange(64 * 48, dtype=np.float32).reshape(64, 48), chunks=(8, 48), spec=spec)
+    arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
+    dry.launched.clear()
+    y = x.rechunk((64, 8))
+    arrays_to_plan(y).execute(executor=dry, resume=True, array_names=[y.name])
+    copies = [l for l in dry.launched if isinstance(l, CopyLaunch)]
+    assert len(copies) == 1
+    # every target element is written exactly once
+    boxes = copies[0].boxes
+    assert sum(int(np.prod(b.extent)) for b in boxes) == 64 * 48
+
+
+def test_task_table_rows_match_tasks(built, dry):
+    spec = cubed.Spec(allowed_mem=10**8, executor=dry)
+    a = cubed.from_array(np.ones((30, 40)), chunks=(7, 9), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    s = xp.sum(a, axis=1)
+    arrays_to_plan(s).execute(executor=dry, resume=True, array_names=[s.name])
+    for L in _fused(dry):
+        tab = L.table.numpy().view(nat.TASK_DTYPE)
+        assert len(tab) == L.ntasks
+        assert (tab["extent"] >= 1).all()

@@ -44,7 +44,7 @@ def test_library_loads_through_binding(built):
     from cubed_amd import _native as nat
 
     L = nat.lib()
-    assert L.cubed_abi_version() == 1
+    assert L.cubed_abi_version() == nat.ABI_VERSION
 
 
 def test_workspace_query_is_host_only(built):

@@ -1,0 +1,190 @@
+"""Plan-level behaviour of the drop-in API (CPU only: nothing is computed).
+
+Mirrors the reference's structural tests -- task counts after fusion
+(cubed/tests/test_optimization.py), projected-memory errors
+(primitive/test_blockwise.py:139-166, test_core.py:280-285,350-355),
+rechunk op counts (primitive/test_rechunk.py:16-117), merge_chunks checks
+(test_core.py:384-398) -- against this package's plans.
+"""
+
+import numpy as np
+import pytest
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.random as crandom
+from cubed_amd.core.ops import elemwise, merge_chunks, partial_reduce, reduction, tree_reduce
+from cubed_amd.core.optimization import (
+    fuse_all_optimize_dag,
+    multiple_inputs_optimize_dag,
+    simple_optimize_dag,
+)
+from cubed_amd.core.plan import arrays_to_plan
+from cubed_amd.utils import convert_to_bytes
+
+
+@pytest.fixture()
+def spec():
+    return cubed.Spec(allowed_mem=100000)
+
+
+def test_fusion_task_counts(spec):
+    # test_optimization.py:29-53
+    a = xp.asarray([[1, 2, 3], [4, 5, 6], [7, 8, 9]], chunks=(2, 2), spec=spec)
+    b = xp.negative(a)
+    c = xp.astype(b, np.float32)
+    d = xp.negative(c)
+    assert d.plan.num_arrays(optimize_graph=False) == 4
+    assert d.plan.num_tasks(optimize_graph=False) == 3 + 12
+    assert d.plan.total_nbytes(optimize_graph=False) == b.nbytes + c.nbytes + d.nbytes
+    assert d.plan.num_arrays(optimize_graph=True) == 2
+    assert d.plan.num_tasks(optimize_graph=True) == 1 + 4
+    assert d.plan.total_nbytes(optimize_graph=True) == d.nbytes
+
+
+def test_fusion_transpose_task_counts(spec):
+    a = xp.asarray([[1, 2, 3], [4, 5, 6], [7, 8, 9]], chunks=(2, 2), spec=spec)
+    d = xp.astype(xp.negative(a), np.float32).T
+    assert d.plan.num_tasks(optimize_graph=False) == 3 + 12
+    assert d.plan.num_tasks(optimize_graph=True) == 1 + 4
+
+
+def test_no_fusion_multiple_dependents(spec):
+    # test_optimization.py:77-94: b feeds c and d, so b is not fused away
+    a = xp.ones((2, 2), chunks=(2, 2), spec=spec)
+    b = xp.positive(a)
+    c = xp.positive(b)
+    d = xp.equal(b, c)
+    assert d.plan.num_tasks(optimize_graph=False) == 3 + 3
+    assert d.plan.num_tasks(optimize_function=simple_optimize_dag) == 3 + 3
+
+
+def test_multiple_inputs_fuse_binary(spec):
+    a = xp.ones((2, 2), chunks=(2, 2), spec=spec)
+    b = xp.ones((2, 2), chunks=(2, 2), spec=spec)
+    c = xp.add(xp.negative(a), xp.negative(b))
+    opt = lambda dag: multiple_inputs_optimize_dag(dag)  # noqa: E731
+    assert c.plan.num_tasks(optimize_function=opt) == 1 + 1
+    assert c.plan.num_tasks(optimize_function=fuse_all_optimize_dag) == 1 + 1
+
+
+def test_blockwise_allowed_mem_exceeded():
+    spec = cubed.Spec(allowed_mem=100)
+    a = xp.asarray(np.arange(24).reshape(4, 6), chunks=(2, 3), spec=cubed.Spec(allowed_mem=10**6))
+    with pytest.raises(ValueError, match=r"Projected blockwise memory \(\d+\) exceeds allowed_mem \(100\), including reserved_mem \(0\)"):
+        elemwise(np.negative, xp.asarray(np.arange(24).reshape(4, 6), chunks=(2, 3), spec=spec),
+                 dtype=np.int64)
+    assert a is not None
+
+
+def test_default_spec_allowed_mem_exceeded():
+    # test_core.py:280-285: a 100 MB chunk doesn't fit the default 200MB budget x4
+    a = xp.ones((20000, 10000), chunks=(10000, 10000))
+    with pytest.raises(ValueError):
+        xp.negative(a)
+
+
+def test_reduction_not_enough_memory():
+    spec = cubed.Spec(allowed_mem=50)
+    a = xp.ones((100, 10), dtype=np.uint8, chunks=(1, 10), spec=spec)
+    with pytest.raises(ValueError, match=r"Not enough memory for reduction"):
+        xp.sum(a, axis=0, dtype=np.uint8)
+
+
+def test_reduction_multiple_rounds_plan():
+    spec = cubed.Spec(allowed_mem=1000)
+    a = xp.ones((100, 10), dtype=np.uint8, chunks=(1, 10), spec=spec)
+    b = xp.sum(a, axis=0, dtype=np.uint8)
+    # several merge+combine rounds were needed (test_core.py:335-347)
+    dag = b.plan._finalize_dag(optimize_graph=False)
+    # func, then >= 2 x (merge_chunks + combine), then aggregate: all "blockwise" ops
+    assert sum(1 for _, d in dag.nodes(data=True) if d.get("op_name") == "blockwise") >= 5
+
+
+@pytest.mark.parametrize("target_chunks, expected_chunksize", [((2, 2), (2, 2)), ((4, 2), (4, 2)), ((2, 4), (2, 4)), ((4, 4), (4, 4))])
+def test_merge_chunks(spec, target_chunks, expected_chunksize):
+    a = xp.ones((10, 10), dtype=np.uint8, chunks=(2, 2), spec=spec)
+    b = merge_chunks(a, target_chunks)
+    assert b.chunksize == expected_chunksize
+
+
+@pytest.mark.parametrize("target_chunks", [(2,), (4, 3)])
+def test_merge_chunks_fails(spec, target_chunks):
+    a = xp.ones((10, 10), dtype=np.uint8, chunks=(2, 2), spec=spec)
+    with pytest.raises(ValueError):
+        merge_chunks(a, target_chunks)
+
+
+def test_partial_and_tree_reduce_shapes(spec):
+    a = xp.asarray(np.arange(242).reshape((11, 22)), chunks=(3, 4), spec=spec)
+    b = partial_reduce(a, np.sum, split_every={0: 2})
+    assert b.chunks == ((1, 1), (4, 4, 4, 4, 4, 2))
+    c = tree_reduce(a, np.sum, axis=0, dtype=np.int64, split_every={0: 2})
+    assert c.shape == (1, 22)
+
+
+@pytest.mark.parametrize("shape, source, target, allowed, nops", [
+    ((50000, 50000), (1000, 50000), (50000, 1000), "2GB", 2),
+    ((50000, 50000), (1000, 50000), (50000, 1000), "288GB", 1),
+    ((4, 4), (1, 2), (2, 1), 1000, 1),
+])
+def test_rechunk_op_counts(shape, source, target, allowed, nops):
+    spec = cubed.Spec(allowed_mem=allowed)
+    a = xp.empty(shape, dtype=np.float32 if shape[0] > 100 else np.float64, chunks=source, spec=spec)
+    b = a.rechunk(target)
+    dag = b.plan._finalize_dag(optimize_graph=False)
+    assert sum(1 for _, d in dag.nodes(data=True) if d.get("op_name") == "rechunk") == nops
+    assert b.chunksize == tuple(target)
+
+
+def test_rechunk_source_chunk_too_big():
+    spec = cubed.Spec(allowed_mem="2GB")
+    a = xp.empty((50000, 50000), dtype=np.float32, chunks=(6250, 50000), spec=spec)
+    with pytest.raises(ValueError, match=r"Source chunk memory \(1250000000\) exceeds max_mem \(500000000\)"):
+        a.rechunk((50000, 1000))
+
+
+def test_rechunk_same_chunks_is_noop(spec):
+    a = xp.ones((4, 4), chunks=(2, 2), spec=spec)
+    assert a.rechunk((2, 2)) is a
+
+
+@pytest.mark.parametrize("value, expected", [("1B", 1), ("1kB", 1000), ("1MB", 10**6), ("2GB", 2 * 10**9), ("288GB", 288 * 10**9), (1e6, 10**6), ("1.5MB", 1500000)])
+def test_convert_to_bytes(value, expected):
+    assert convert_to_bytes(value) == expected
+
+
+def test_quad_means_plan_shape():
+    # test_core.py:527-538 (plan only)
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB")
+    u = crandom.random((1000, 1, 72, 144), chunks=(10, 1, -1, -1), spec=spec)
+    v = crandom.random((1000, 1, 72, 144), chunks=(10, 1, -1, -1), spec=spec)
+    m = xp.mean(u * v, axis=0)
+    assert m.shape == (1, 72, 144)
+    assert m.plan.num_tasks() > 0
+    assert m.plan.max_projected_mem() <= spec.allowed_mem
+
+
+def test_random_is_deterministic_per_seed():
+    import random
+
+    from cubed_amd import ir
+
+    def seed_of(arr):
+        dag = arr.plan._finalize_dag()
+        for _, d in dag.nodes(data=True):
+            fn = getattr(d.get("pipeline"), "config", None)
+            prog = getattr(fn, "function", None)
+            if isinstance(prog, ir.ExprProgram):
+                for _, e in prog.output_items():
+                    for lf in ir.leaves(e):
+                        if isinstance(lf, ir.Philox):
+                            return lf.root_seed
+        return None
+
+    spec = cubed.Spec(allowed_mem=10**8)
+    random.seed(42)
+    a = crandom.random((10, 10), chunks=(5, 5), spec=spec)
+    random.seed(42)
+    b = crandom.random((10, 10), chunks=(5, 5), spec=spec)
+    assert seed_of(a) == seed_of(b) == 0xbdd640fb06671ad11c80317fa3b1799d
