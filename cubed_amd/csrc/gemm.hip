@@ -72,45 +72,52 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const cubed_gemm_task_t* __res
   }
 }
 
-__global__ __launch_bounds__(256) void k_gemm_f64(const cubed_gemm_task_t* __restrict__ tasks,
+// c + a*b: fused for f64 (matches BLAS dgemm's FMA accumulation), wrapping for int64
+CUBED_DEV double mul_add(double a, double b, double c) { return fma(a, b, c); }
+CUBED_DEV int64_t mul_add(int64_t a, int64_t b, int64_t c) {
+  return (int64_t)((uint64_t)c + (uint64_t)a * (uint64_t)b);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gemm_scalar(const cubed_gemm_task_t* __restrict__ tasks,
                                                   int64_t ntasks, int64_t tiles_m, int64_t tiles_n) {
-  __shared__ double As[TK][TM + 1];
-  __shared__ double Bs[TK][TN + 1];
+  __shared__ T As[TK][TM + 1];
+  __shared__ T Bs[TK][TN + 1];
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int64_t tpt = tiles_m * tiles_n;
   const int64_t t = g / tpt, tile = g % tpt;
   if (t >= ntasks) return;
-  const cubed_gemm_task_t* __restrict__ T = tasks + t;
-  const int64_t M = T->m, N = T->n, K = T->k;
+  const cubed_gemm_task_t* __restrict__ TT = tasks + t;
+  const int64_t M = TT->m, N = TT->n, K = TT->k;
   const int64_t m0 = (tile / tiles_n) * TM, n0 = (tile % tiles_n) * TN;
   if (m0 >= M || n0 >= N) return;
-  const double* __restrict__ A = (const double*)T->a;
-  const double* __restrict__ B = (const double*)T->b;
-  double* __restrict__ C = (double*)T->c;
+  const T* __restrict__ A = (const T*)TT->a;
+  const T* __restrict__ B = (const T*)TT->b;
+  T* __restrict__ C = (T*)TT->c;
   const int tid = threadIdx.x;
   const int tr = (tid >> 4) * 4, tc = (tid & 15) * 4;  // 4x4 per thread
-  double acc[4][4] = {};
+  T acc[4][4] = {};
   for (int64_t k0 = 0; k0 < K; k0 += TK) {
     for (int i = tid; i < TM * TK; i += 256) {
       const int mm = i / TK, kk = i % TK;
       const int64_t gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < M && gk < K) ? A[gm * T->lda + gk] : 0.0;
+      As[kk][mm] = (gm < M && gk < K) ? A[gm * TT->lda + gk] : (T)0;
     }
     for (int i = tid; i < TN * TK; i += 256) {
       const int kk = i / TN, nn = i % TN;
       const int64_t gk = k0 + kk, gn = n0 + nn;
-      Bs[kk][nn] = (gk < K && gn < N) ? B[gk * T->ldb + gn] : 0.0;
+      Bs[kk][nn] = (gk < K && gn < N) ? B[gk * TT->ldb + gn] : (T)0;
     }
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < TK; ++kk) {
-      double a[4], b[4];
+      T a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) { a[i] = As[kk][tr + i]; b[i] = Bs[kk][tc + i]; }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mul_add(a[i], b[j], acc[i][j]);
     }
     __syncthreads();
   }
@@ -120,8 +127,8 @@ __global__ __launch_bounds__(256) void k_gemm_f64(const cubed_gemm_task_t* __res
     for (int j = 0; j < 4; ++j) {
       const int64_t gm = m0 + tr + i, gn = n0 + tc + j;
       if (gm < M && gn < N) {
-        double* c = C + gm * T->ldc + gn;
-        *c = T->accumulate ? (*c + acc[i][j]) : acc[i][j];
+        T* c = C + gm * TT->ldc + gn;
+        *c = TT->accumulate ? (*c + acc[i][j]) : acc[i][j];
       }
     }
 }
@@ -141,7 +148,9 @@ extern "C" int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntask
   if (dtype == CUBED_F32) {
     hipLaunchKernelGGL(k_gemm_f32, grid, dim3(256), 0, st, d_tasks, ntasks, tm, tn);
   } else if (dtype == CUBED_F64) {
-    hipLaunchKernelGGL(k_gemm_f64, grid, dim3(256), 0, st, d_tasks, ntasks, tm, tn);
+    hipLaunchKernelGGL(k_gemm_scalar<double>, grid, dim3(256), 0, st, d_tasks, ntasks, tm, tn);
+  } else if (dtype == CUBED_I64) {
+    hipLaunchKernelGGL(k_gemm_scalar<int64_t>, grid, dim3(256), 0, st, d_tasks, ntasks, tm, tn);
   } else {
     snprintf(g_err, sizeof(g_err), "cubed_gemm_chunks: dtype %d not supported", dtype);
     return CUBED_E_DTYPE;

@@ -320,9 +320,10 @@ class GpuDagExecutor(DagExecutor):
                 raise LoweringError("batched matmul chunks are not lowered yet")
             if f32 and not (A.dtype == np.float32 and B.dtype == np.float32):
                 raise LoweringError("f32 matmul with non-f32 inputs")
-            if not f32 and (A.dtype != np.float64 or B.dtype != np.float64 or target.dtype != np.float64):
+            if not f32 and not (A.dtype == B.dtype == target.dtype and
+                                A.dtype in (np.float64, np.int64)):
                 raise LoweringError(f"matmul of {A.dtype} x {B.dtype} -> {target.dtype} is not lowered "
-                                    "(f32 and f64 only)")
+                                    "(f32, f64 and int64 only)")
             am, ak = A.chunk_extent(a_key[1:])
             bk, bn = B.chunk_extent(b_key[1:])
             if ak != bk:
@@ -330,7 +331,7 @@ class GpuDagExecutor(DagExecutor):
             rows[i] = (A.chunk_addr(a_key[1:]), B.chunk_addr(b_key[1:]), target.chunk_addr(key),
                        am, bn, ak, ak, bn, bn, 0)
             max_m, max_n = max(max_m, am), max(max_n, bn)
-        code = ir.dtype_code(np.float32 if f32 else np.float64)
+        code = ir.dtype_code(np.float32 if f32 else target.dtype)
         return GemmLaunch(rows, code, max_m, max_n, self.device)
 
     # -- execution -------------------------------------------------------------

@@ -1,15 +1,22 @@
 #!/bin/bash
-# One GPU session: smoke, parity smoke, bench, kernel-trace profile.
+# One GPU session: smoke, GPU parity tests, bench, kernel-trace profile.
+# Every GPU step has its own time limit; a crash/abort/timeout ends the session
+# (test *failures* -- pytest exit 1 -- do not, so the bench still runs).
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-step() { echo "== $1" >> gpurun_out/steps.log; }
+step() { echo "== $1 $(date +%T)" >> gpurun_out/steps.log; }
+fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 step smoke
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; exit 1; }
-step parity
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo pytest-gpu failed; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke.log; exit 1; }
+step pytest
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -15 gpurun_out/pytest_gpu.log
+if fatal $rc; then echo "pytest-gpu crashed rc=$rc"; exit 1; fi
 step bench
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; exit 1; }
+timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
 step prof
-cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { echo prof failed; exit 1; }
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { echo prof failed; tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
 echo all-done
