@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := cubed_amd/csrc
-SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/copy_random.hip $(CSRC)/gemm.hip
+SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm.hip
 OBJS := $(SRCS:.hip=.o)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -Iinclude
@@ -10,11 +10,11 @@ LIB := cubed_amd/libcubed_amd.so
 
 all: $(LIB) oracle
 
-$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h include/cubed_amd.h
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h $(CSRC)/kernels.h include/cubed_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

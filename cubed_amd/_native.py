@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 2  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 3  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -125,6 +125,15 @@ def lib():
     L.cubed_copy_boxes.restype = c_int
     L.cubed_gemm_chunks.argtypes = [c_void_p, c_int64, c_int32, c_int64, c_int64, c_void_p]
     L.cubed_gemm_chunks.restype = c_int
+    L.cubed_fused_compile.argtypes = [POINTER(Program), c_char_p, POINTER(c_void_p)]
+    L.cubed_fused_compile.restype = c_int
+    L.cubed_fused_chunks_compiled.argtypes = [c_void_p, POINTER(Program), c_void_p, c_void_p, c_int64,
+                                              c_int64, c_int64, c_void_p, c_int64, c_void_p]
+    L.cubed_fused_chunks_compiled.restype = c_int
+    L.cubed_fused_source.argtypes = [c_void_p]
+    L.cubed_fused_source.restype = c_char_p
+    L.cubed_fused_code_bytes.argtypes = [c_void_p]
+    L.cubed_fused_code_bytes.restype = c_int64
     L.cubed_abi_version.restype = c_int
     L.cubed_last_error.restype = c_char_p
     L.cubed_device_count.restype = c_int
@@ -143,5 +152,29 @@ def check(rc: int, what: str):
 EXPORTED_SYMBOLS = (
     "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_random_chunks",
     "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
-    "cubed_device_count",
+    "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
+    "cubed_fused_code_bytes",
 )
+
+
+INCLUDE_DIRS = ";".join([os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc"),
+                         os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")])
+
+
+def jit_enabled() -> bool:
+    """Runtime-specialised fused kernels (default).  CUBED_AMD_JIT=0 selects
+    the ahead-of-time interpreter kernels instead (for comparison/debug)."""
+    return os.environ.get("CUBED_AMD_JIT", "1") != "0"
+
+
+def compile_program(prog: "Program"):
+    """Compile (or fetch from the process cache) the specialised kernels of
+    one fused program; returns the opaque handle."""
+    h = c_void_p()
+    check(lib().cubed_fused_compile(ctypes.byref(prog), INCLUDE_DIRS.encode(), ctypes.byref(h)),
+          "cubed_fused_compile")
+    return h
+
+
+def program_source(handle) -> str:
+    return lib().cubed_fused_source(handle).decode()

@@ -4,12 +4,12 @@
 // semantics of the VM ops (npy_divmod, NaN-propagating maximum, ...), and
 // the Philox4x64-10 generator numpy uses for Generator.random().
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
-#include <hip/hip_fp16.h>
-#include <hip/hip_bf16.h>
 #include <stdint.h>
 #include <type_traits>
-#include "../../include/cubed_amd.h"
+#endif
+#include "cubed_amd.h"
 
 #define CUBED_DEV __device__ __forceinline__
 
@@ -29,6 +29,13 @@ template <typename T>
 CUBED_DEV CUBED_G T* gstore_ptr(char* p) { return (CUBED_G T*)(uintptr_t)p; }
 
 namespace cubed {
+
+// minimal type traits (hipRTC builds have no <type_traits>)
+template <typename A, typename B> struct is_same_t { static constexpr bool value = false; };
+template <typename A> struct is_same_t<A, A> { static constexpr bool value = true; };
+template <typename A, typename B> inline constexpr bool is_same_v = is_same_t<A, B>::value;
+template <bool C, typename A, typename B> struct conditional { using type = A; };
+template <typename A, typename B> struct conditional<false, A, B> { using type = B; };
 
 static constexpr int kBlock = 256;  // 4 waves of 64
 
@@ -86,7 +93,7 @@ CUBED_DEV int64_t f2i64(double x) {
 
 template <typename V>
 CUBED_DEV int64_t to_i64(V x) {
-  if constexpr (std::is_same<V, int64_t>::value) return x;
+  if constexpr (is_same_v<V, int64_t>) return x;
   else return f2i64((double)x);
 }
 
@@ -103,7 +110,7 @@ CUBED_DEV void st1(char* p, int dt, V v) {
     case CUBED_U16: *gstore_ptr<uint16_t>(p) = (uint16_t)to_i64(v); return;
     case CUBED_U32: *gstore_ptr<uint32_t>(p) = (uint32_t)to_i64(v); return;
     case CUBED_U64:
-      if constexpr (std::is_same<V, int64_t>::value) *gstore_ptr<uint64_t>(p) = (uint64_t)v;
+      if constexpr (is_same_v<V, int64_t>) *gstore_ptr<uint64_t>(p) = (uint64_t)v;
       else *gstore_ptr<uint64_t>(p) = ((double)v >= 9223372036854775808.0)
                                ? (uint64_t)((double)v)
                                : (uint64_t)to_i64(v);

@@ -75,9 +75,9 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restrict__ boxes,
                                                       int64_t nboxes, int32_t ndim, int32_t isz,
                                                       int64_t bpb, int64_t rows_per_block) {
-  using T = typename std::conditional<W == 16, u32x4,
-            typename std::conditional<W == 8, uint64_t,
-            typename std::conditional<W == 4, uint32_t, uint8_t>::type>::type>::type;
+  using T = typename conditional<W == 16, u32x4,
+            typename conditional<W == 8, uint64_t,
+            typename conditional<W == 4, uint32_t, uint8_t>::type>::type>::type;
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const int64_t bi = g / bpb, blk = g % bpb;
   if (bi >= nboxes) return;

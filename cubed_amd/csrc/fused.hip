@@ -17,182 +17,22 @@
 //   split: when a launch would not fill 256 CUs, the reduced range is split
 //      over workgroups that write partial accumulators to the workspace;
 //      k_finalize combines them in split order and runs the epilogue.
-#include "fused_common.h"
+#include "kernels.h"
 #include <stdio.h>
 #include <string.h>
 
 namespace cubed {
 
 thread_local char g_err[512];
-static void set_err(const char* m) { snprintf(g_err, sizeof(g_err), "%s", m); }
-
-// Load leaf l (VEC elements) at element offset `off`; `inner` is the leaf's
-// stride along the dim the VEC elements run on (0 = broadcast, 1 = packed).
-template <typename V, int VEC>
-CUBED_DEV void load_leaf(V (&o)[VEC], const cubed_program_t& P,
-                         const cubed_task_t* T, int l, int64_t off,
-                         int64_t inner) {
-  const int kind = P.leaf_kind[l];
-  if (kind == CUBED_LEAF_ARRAY) {
-    const char* base = (const char*)T->leaf_base[l];
-    const int dt = P.leaf_dtype[l];
-    if (VEC == 1 || inner == 1) {
-      ldv<V, VEC>(o, base, off, dt);
-    } else if (inner == 0) {
-      const V v = ld1<V>(base + off * dt_size(dt), dt);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = v;
-    } else {
-      const int sz = dt_size(dt);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = ld1<V>(base + (off + j * inner) * sz, dt);
-    }
-  } else if (kind == CUBED_LEAF_PHILOX) {
-    if (VEC == 4 && inner == 1 && (off & 3) == 0) {
-      const uint64_t b = (uint64_t)(off >> 2) + 1ull;
-      P4 r = philox4x64_10(b, 0ull, T->key_lo, T->key_hi);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = (V)u64_to_unit(r.x[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) o[j] = (V)philox_at(T->key_lo, T->key_hi, off + j * inner);
-    }
-  } else if (kind == CUBED_LEAF_IOTA) {
-    const int64_t b = T->leaf_base[l] + off;
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) o[j] = (V)(b + j * inner);
-  } else {
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) o[j] = (V)T->block_offset;
-  }
-}
-
-template <typename V, int VEC>
-CUBED_DEV void load_leaves(Regs<V, VEC>& regs, const cubed_program_t& P,
-                           const cubed_task_t* T, const int64_t (&off)[CUBED_MAX_LEAVES],
-                           const int64_t (&inner)[CUBED_MAX_LEAVES]) {
-  const int nl = P.nleaves;
-  if (nl > 0) load_leaf<V, VEC>(regs.r0, P, T, 0, off[0], inner[0]);
-  if (nl > 1) load_leaf<V, VEC>(regs.r1, P, T, 1, off[1], inner[1]);
-  if (nl > 2) load_leaf<V, VEC>(regs.r2, P, T, 2, off[2], inner[2]);
-  if (nl > 3) load_leaf<V, VEC>(regs.r3, P, T, 3, off[3], inner[3]);
-}
+void set_error(const char* m) { snprintf(g_err, sizeof(g_err), "%s", m); }
+static void set_err(const char* m) { set_error(m); }
 
 // ------------------------------------------------------------------ kernel A
 template <typename V, int VEC>
 __global__ __launch_bounds__(kBlock) void k_fused_a(
     const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
-  const cubed_program_t& P = *Pd;
-  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  const int64_t b = g % bpt;
-  const int64_t rest = g / bpt;
-  const int s = (int)(rest % nsplit);
-  const int64_t t = rest / nsplit;
-  if (t >= ntasks) return;
-  const cubed_task_t* __restrict__ T = tasks + t;
-  const int nd = P.ndim, nr = P.nred;
-
-  int64_t nk = 1, nrd = 1;
-  for (int d = 0; d < nd; ++d) { if (d < nr) nrd *= T->extent[d]; else nk *= T->extent[d]; }
-  const int64_t items = nk / VEC;
-  // split range of the reduced index
-  const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
-
-  int64_t inner[CUBED_MAX_LEAVES];
-#pragma unroll
-  for (int l = 0; l < CUBED_MAX_LEAVES; ++l) inner[l] = T->leaf_stride[l][nd - 1];
-
-  for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
-    int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-    int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
-    int64_t k = item * VEC;
-    const int64_t kflat = k;
-#pragma unroll
-    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-      if (d < nd && d >= nr) {
-        int64_t q, c;
-        divmod64(k, T->extent[d], q, c);
-        k = q;
-#pragma unroll
-        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) loff[l] += c * T->leaf_stride[l][d];
-#pragma unroll
-        for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
-      }
-    }
-    Regs<V, VEC> regs;
-    if (P.nfields == 0) {
-      load_leaves<V, VEC>(regs, P, T, loff, inner);
-      run_vm<V, VEC>(regs, P.insns, P.ninsns, P);
-#pragma unroll
-      for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
-        if (o < P.nouts) {
-          V X[VEC];
-          fetch(regs, P.out_src[o], X);
-          stv<V, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
-        }
-      }
-      continue;
-    }
-    Acc acc[CUBED_MAX_FIELDS][VEC];
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
-
-    // reduced coordinates of r0 (odometer over dims [0, nr))
-    int64_t cr[CUBED_MAX_DIMS];
-    int64_t roff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-    {
-      int64_t rr = r0;
-#pragma unroll
-      for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-        cr[d] = 0;
-        if (d < nr) {
-          int64_t q, c;
-          divmod64(rr, T->extent[d], q, c);
-          rr = q; cr[d] = c;
-#pragma unroll
-          for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] += c * T->leaf_stride[l][d];
-        }
-      }
-    }
-    for (int64_t r = r0; r < r1; ++r) {
-      int64_t off[CUBED_MAX_LEAVES];
-#pragma unroll
-      for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l] + roff[l];
-      load_leaves<V, VEC>(regs, P, T, off, inner);
-      run_vm<V, VEC>(regs, P.insns, P.ninsns, P);
-      accumulate<V, VEC>(acc, regs, P);
-      // advance the odometer
-      bool carry = true;
-#pragma unroll
-      for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-        if (carry && d < nr) {
-          cr[d] += 1;
-#pragma unroll
-          for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] += T->leaf_stride[l][d];
-          if (cr[d] == T->extent[d] && d > 0) {
-            cr[d] = 0;
-#pragma unroll
-            for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] -= T->extent[d] * T->leaf_stride[l][d];
-          } else {
-            carry = false;
-          }
-        }
-      }
-    }
-    if (nsplit == 1) {
-      finish<VEC>(P, T, acc, ooff);
-    } else {
-      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + kflat) * P.nfields;
-#pragma unroll
-      for (int j = 0; j < VEC; ++j)
-#pragma unroll
-        for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-          if (f < P.nfields) w[j * P.nfields + f] = acc[f][j];
-    }
-  }
+  fused_a_body<V, VEC>(*Pd, tasks, ntasks, bpt, nsplit, ws, max_kept);
 }
 
 // ------------------------------------------------------------------ kernel B
@@ -200,106 +40,7 @@ template <typename V, int VEC>
 __global__ __launch_bounds__(kBlock) void k_fused_b(
     const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, int32_t nsplit, Acc* __restrict__ ws) {
-  const cubed_program_t& P = *Pd;
-  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
-  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  const int s = (int)(g % nsplit);
-  const int64_t rest = g / nsplit;
-  const int64_t k = rest % max_kept;
-  const int64_t t = rest / max_kept;
-  if (t >= ntasks) return;
-  const cubed_task_t* __restrict__ T = tasks + t;
-  const int nd = P.ndim, nr = P.nred, nkd = nd - nr;
-  int64_t nk = 1, nrd = 1;
-  for (int d = 0; d < nd; ++d) { if (d < nkd) nk *= T->extent[d]; else nrd *= T->extent[d]; }
-  if (k >= nk) return;
-
-  int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
-  {
-    int64_t kk = k;
-#pragma unroll
-    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-      if (d < nkd) {
-        int64_t q, c;
-        divmod64(kk, T->extent[d], q, c);
-        kk = q;
-#pragma unroll
-        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) loff[l] += c * T->leaf_stride[l][d];
-#pragma unroll
-        for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
-      }
-    }
-  }
-  int64_t inner[CUBED_MAX_LEAVES];
-#pragma unroll
-  for (int l = 0; l < CUBED_MAX_LEAVES; ++l) inner[l] = T->leaf_stride[l][nd - 1];
-
-  // split range, aligned to VEC (the innermost reduced extent is a multiple of VEC)
-  int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
-  r0 -= r0 % VEC; r1 -= r1 % VEC;
-  if (s == nsplit - 1) r1 = nrd;
-
-  Acc acc[CUBED_MAX_FIELDS][VEC];
-#pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
-
-  Regs<V, VEC> regs;
-  for (int64_t p = r0 + (int64_t)threadIdx.x * VEC; p < r1; p += (int64_t)kBlock * VEC) {
-    int64_t off[CUBED_MAX_LEAVES];
-#pragma unroll
-    for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l];
-    int64_t rr = p;
-#pragma unroll
-    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-      if (d < nd && d >= nkd) {
-        int64_t q, c;
-        if (d == nkd) { q = 0; c = rr; } else divmod64(rr, T->extent[d], q, c);
-        rr = q;
-#pragma unroll
-        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] += c * T->leaf_stride[l][d];
-      }
-    }
-    load_leaves<V, VEC>(regs, P, T, off, inner);
-    run_vm<V, VEC>(regs, P.insns, P.ninsns, P);
-    accumulate<V, VEC>(acc, regs, P);
-  }
-  // combine VEC lanes, then the 64-wide wave, then the 4 waves
-  Acc a[CUBED_MAX_FIELDS];
-#pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    a[f] = acc[f][0];
-#pragma unroll
-    for (int j = 1; j < VEC; ++j) a[f] = acc_combine(a[f], acc[f][j], P.field_rop[f], P.field_acc[f]);
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) red[wave][f] = a[f];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    Acc fin[CUBED_MAX_FIELDS][1];
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-      Acc x = red[0][f];
-#pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
-      fin[f][0] = x;
-    }
-    if (nsplit == 1) {
-      finish<1>(P, T, fin, ooff);
-    } else {
-      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + k) * P.nfields;
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f) if (f < P.nfields) w[f] = fin[f][0];
-    }
-  }
+  fused_b_body<V, VEC>(*Pd, tasks, ntasks, max_kept, nsplit, ws);
 }
 
 // ---------------------------------------------------------------- finalize
@@ -308,34 +49,10 @@ __global__ __launch_bounds__(kBlock) void k_fused_b(
 __global__ __launch_bounds__(kBlock) void k_finalize(
     const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, int kd0, int kd1) {
-  const cubed_program_t& P = *Pd;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t t = i / max_kept, k = i % max_kept;
-  if (t >= ntasks) return;
-  const cubed_task_t* __restrict__ T = tasks + t;
-  int64_t nk = 1;
-  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
-  if (k >= nk) return;
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
-  int64_t kk = k;
-  for (int d = kd1 - 1; d >= kd0; --d) {
-    int64_t q, c;
-    divmod64(kk, T->extent[d], q, c);
-    kk = q;
-    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
-  }
-  Acc fin[CUBED_MAX_FIELDS][1];
-  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-    Acc x = ws[(t * max_kept + k) * P.nfields + f];
-    for (int s = 1; s < nsplit; ++s)
-      x = acc_combine(x, ws[(((int64_t)s * ntasks + t) * max_kept + k) * P.nfields + f],
-                      P.field_rop[f], P.field_acc[f]);
-    fin[f][0] = x;
-  }
-  finish<1>(P, T, fin, ooff);
+  finalize_body(*Pd, tasks, ntasks, max_kept, nsplit, ws, kd0, kd1);
 }
 
-static LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
+LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red) {
   LaunchPlan L;
   L.kernel = P->mode & 3;
@@ -395,23 +112,7 @@ static void launch_fused(const cubed_program_t& P, const cubed_program_t* dP, co
   }
 }
 
-}  // namespace cubed
-
-using namespace cubed;
-
-extern "C" int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
-                                               int64_t max_kept, int64_t max_red) {
-  if (!prog || ntasks <= 0) return 0;
-  return plan_launch(prog, ntasks, max_kept, max_red).ws_bytes;
-}
-
-extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_prog,
-                                  const cubed_task_t* d_tasks,
-                                  int64_t ntasks, int64_t max_kept, int64_t max_red,
-                                  void* d_workspace, int64_t workspace_bytes, void* stream) {
-  if (!prog || !d_prog || (!d_tasks && ntasks > 0)) { set_err("cubed_fused_chunks: null argument"); return CUBED_E_ARG; }
-  if (ntasks == 0) return 0;
-  const cubed_program_t& P = *prog;
+int check_program(const cubed_program_t& P) {
   if (P.ndim < 1 || P.ndim > CUBED_MAX_DIMS || P.nred < 0 || P.nred > P.ndim ||
       P.nleaves < 0 || P.nleaves > CUBED_MAX_LEAVES || P.nfields < 0 ||
       P.nfields > CUBED_MAX_FIELDS || P.nouts < 1 || P.nouts > CUBED_MAX_OUTS ||
@@ -433,6 +134,27 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
         return CUBED_E_LAYOUT;
       }
   }
+  return 0;
+}
+
+}  // namespace cubed
+
+using namespace cubed;
+
+extern "C" int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
+                                               int64_t max_kept, int64_t max_red) {
+  if (!prog || ntasks <= 0) return 0;
+  return plan_launch(prog, ntasks, max_kept, max_red).ws_bytes;
+}
+
+extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                  const cubed_task_t* d_tasks,
+                                  int64_t ntasks, int64_t max_kept, int64_t max_red,
+                                  void* d_workspace, int64_t workspace_bytes, void* stream) {
+  if (!prog || !d_prog || (!d_tasks && ntasks > 0)) { set_err("cubed_fused_chunks: null argument"); return CUBED_E_ARG; }
+  if (ntasks == 0) return 0;
+  const cubed_program_t& P = *prog;
+  if (int rc = check_program(P)) return rc;
   if (max_kept <= 0 || max_red <= 0) { set_err("cubed_fused_chunks: empty task bounds"); return CUBED_E_ARG; }
   const LaunchPlan L = plan_launch(&P, ntasks, max_kept, max_red);
   if (L.ws_bytes > 0 && (d_workspace == nullptr || workspace_bytes < L.ws_bytes)) {

@@ -3,6 +3,16 @@
 #pragma once
 #include "vm.h"
 
+// Program hooks: the ahead-of-time kernels interpret P's instruction lists;
+// runtime-specialised builds (jit.cpp) define these to generated
+// straight-line functions before including this header.
+#ifndef CUBED_RUN_PROLOGUE
+#define CUBED_RUN_PROLOGUE(V, VEC, regs) run_vm<V, VEC>(regs, P.insns, P.ninsns, P)
+#endif
+#ifndef CUBED_RUN_EPILOGUE
+#define CUBED_RUN_EPILOGUE(VEC, regs) run_vm<double, VEC>(regs, P.epi, P.nepi, P)
+#endif
+
 namespace cubed {
 
 CUBED_DEV void divmod64(int64_t a, int64_t b, int64_t& q, int64_t& r) {
@@ -47,7 +57,7 @@ CUBED_DEV void finish(const cubed_program_t& P, const cubed_task_t* T,
         put(er, f, X);
       }
     }
-    run_vm<double, VEC>(er, P.epi, P.nepi, P);
+    CUBED_RUN_EPILOGUE(VEC, er);
 #pragma unroll
     for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
       if (o < P.nouts) {
@@ -77,6 +87,7 @@ CUBED_DEV void finish(const cubed_program_t& P, const cubed_task_t* T,
   }
 }
 
+#ifndef __HIPCC_RTC__
 // ---------------------------------------------------------------- launch plan
 struct LaunchPlan {
   int kernel;     // 0 = A, 1 = B
@@ -93,5 +104,10 @@ void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const La
                    int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st);
 
 dim3 grid_of(int64_t blocks);
+LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept, int64_t max_red);
+int check_program(const cubed_program_t& P);  // 0 or a CUBED_E_* code (message set)
+void set_error(const char* msg);
+
+#endif  // __HIPCC_RTC__
 
 }  // namespace cubed

@@ -1,0 +1,461 @@
+// kernels.h -- device bodies of the fused chunk kernels (gfx950).
+//
+// Each body takes the fused program as `const cubed_program_t& P`.  The
+// ahead-of-time kernels (fused.hip, stream.hip) bind P to a device-memory
+// copy read through the scalar cache; the runtime-specialised kernels
+// (jit.cpp) bind it to a compile-time constant, so every switch of the
+// interpreter folds away and the body compiles to straight-line code.
+//
+#pragma once
+#include "fused_common.h"
+
+namespace cubed {
+
+// Load leaf l (VEC elements) at element offset `off`; `inner` is the leaf's
+// stride along the dim the VEC elements run on (0 = broadcast, 1 = packed).
+template <typename V, int VEC>
+CUBED_DEV void load_leaf(V (&o)[VEC], const cubed_program_t& P,
+                         const cubed_task_t* T, int l, int64_t off,
+                         int64_t inner) {
+  const int kind = P.leaf_kind[l];
+  if (kind == CUBED_LEAF_ARRAY) {
+    const char* base = (const char*)T->leaf_base[l];
+    const int dt = P.leaf_dtype[l];
+    if (VEC == 1 || inner == 1) {
+      ldv<V, VEC>(o, base, off, dt);
+    } else if (inner == 0) {
+      const V v = ld1<V>(base + off * dt_size(dt), dt);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = v;
+    } else {
+      const int sz = dt_size(dt);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = ld1<V>(base + (off + j * inner) * sz, dt);
+    }
+  } else if (kind == CUBED_LEAF_PHILOX) {
+    if (VEC == 4 && inner == 1 && (off & 3) == 0) {
+      const uint64_t b = (uint64_t)(off >> 2) + 1ull;
+      P4 r = philox4x64_10(b, 0ull, T->key_lo, T->key_hi);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = (V)u64_to_unit(r.x[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = (V)philox_at(T->key_lo, T->key_hi, off + j * inner);
+    }
+  } else if (kind == CUBED_LEAF_IOTA) {
+    const int64_t b = T->leaf_base[l] + off;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (V)(b + j * inner);
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (V)T->block_offset;
+  }
+}
+
+template <typename V, int VEC>
+CUBED_DEV void load_leaves(Regs<V, VEC>& regs, const cubed_program_t& P,
+                           const cubed_task_t* T, const int64_t (&off)[CUBED_MAX_LEAVES],
+                           const int64_t (&inner)[CUBED_MAX_LEAVES]) {
+  const int nl = P.nleaves;
+  if (nl > 0) load_leaf<V, VEC>(regs.r0, P, T, 0, off[0], inner[0]);
+  if (nl > 1) load_leaf<V, VEC>(regs.r1, P, T, 1, off[1], inner[1]);
+  if (nl > 2) load_leaf<V, VEC>(regs.r2, P, T, 2, off[2], inner[2]);
+  if (nl > 3) load_leaf<V, VEC>(regs.r3, P, T, 3, off[3], inner[3]);
+}
+
+// ------------------------------------------------------------------ kernel A
+template <typename V, int VEC>
+CUBED_DEV void fused_a_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t b = g % bpt;
+  const int64_t rest = g / bpt;
+  const int s = (int)(rest % nsplit);
+  const int64_t t = rest / nsplit;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  const int nd = P.ndim, nr = P.nred;
+
+  int64_t nk = 1, nrd = 1;
+  for (int d = 0; d < nd; ++d) { if (d < nr) nrd *= T->extent[d]; else nk *= T->extent[d]; }
+  const int64_t items = nk / VEC;
+  // split range of the reduced index
+  const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
+
+  int64_t inner[CUBED_MAX_LEAVES];
+#pragma unroll
+  for (int l = 0; l < CUBED_MAX_LEAVES; ++l) inner[l] = T->leaf_stride[l][nd - 1];
+
+  for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
+    int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
+    int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+    int64_t k = item * VEC;
+    const int64_t kflat = k;
+#pragma unroll
+    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+      if (d < nd && d >= nr) {
+        int64_t q, c;
+        divmod64(k, T->extent[d], q, c);
+        k = q;
+#pragma unroll
+        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) loff[l] += c * T->leaf_stride[l][d];
+#pragma unroll
+        for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
+      }
+    }
+    Regs<V, VEC> regs;
+    if (P.nfields == 0) {
+      load_leaves<V, VEC>(regs, P, T, loff, inner);
+      CUBED_RUN_PROLOGUE(V, VEC, regs);
+#pragma unroll
+      for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
+        if (o < P.nouts) {
+          V X[VEC];
+          fetch(regs, P.out_src[o], X);
+          stv<V, VEC>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+        }
+      }
+      continue;
+    }
+    Acc acc[CUBED_MAX_FIELDS][VEC];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
+
+    // reduced coordinates of r0 (odometer over dims [0, nr))
+    int64_t cr[CUBED_MAX_DIMS];
+    int64_t roff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
+    {
+      int64_t rr = r0;
+#pragma unroll
+      for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+        cr[d] = 0;
+        if (d < nr) {
+          int64_t q, c;
+          divmod64(rr, T->extent[d], q, c);
+          rr = q; cr[d] = c;
+#pragma unroll
+          for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] += c * T->leaf_stride[l][d];
+        }
+      }
+    }
+    for (int64_t r = r0; r < r1; ++r) {
+      int64_t off[CUBED_MAX_LEAVES];
+#pragma unroll
+      for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l] + roff[l];
+      load_leaves<V, VEC>(regs, P, T, off, inner);
+      CUBED_RUN_PROLOGUE(V, VEC, regs);
+      accumulate<V, VEC>(acc, regs, P);
+      // advance the odometer
+      bool carry = true;
+#pragma unroll
+      for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+        if (carry && d < nr) {
+          cr[d] += 1;
+#pragma unroll
+          for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] += T->leaf_stride[l][d];
+          if (cr[d] == T->extent[d] && d > 0) {
+            cr[d] = 0;
+#pragma unroll
+            for (int l = 0; l < CUBED_MAX_LEAVES; ++l) roff[l] -= T->extent[d] * T->leaf_stride[l][d];
+          } else {
+            carry = false;
+          }
+        }
+      }
+    }
+    if (nsplit == 1) {
+      finish<VEC>(P, T, acc, ooff);
+    } else {
+      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + kflat) * P.nfields;
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+#pragma unroll
+        for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+          if (f < P.nfields) w[j * P.nfields + f] = acc[f][j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ kernel B
+template <typename V, int VEC>
+CUBED_DEV void fused_b_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, int32_t nsplit, Acc* __restrict__ ws) {
+  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int s = (int)(g % nsplit);
+  const int64_t rest = g / nsplit;
+  const int64_t k = rest % max_kept;
+  const int64_t t = rest / max_kept;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  const int nd = P.ndim, nr = P.nred, nkd = nd - nr;
+  int64_t nk = 1, nrd = 1;
+  for (int d = 0; d < nd; ++d) { if (d < nkd) nk *= T->extent[d]; else nrd *= T->extent[d]; }
+  if (k >= nk) return;
+
+  int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
+  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  {
+    int64_t kk = k;
+#pragma unroll
+    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+      if (d < nkd) {
+        int64_t q, c;
+        divmod64(kk, T->extent[d], q, c);
+        kk = q;
+#pragma unroll
+        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) loff[l] += c * T->leaf_stride[l][d];
+#pragma unroll
+        for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
+      }
+    }
+  }
+  int64_t inner[CUBED_MAX_LEAVES];
+#pragma unroll
+  for (int l = 0; l < CUBED_MAX_LEAVES; ++l) inner[l] = T->leaf_stride[l][nd - 1];
+
+  // split range, aligned to VEC (the innermost reduced extent is a multiple of VEC)
+  int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
+  r0 -= r0 % VEC; r1 -= r1 % VEC;
+  if (s == nsplit - 1) r1 = nrd;
+
+  Acc acc[CUBED_MAX_FIELDS][VEC];
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
+
+  Regs<V, VEC> regs;
+  for (int64_t p = r0 + (int64_t)threadIdx.x * VEC; p < r1; p += (int64_t)kBlock * VEC) {
+    int64_t off[CUBED_MAX_LEAVES];
+#pragma unroll
+    for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l];
+    int64_t rr = p;
+#pragma unroll
+    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+      if (d < nd && d >= nkd) {
+        int64_t q, c;
+        if (d == nkd) { q = 0; c = rr; } else divmod64(rr, T->extent[d], q, c);
+        rr = q;
+#pragma unroll
+        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] += c * T->leaf_stride[l][d];
+      }
+    }
+    load_leaves<V, VEC>(regs, P, T, off, inner);
+    CUBED_RUN_PROLOGUE(V, VEC, regs);
+    accumulate<V, VEC>(acc, regs, P);
+  }
+  // combine VEC lanes, then the 64-wide wave, then the 4 waves
+  Acc a[CUBED_MAX_FIELDS];
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+    a[f] = acc[f][0];
+#pragma unroll
+    for (int j = 1; j < VEC; ++j) a[f] = acc_combine(a[f], acc[f][j], P.field_rop[f], P.field_acc[f]);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) red[wave][f] = a[f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc fin[CUBED_MAX_FIELDS][1];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+      Acc x = red[0][f];
+#pragma unroll
+      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
+      fin[f][0] = x;
+    }
+    if (nsplit == 1) {
+      finish<1>(P, T, fin, ooff);
+    } else {
+      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + k) * P.nfields;
+#pragma unroll
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f) if (f < P.nfields) w[f] = fin[f][0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- finalize
+CUBED_DEV void finalize_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, int kd0, int kd1) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t t = i / max_kept, k = i % max_kept;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  int64_t nk = 1;
+  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+  if (k >= nk) return;
+  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t kk = k;
+  for (int d = kd1 - 1; d >= kd0; --d) {
+    int64_t q, c;
+    divmod64(kk, T->extent[d], q, c);
+    kk = q;
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
+  }
+  Acc fin[CUBED_MAX_FIELDS][1];
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+    Acc x = ws[(t * max_kept + k) * P.nfields + f];
+    for (int s = 1; s < nsplit; ++s)
+      x = acc_combine(x, ws[(((int64_t)s * ntasks + t) * max_kept + k) * P.nfields + f],
+                      P.field_rop[f], P.field_acc[f]);
+    fin[f][0] = x;
+  }
+  finish<1>(P, T, fin, ooff);
+}
+
+// ---------------------------------------------------------------- streaming fast path
+CUBED_DEV void ld4(float (&o)[4], const CUBED_G float* p) {
+  const f32x4 v = __builtin_nontemporal_load((const CUBED_G f32x4*)p);
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+CUBED_DEV void ld4(double (&o)[4], const CUBED_G double* p) {
+  const f64x2 a = __builtin_nontemporal_load((const CUBED_G f64x2*)p);
+  const f64x2 b = __builtin_nontemporal_load((const CUBED_G f64x2*)(p + 2));
+  o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+CUBED_DEV void ld4(int64_t (&o)[4], const CUBED_G int64_t* p) {
+  const i64x2 a = __builtin_nontemporal_load((const CUBED_G i64x2*)p);
+  const i64x2 b = __builtin_nontemporal_load((const CUBED_G i64x2*)(p + 2));
+  o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+
+template <int NL, typename V>
+CUBED_DEV void set_leaves(Regs<V, 4>& regs, const V (&b)[NL][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    regs.r0[j] = b[0][j];
+    if constexpr (NL > 1) regs.r1[j] = b[1][j];
+    if constexpr (NL > 2) regs.r2[j] = b[2][j];
+    if constexpr (NL > 3) regs.r3[j] = b[3][j];
+  }
+}
+
+template <typename V>
+CUBED_DEV void accumulate_nocount(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
+                                  const cubed_program_t& P) {
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+    if (f < P.nfields && P.field_rop[f] != CUBED_R_COUNT) {
+      V src[4];
+      fetch(regs, P.field_src[f], src);
+      const int rop = P.field_rop[f], ai = P.field_acc[f];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
+    }
+  }
+}
+
+template <typename V, int NL, int U>
+CUBED_DEV void stream_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t b = g % bpt;
+  const int64_t rest = g / bpt;
+  const int s = (int)(rest % nsplit);
+  const int64_t t = rest / nsplit;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  const int nr = P.nred;  // 0 (map) or 1
+  const int64_t nk = T->extent[nr];
+  const int64_t nrd = nr ? T->extent[0] : 1;
+  const int64_t items = nk >> 2;
+  const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
+
+  const CUBED_G V* base[NL];
+  int64_t rs[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    base[l] = (const CUBED_G V*)(uintptr_t)T->leaf_base[l];
+    rs[l] = nr ? T->leaf_stride[l][0] : 0;
+  }
+
+  for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
+    const int64_t k = item * 4;
+    int64_t ooff[CUBED_MAX_OUTS];
+#pragma unroll
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] = k;
+    Regs<V, 4> regs;
+    if (P.nfields == 0) {
+      V buf[NL][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) ld4(buf[l], base[l] + k);
+      set_leaves<NL, V>(regs, buf);
+      CUBED_RUN_PROLOGUE(V, 4, regs);
+#pragma unroll
+      for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
+        if (o < P.nouts) {
+          V X[4];
+          fetch(regs, P.out_src[o], X);
+          stv<V, 4>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+        }
+      }
+      continue;
+    }
+    Acc acc[CUBED_MAX_FIELDS][4];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
+
+    const CUBED_G V* p[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) p[l] = base[l] + k + r0 * rs[l];
+    int64_t r = r0;
+    for (; r + U <= r1; r += U) {
+      V buf[U][NL][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int l = 0; l < NL; ++l) ld4(buf[u][l], p[l] + u * rs[l]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        set_leaves<NL, V>(regs, buf[u]);
+        CUBED_RUN_PROLOGUE(V, 4, regs);
+        accumulate_nocount<V>(acc, regs, P);
+      }
+#pragma unroll
+      for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
+    }
+    for (; r < r1; ++r) {
+      V buf[NL][4];
+#pragma unroll
+      for (int l = 0; l < NL; ++l) ld4(buf[l], p[l]);
+      set_leaves<NL, V>(regs, buf);
+      CUBED_RUN_PROLOGUE(V, 4, regs);
+      accumulate_nocount<V>(acc, regs, P);
+#pragma unroll
+      for (int l = 0; l < NL; ++l) p[l] += rs[l];
+    }
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+      if (f < P.nfields && P.field_rop[f] == CUBED_R_COUNT)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[f][j].i += r1 - r0;
+
+    if (nsplit == 1) {
+      finish<4>(P, T, acc, ooff);
+    } else {
+      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + k) * P.nfields;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+          if (f < P.nfields) w[j * P.nfields + f] = acc[f][j];
+    }
+  }
+}
+
+}  // namespace cubed

@@ -44,7 +44,7 @@ CUBED_DEV void put(Regs<V, VEC>& regs, int idx, const V (&X)[VEC]) {
 template <typename V>
 CUBED_DEV V cast_val(V x, int t, int s) {
   if (t == CUBED_BOOL) return (x != (V)0) ? (V)1 : (V)0;
-  if constexpr (std::is_same<V, int64_t>::value) {
+  if constexpr (is_same_v<V, int64_t>) {
     switch (t) {
       case CUBED_I8: return (int64_t)(int8_t)x;
       case CUBED_I16: return (int64_t)(int16_t)x;
@@ -79,7 +79,7 @@ CUBED_DEV V cast_val(V x, int t, int s) {
 
 template <typename V, int VEC>
 CUBED_DEV void unary(int op, V (&X)[VEC]) {
-  if constexpr (std::is_same<V, int64_t>::value) {
+  if constexpr (is_same_v<V, int64_t>) {
     switch (op) {
       case CUBED_OP_NEG: CUBED_EACH((int64_t)(0ull - (uint64_t)x)); break;
       case CUBED_OP_ABS: CUBED_EACH(x < 0 ? (int64_t)(0ull - (uint64_t)x) : x); break;
@@ -135,7 +135,7 @@ CUBED_DEV void unary(int op, V (&X)[VEC]) {
 
 template <typename V, int VEC>
 CUBED_DEV void binary(int op, V (&X)[VEC], const V (&Y)[VEC]) {
-  if constexpr (std::is_same<V, int64_t>::value) {
+  if constexpr (is_same_v<V, int64_t>) {
     switch (op) {
       case CUBED_OP_ADD: CUBED_EACH2((int64_t)((uint64_t)x + (uint64_t)y)); break;
       case CUBED_OP_SUB: CUBED_EACH2((int64_t)((uint64_t)x - (uint64_t)y)); break;
@@ -206,7 +206,7 @@ CUBED_DEV void run_vm(Regs<V, VEC>& regs, const cubed_insn_t* ins, int n,
     V X[VEC];
     if (op == CUBED_OP_CONST) {
       V c;
-      if constexpr (std::is_same<V, int64_t>::value) c = P.consts[I.imm].i;
+      if constexpr (is_same_v<V, int64_t>) c = P.consts[I.imm].i;
       else c = (V)P.consts[I.imm].f;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) X[j] = c;
@@ -236,6 +236,54 @@ CUBED_DEV void run_vm(Regs<V, VEC>& regs, const cubed_insn_t* ins, int n,
       unary<V, VEC>(op, X);
     }
     put(regs, I.a, X);
+  }
+}
+
+
+// ---------------------------------------------------------------- static form
+// One instruction with every operand a compile-time constant: the form the
+// runtime-specialised kernels (jit.cpp) are generated in.  Register operands
+// resolve to named registers at compile time and the op switch folds, so a
+// program compiles to straight-line VALU code with no scratch and no branches.
+template <int I, typename V, int VEC>
+CUBED_DEV V (&regref(Regs<V, VEC>& r))[VEC] {
+  if constexpr (I == 0) return r.r0;
+  else if constexpr (I == 1) return r.r1;
+  else if constexpr (I == 2) return r.r2;
+  else if constexpr (I == 3) return r.r3;
+  else if constexpr (I == 4) return r.r4;
+  else return r.r5;
+}
+
+template <int OP, int A, int B, int C, int T, int IMM, typename V, int VEC>
+CUBED_DEV void sinsn(Regs<V, VEC>& regs, const cubed_program_t& P) {
+  V (&X)[VEC] = regref<A>(regs);
+  if constexpr (OP == CUBED_OP_CONST) {
+    V c;
+    if constexpr (is_same_v<V, int64_t>) c = P.consts[IMM].i;
+    else c = (V)P.consts[IMM].f;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) X[j] = c;
+  } else if constexpr (OP == CUBED_OP_MOV) {
+    const V (&Y)[VEC] = regref<B>(regs);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) X[j] = Y[j];
+  } else if constexpr (OP == CUBED_OP_CAST) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) X[j] = cast_val<V>(X[j], T, IMM);
+  } else if constexpr (OP == CUBED_OP_WHERE) {
+    V Y[VEC], Cn[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { Y[j] = regref<B>(regs)[j]; Cn[j] = regref<C>(regs)[j]; }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) X[j] = (Cn[j] != (V)0) ? X[j] : Y[j];
+  } else if constexpr (OP >= CUBED_OP_ADD) {
+    V Y[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) Y[j] = regref<B>(regs)[j];
+    binary<V, VEC>(OP, X, Y);
+  } else {
+    unary<V, VEC>(OP, X);
   }
 }
 

@@ -567,6 +567,7 @@ class FusedLaunch:
         raw = np.frombuffer(ctypes.string_at(ctypes.addressof(prog_struct), ctypes.sizeof(prog_struct)),
                             dtype=np.uint8)
         self.d_prog = torch.from_numpy(raw.copy()).to(device)  # read by the kernels
+        self.handle = nat.compile_program(prog_struct) if nat.jit_enabled() else None
         self.table = table
         self.ntasks = ntasks
         self.max_kept = max_kept
@@ -579,6 +580,12 @@ class FusedLaunch:
         for g in self.gathers:
             g.run(stream)
         L = nat.lib()
+        if self.handle is not None:
+            nat.check(L.cubed_fused_chunks_compiled(
+                self.handle, self.prog, self.d_prog.data_ptr(), self.table.data_ptr(), self.ntasks,
+                self.max_kept, self.max_red, self.ws.data_ptr() if self.ws is not None else None,
+                self.ws_bytes, stream), "cubed_fused_chunks_compiled")
+            return
         nat.check(L.cubed_fused_chunks(self.prog, self.d_prog.data_ptr(), self.table.data_ptr(),
                                        self.ntasks, self.max_kept,
                                        self.max_red, self.ws.data_ptr() if self.ws is not None else None,

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 2
+#define CUBED_ABI_VERSION 3
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -61,6 +61,7 @@ extern "C" {
 #define CUBED_E_DTYPE (-2)
 #define CUBED_E_LAYOUT (-3)
 #define CUBED_E_WORKSPACE (-4)
+#define CUBED_E_JIT (-5)
 
 /* element dtypes (numpy kinds); bool is 1 byte 0/1 */
 enum cubed_dtype {
@@ -185,6 +186,25 @@ int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_pro
                        const cubed_task_t* d_tasks,
                        int64_t ntasks, int64_t max_kept, int64_t max_red,
                        void* d_workspace, int64_t workspace_bytes, void* stream);
+
+/* Runtime-specialised form of cubed_fused_chunks (same semantics, same task
+ * table): cubed_fused_compile() generates a kernel for *prog with the program
+ * baked in as compile-time constants (straight-line code, no interpreter
+ * dispatch), compiles it for gfx950 with hipRTC and caches the code object
+ * per program for the life of the process.  `include_dirs` is a ';'-separated
+ * list holding kernels.h/vm.h/common.h and cubed_amd.h.  Needs no GPU; the
+ * code object is loaded on the current device at first launch.
+ * Replaces the same reference interface as cubed_fused_chunks, plus the
+ * plan-time composition of the chunk function (fuse / fuse_multiple,
+ * cubed/primitive/blockwise.py:368-508). */
+int cubed_fused_compile(const cubed_program_t* prog, const char* include_dirs, void** handle);
+int cubed_fused_chunks_compiled(void* handle, const cubed_program_t* prog,
+                                const cubed_program_t* d_prog, const cubed_task_t* d_tasks,
+                                int64_t ntasks, int64_t max_kept, int64_t max_red,
+                                void* d_workspace, int64_t workspace_bytes, void* stream);
+/* The generated source / code object size of a compiled program (diagnostics). */
+const char* cubed_fused_source(const void* handle);
+int64_t cubed_fused_code_bytes(const void* handle);
 
 /* Workspace the call above needs (split reductions keep partial
  * accumulators there).  Pure host function. */

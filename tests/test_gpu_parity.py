@@ -370,3 +370,40 @@ def test_bench_size_rechunk_roundtrip(ex):
     zs = z.zarray.slabs[None][: z.nbytes].view(torch.int32).to(torch.int64)
     assert int(xs.sum()) == int(zs.sum())
     assert torch.equal(x.zarray.slabs[None][: x.nbytes], z.zarray.slabs[None][: z.nbytes])
+
+
+# ------------------------------------------- specialised vs interpreted kernels
+
+
+@pytest.mark.parametrize("case", ["quad", "where", "nanmean", "int_sum_rows", "cast_chain"])
+def test_specialised_kernels_match_interpreter(monkeypatch, case):
+    """The runtime-specialised kernels (default) and the ahead-of-time
+    interpreter kernels (CUBED_AMD_JIT=0) compute bit-identical results."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    def run():
+        ex = GpuDagExecutor("cuda:0")
+        spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex)
+        rng = np.random.default_rng(21)
+        x = rng.random((64, 40, 24))
+        x[x < 0.1] = np.nan
+        a = cubed.from_array(x, chunks=(16, 40, 24), spec=spec)
+        b = cubed.from_array((x * 100).astype(np.float32), chunks=(16, 40, 24), spec=spec)
+        if case == "quad":
+            out = xp.mean(b * b, axis=0)
+        elif case == "where":
+            out = xp.where(a > 0.5, a * 2, -a)
+        elif case == "nanmean":
+            out = cubed.nanmean(a, axis=2)
+        elif case == "int_sum_rows":
+            out = xp.sum(xp.astype(b, xp.int64), axis=2)
+        else:
+            out = xp.astype(xp.astype(b, xp.int32) * 3 + 1, xp.float64) / 7
+        return out.compute()
+
+    monkeypatch.setenv("CUBED_AMD_JIT", "1")
+    got = run()
+    monkeypatch.setenv("CUBED_AMD_JIT", "0")
+    exp = run()
+    assert got.dtype == exp.dtype
+    assert np.array_equal(got, exp, equal_nan=True)

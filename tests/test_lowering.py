@@ -92,3 +92,22 @@ def test_task_table_rows_match_tasks(built, dry):
         tab = L.table.numpy().view(nat.TASK_DTYPE)
         assert len(tab) == L.ntasks
         assert (tab["extent"] >= 1).all()
+
+
+def test_fused_programs_compile_specialised(built, dry):
+    """Every fused launch of a mixed plan gets a runtime-specialised gfx950
+    kernel (hipRTC; no GPU needed to compile) with the program baked in."""
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(2)
+    a = xp.astype(crandom.random((60, 8, 12), chunks=(10, 8, 12), spec=spec), xp.float32)
+    b = cubed.from_array(np.arange(60 * 96, dtype=np.int64).reshape(60, 96), chunks=(7, 32), spec=spec)
+    outs = [xp.mean(a * a, axis=0), xp.sum(b, axis=1), xp.max(b, axis=0), cubed.nanmean(a, axis=2),
+            xp.where(a > 0.5, a, -a), xp.astype(b, xp.float64) / 3]
+    arrays_to_plan(*outs).execute(executor=dry, array_names=[o.name for o in outs])
+    fused = _fused(dry)
+    assert len(fused) >= 6
+    for L in fused:
+        assert L.handle is not None
+        src = nat.program_source(L.handle)
+        assert "fused_main" in src
+        assert nat.lib().cubed_fused_code_bytes(L.handle) > 0
