@@ -52,6 +52,32 @@ __global__ __launch_bounds__(kBlock) void k_finalize(
   finalize_body(*Pd, tasks, ntasks, max_kept, nsplit, ws, kd0, kd1);
 }
 
+// Split factor for a reduction whose un-split grid has `base` workgroups:
+// enough workgroups to fill the chip (`resident` = 256 CUs x 8 resident
+// 256-thread groups at the specialised kernels' occupancy), rounded so the
+// last round of workgroups is nearly full (a 1.5-round grid idles half the
+// chip for its last third).  Deterministic in its arguments, so the
+// workspace size the host queries matches the launch.
+static int64_t choose_split(int64_t base, int64_t max_split, int64_t resident) {
+  if (max_split < 2) return 1;
+  if (max_split > 4096) max_split = 4096;
+  int64_t best = 1;
+  double best_eff = 0.0;
+  for (int64_t s = 1; s <= max_split && s <= 64; ++s) {
+    const int64_t blocks = base * s;
+    if (blocks < (resident * 9) / 10) continue;
+    const int64_t rounds = (blocks + resident - 1) / resident;
+    const double eff = (double)blocks / (double)(rounds * resident);
+    if (eff >= 0.9) return s;
+    if (eff > best_eff) { best_eff = eff; best = s; }
+  }
+  if (best_eff == 0.0) {  // even max_split cannot fill the chip: use it
+    int64_t s = (resident + base - 1) / base;
+    return s > max_split ? max_split : s;
+  }
+  return best;
+}
+
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red) {
   LaunchPlan L;
@@ -67,10 +93,7 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     if (L.bpt > 65536) L.bpt = 65536;
     const int64_t base = ntasks * L.bpt;
     if (P->nfields > 0 && base < target && max_red >= 64) {
-      int64_t s = (target + base - 1) / base;
-      if (s > max_red / 16) s = max_red / 16;
-      if (s > 4096) s = 4096;
-      if (s > 1) L.nsplit = (int32_t)s;
+      L.nsplit = (int32_t)choose_split(base, max_red / 16, target);
     }
     L.blocks = ntasks * L.nsplit * L.bpt;
   } else {

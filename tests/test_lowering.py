@@ -109,5 +109,5 @@ def test_fused_programs_compile_specialised(built, dry):
     for L in fused:
         assert L.handle is not None
         src = nat.program_source(L.handle)
-        assert "fused_main" in src
+        assert "jit_prologue" in src and "cubed_" in src
         assert nat.lib().cubed_fused_code_bytes(L.handle) > 0

@@ -19,4 +19,11 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpuru
 cat gpurun_out/bench.json
 step prof
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-extra --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { echo prof failed; tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
+if [ -z "${NO_PMC}" ]; then
+  step pmc
+  R=$GRAFT_REPO_ROOT
+  cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline > $R/gpurun_out/pmc_fetch.log 2>&1 || { echo pmc fetch failed; tail -20 $R/gpurun_out/pmc_fetch.log; exit 1; }
+  cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline > $R/gpurun_out/pmc_write.log 2>&1 || { echo pmc write failed; tail -20 $R/gpurun_out/pmc_write.log; exit 1; }
+  cd $R && python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write cubed_stream_f32 > gpurun_out/traffic.json && cat gpurun_out/traffic.json
+fi
 echo all-done
