@@ -24,6 +24,6 @@ if [ -z "${NO_PMC}" ]; then
   R=$GRAFT_REPO_ROOT
   cd /tmp && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline > $R/gpurun_out/pmc_fetch.log 2>&1 || { echo pmc fetch failed; tail -20 $R/gpurun_out/pmc_fetch.log; exit 1; }
   cd /tmp && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-extra --no-cpu-baseline > $R/gpurun_out/pmc_write.log 2>&1 || { echo pmc write failed; tail -20 $R/gpurun_out/pmc_write.log; exit 1; }
-  cd $R && python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write cubed_stream_f32 > gpurun_out/traffic.json && cat gpurun_out/traffic.json
+  cd $R && python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write cubed_stream_f32_l2_r1 > gpurun_out/traffic.json && cat gpurun_out/traffic.json
 fi
 echo all-done
