@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 3  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 4  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -134,6 +134,12 @@ def lib():
     L.cubed_fused_source.restype = c_char_p
     L.cubed_fused_code_bytes.argtypes = [c_void_p]
     L.cubed_fused_code_bytes.restype = c_int64
+    L.cubed_fused_finish.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                     c_void_p]
+    L.cubed_fused_finish.restype = c_int
+    L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
+                                         c_void_p]
+    L.cubed_combine_partials.restype = c_int
     L.cubed_abi_version.restype = c_int
     L.cubed_last_error.restype = c_char_p
     L.cubed_device_count.restype = c_int
@@ -153,7 +159,7 @@ EXPORTED_SYMBOLS = (
     "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_random_chunks",
     "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
-    "cubed_fused_code_bytes",
+    "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
 )
 
 

@@ -216,19 +216,32 @@ def contributing_keys(chain: Chain, final_key) -> List[Tuple[int, ...]]:
     return sorted(set(keys))
 
 
-def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys) -> Tuple[List[TaskRow], set]:
+def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys, select=None, out_owned=None,
+               discard=0) -> Tuple[List[TaskRow], set]:
     """Fused task rows (space = [one chunk dim per reduced axis] + first
-    node's dims) and the reduced dim set."""
+    node's dims) and the reduced dim set.
+
+    Multi-GPU (partials mode): ``select[K]`` = the contributing first-level
+    task keys this rank owns for output block K (possibly none: the row then
+    has extent 0 along the chunk dims and yields the reduction identity);
+    outputs of blocks ``out_owned(K)`` is false for go to ``discard``."""
+    from .storage import geometry_only
+
     p1 = chain.first_spec.function
     axes = tuple(chain.program.reduce.axes)
     na = len(axes)
     n = chain.program.ndim
     red = set(range(na)) | {na + a for a in axes}
     rows = []
+    empty = []  # (row index, K) of rows with no local contribution
     final = chain.final_target
     outs = chain.program.output_items()
     for K in final_keys:
-        tkeys = contributing_keys(chain, K)
+        tkeys = contributing_keys(chain, K) if select is None else select[K]
+        if not tkeys:
+            empty.append((len(rows), K))
+            rows.append(None)
+            continue
         layouts = {}
         for t in tkeys:
             layouts[t] = lowerer.task_layout(p1, chain.first_spec, chain.first_target, t, leaves,
@@ -263,22 +276,47 @@ def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys) -> Tuple[List[T
                 if layouts[t].bases[l] != exp:
                     raise LoweringError("leaf chunks are not at an affine stride")
             qstr.append(s_l)
-        # output: the final target chunk K, mapped through the final out_axes
         extent = nq + list(r0.extent)
         lstrides = [qs + list(st) for qs, st in zip(qstr, r0.lstrides)]
-        ostr, obases = [], []
-        for name, _ in outs:
-            fname = name if chain.program.structured else None
-            v = chunk_view(final, K, fname) if final.ndim else None
-            st = [0] * (na + n)
-            if v is not None:
-                for j, s in enumerate(chain.program.out_axes):
-                    if s is not None and j < len(v.stride) and s not in axes:
-                        st[na + s] = v.stride[j] if extent[na + s] != 1 else 0
-                obases.append(v.base)
-            else:
-                obases.append(final.chunk_addr((), fname))
-            ostr.append(st)
+        obases, ostr = _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard)
         rows.append(TaskRow(extent, list(r0.bases), lstrides, obases, ostr,
                             r0.key_lo, r0.key_hi, r0.block_offset))
+    if empty:
+        template = next((r for r in rows if r is not None), None)
+        for i, K in empty:
+            # shape of block K's tasks (no addresses are read through it)
+            with geometry_only():
+                t0 = contributing_keys(chain, K)[0]
+                g = lowerer.task_layout(p1, chain.first_spec, chain.first_target, t0, leaves,
+                                        [], p1.structured, [])
+            extent = [0] * na + list(g.extent)
+            if template is not None:
+                lstrides = [list(st) for st in template.lstrides]
+            else:
+                lstrides = [[0] * na + list(st) for st in g.lstrides]
+            obases, ostr = _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard)
+            rows[i] = TaskRow(extent, [0] * len(leaves), lstrides, obases, ostr, 0, 0, 0)
     return rows, red
+
+
+def _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard):
+    """Output views of final block K through the final out_axes (block K's
+    own strides; base = ``discard`` when another rank owns K)."""
+    from .storage import geometry_only
+
+    final = chain.final_target
+    owned = out_owned is None or out_owned(K)
+    ostr, obases = [], []
+    for name, _ in chain.program.output_items():
+        fname = name if chain.program.structured else None
+        with geometry_only():
+            v = chunk_view(final, K, fname) if final.ndim else None
+            base0 = final.chunk_addr((), fname) if v is None else v.base
+        st = [0] * (na + n)
+        if v is not None:
+            for j, s in enumerate(chain.program.out_axes):
+                if s is not None and j < len(v.stride) and s not in axes:
+                    st[na + s] = v.stride[j] if extent[na + s] != 1 else 0
+        obases.append(base0 if owned else discard)
+        ostr.append(st)
+    return obases, ostr

@@ -52,6 +52,44 @@ __global__ __launch_bounds__(kBlock) void k_finalize(
   finalize_body(*Pd, tasks, ntasks, max_kept, nsplit, ws, kd0, kd1);
 }
 
+// Partials mode: combine splits into SoA per-field partials (kernels.h).
+__global__ __launch_bounds__(kBlock) void k_collect(
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, Acc* __restrict__ soa, int kd0, int kd1) {
+  collect_body(*Pd, tasks, ntasks, max_kept, nsplit, ws, soa, kd0, kd1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_finish_soa(
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, int kd0, int kd1) {
+  finish_soa_body(*Pd, tasks, ntasks, max_kept, soa, kd0, kd1);
+}
+
+__global__ __launch_bounds__(kBlock) void k_combine_parts(
+    const cubed_program_t* __restrict__ Pd, const Acc* __restrict__ parts, int32_t nparts, int64_t n,
+    Acc* __restrict__ out) {
+  combine_parts_body(*Pd, parts, nparts, n, out);
+}
+
+void kept_dims(const cubed_program_t& P, int& kd0, int& kd1) {
+  const bool a = (P.mode & 3) == 0;
+  kd0 = a ? P.nred : 0;
+  kd1 = a ? P.ndim : P.ndim - P.nred;
+}
+
+int launch_collect(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
+                   const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws_base,
+                   hipStream_t st) {
+  int kd0, kd1;
+  kept_dims(P, kd0, kd1);
+  const int64_t n = ntasks * max_kept;
+  hipLaunchKernelGGL(k_collect, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, dP, d_tasks,
+                     ntasks, max_kept, L.nsplit, (const Acc*)(ws_base + L.soa_elems), ws_base, kd0, kd1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
 // Split factor for a reduction whose un-split grid has `base` workgroups:
 // enough workgroups to fill the chip (`resident` = 256 CUs x 8 resident
 // 256-thread groups at the specialised kernels' occupancy), rounded so the
@@ -106,7 +144,11 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     }
     L.blocks = ntasks * max_kept * L.nsplit;
   }
-  L.ws_bytes = L.nsplit > 1 ? (int64_t)L.nsplit * ntasks * max_kept * P->nfields * (int64_t)sizeof(Acc) : 0;
+  const bool partials = (P->mode & CUBED_MODE_PARTIALS) != 0;
+  L.soa_elems = partials ? (int64_t)P->nfields * ntasks * max_kept : 0;
+  L.ws_bytes = (L.nsplit > 1 || partials)
+                   ? (L.soa_elems + (int64_t)L.nsplit * ntasks * max_kept * P->nfields) * (int64_t)sizeof(Acc)
+                   : 0;
   return L;
 }
 
@@ -143,6 +185,7 @@ int check_program(const cubed_program_t& P) {
     set_err("cubed_fused_chunks: program header out of range");
     return CUBED_E_ARG;
   }
+  if ((P.mode & CUBED_MODE_PARTIALS) && P.nfields == 0) { set_err("cubed_fused_chunks: partials mode needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & 3) == 1 && P.nfields == 0) { set_err("cubed_fused_chunks: kernel B needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & CUBED_MODE_STREAM) &&
       ((P.mode & 3) != 0 || !(P.mode & 4) || P.nred > 1 || P.ndim != P.nred + 1 || P.nleaves < 1)) {
@@ -185,7 +228,7 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
     return CUBED_E_WORKSPACE;
   }
   hipStream_t st = (hipStream_t)stream;
-  Acc* ws = (Acc*)d_workspace;
+  Acc* ws = (Acc*)d_workspace + L.soa_elems;  // partials mode: SoA block first
   switch (P.vtype) {
     case CUBED_V_F32: launch_fused<float>(P, d_prog, L, d_tasks, ntasks, max_kept, ws, st); break;
     case CUBED_V_F64: launch_fused<double>(P, d_prog, L, d_tasks, ntasks, max_kept, ws, st); break;
@@ -194,6 +237,8 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
+  if (P.mode & CUBED_MODE_PARTIALS)
+    return launch_collect(P, d_prog, L, d_tasks, ntasks, max_kept, (Acc*)d_workspace, st);
   if (L.nsplit > 1) {
     const int kd0 = (L.kernel == 0) ? P.nred : 0;
     const int kd1 = (L.kernel == 0) ? P.ndim : P.ndim - P.nred;
@@ -203,6 +248,36 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
     e = hipGetLastError();
     if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   }
+  return 0;
+}
+
+extern "C" int cubed_fused_finish(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                  const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                                  const void* d_partials, void* stream) {
+  if (!prog || !d_prog || !d_partials || (!d_tasks && ntasks > 0)) { set_err("cubed_fused_finish: null argument"); return CUBED_E_ARG; }
+  if (ntasks == 0) return 0;
+  if (int rc = check_program(*prog)) return rc;
+  if (prog->nfields == 0 || max_kept <= 0) { set_err("cubed_fused_finish: not a reduction"); return CUBED_E_ARG; }
+  int kd0, kd1;
+  kept_dims(*prog, kd0, kd1);
+  const int64_t n = ntasks * max_kept;
+  hipLaunchKernelGGL(k_finish_soa, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_prog, d_tasks, ntasks, max_kept, (const Acc*)d_partials, kd0, kd1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+extern "C" int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                      const void* d_parts, int32_t nparts, int64_t n, void* d_out,
+                                      void* stream) {
+  if (!prog || !d_prog || !d_parts || !d_out || nparts < 1 || n < 0) { set_err("cubed_combine_partials: bad argument"); return CUBED_E_ARG; }
+  if (n == 0) return 0;
+  if (prog->nfields < 1 || prog->nfields > CUBED_MAX_FIELDS) { set_err("cubed_combine_partials: not a reduction"); return CUBED_E_ARG; }
+  hipLaunchKernelGGL(k_combine_parts, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_prog, (const Acc*)d_parts, nparts, n, (Acc*)d_out);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   return 0;
 }
 

@@ -94,6 +94,7 @@ struct LaunchPlan {
   int vec;        // 1 or 4
   int64_t bpt;    // A: blocks per task per split
   int32_t nsplit;
+  int64_t soa_elems;  // partials mode: SoA per-field partials at the workspace start
   int64_t ws_bytes;
   int64_t blocks;
 };
@@ -105,7 +106,11 @@ void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const La
 
 dim3 grid_of(int64_t blocks);
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept, int64_t max_red);
-int check_program(const cubed_program_t& P);  // 0 or a CUBED_E_* code (message set)
+int check_program(const cubed_program_t& P);
+void kept_dims(const cubed_program_t& P, int& kd0, int& kd1);
+int launch_collect(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
+                   const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws_base,
+                   hipStream_t st);  // 0 or a CUBED_E_* code (message set)
 void set_error(const char* msg);
 
 #endif  // __HIPCC_RTC__

@@ -127,7 +127,7 @@ CUBED_DEV void fused_a_body(
     // reduced coordinates of r0 (odometer over dims [0, nr))
     int64_t cr[CUBED_MAX_DIMS];
     int64_t roff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-    {
+    if (r1 > r0) {  // (an empty task -- a rank without chunks of this block -- has extent 0)
       int64_t rr = r0;
 #pragma unroll
       for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
@@ -166,7 +166,7 @@ CUBED_DEV void fused_a_body(
         }
       }
     }
-    if (nsplit == 1) {
+    if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
       finish<VEC>(P, T, acc, ooff);
     } else {
       Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + kflat) * P.nfields;
@@ -275,7 +275,7 @@ CUBED_DEV void fused_b_body(
       for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
       fin[f][0] = x;
     }
-    if (nsplit == 1) {
+    if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
       finish<1>(P, T, fin, ooff);
     } else {
       Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + k) * P.nfields;
@@ -313,6 +313,78 @@ CUBED_DEV void finalize_body(
     fin[f][0] = x;
   }
   finish<1>(P, T, fin, ooff);
+}
+
+// ---------------------------------------------------------------- partials (multi-GPU)
+// CUBED_MODE_PARTIALS: the reduce kernels above always leave their
+// accumulators in the split workspace; collect_body combines the splits (in
+// split order) and writes one SoA block per field, soa[f][t][k], with the
+// reduction identity in the padding k >= nk of edge tasks, so every rank's
+// block has the same layout and can be summed / gathered by RCCL.
+CUBED_DEV void collect_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, Acc* __restrict__ soa,
+    int kd0, int kd1) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t t = i / max_kept, k = i % max_kept;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  int64_t nk = 1;
+  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+  const int64_t n = ntasks * max_kept;
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+    Acc x = acc_init(P.field_rop[f], P.field_acc[f]);
+    if (k < nk) {
+      x = ws[(t * max_kept + k) * P.nfields + f];
+      for (int s = 1; s < nsplit; ++s)
+        x = acc_combine(x, ws[(((int64_t)s * ntasks + t) * max_kept + k) * P.nfields + f],
+                        P.field_rop[f], P.field_acc[f]);
+    }
+    soa[f * n + i] = x;
+  }
+}
+
+// Epilogue + store from combined SoA partials (the last step of a reduction
+// whose partials were combined across GPUs).
+CUBED_DEV void finish_soa_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, int kd0, int kd1) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t t = i / max_kept, k = i % max_kept;
+  if (t >= ntasks) return;
+  const cubed_task_t* __restrict__ T = tasks + t;
+  int64_t nk = 1;
+  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+  if (k >= nk) return;
+  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t kk = k;
+  for (int d = kd1 - 1; d >= kd0; --d) {
+    int64_t q, c;
+    divmod64(kk, T->extent[d], q, c);
+    kk = q;
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
+  }
+  const int64_t n = ntasks * max_kept;
+  Acc fin[CUBED_MAX_FIELDS][1];
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    fin[f][0] = f < P.nfields ? soa[f * n + i] : acc_init(CUBED_R_NONE, 0);
+  finish<1>(P, T, fin, ooff);
+}
+
+// Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in
+// part order: out[f][i] = part0 (+) part1 (+) ...  Used for the fields RCCL
+// cannot reduce with numpy's semantics (max/min with NaN, prod, any/all).
+CUBED_DEV void combine_parts_body(const cubed_program_t& P, const Acc* __restrict__ parts,
+                                  int32_t nparts, int64_t n, Acc* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t block = (int64_t)P.nfields * n;
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+    Acc x = parts[f * n + i];
+    for (int r = 1; r < nparts; ++r)
+      x = acc_combine(x, parts[r * block + f * n + i], P.field_rop[f], P.field_acc[f]);
+    out[f * n + i] = x;
+  }
 }
 
 // ---------------------------------------------------------------- streaming fast path
@@ -445,7 +517,7 @@ CUBED_DEV void stream_body(
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[f][j].i += r1 - r0;
 
-    if (nsplit == 1) {
+    if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
       finish<4>(P, T, acc, ooff);
     } else {
       Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept + k) * P.nfields;

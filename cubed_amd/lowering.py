@@ -624,7 +624,7 @@ class Lowerer:
         return self.ctx.device_source(proxy.array)
 
     def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
-                            rows_fn=None, sample_key=None):
+                            rows_fn=None, sample_key=None, partials=False):
         """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
         ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
         per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
@@ -779,6 +779,10 @@ class Lowerer:
         P.mode = layout.mode
         if _stream_ok(layout, leaves, kinds, P.vtype):
             P.mode |= MODE_STREAM
+        if partials:
+            if P.nfields == 0:
+                raise LoweringError("partials mode needs a reduction")
+            P.mode |= MODE_PARTIALS
         table = layout.table(self.ctx.device)
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
         return FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
@@ -1147,6 +1151,7 @@ def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout
 
 
 MODE_STREAM = 8  # include/cubed_amd.h CUBED_MODE_STREAM
+MODE_PARTIALS = 16  # include/cubed_amd.h CUBED_MODE_PARTIALS
 _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64: np.dtype(np.int64)}
 
 

@@ -1,0 +1,125 @@
+"""Inter-GPU communication for the multi-GPU executor.
+
+The reference has no collective layer: every byte between tasks moves
+through shared Zarr storage (cubed/core/plan.py:44-48).  On one
+MI355X node the executor runs one process per GPU and moves chunks over
+xGMI with RCCL (torch.distributed's "nccl" backend is RCCL on ROCm):
+
+* ``all_to_all`` -- the chunk exchange of rechunk and of any pipeline whose
+  tasks read chunks owned by another rank (one ``all_to_all_single`` of a
+  packed byte buffer, issued on torch's current stream, so it is ordered
+  with the pack/unpack kernels around it);
+* ``reduce`` / ``all_reduce`` -- the final combine round of a reduction
+  (SUM of f64 totals / i64 counts);
+* ``all_gather`` -- partials whose combine RCCL cannot express with numpy's
+  semantics (max/min with NaN, prod, any/all), folded afterwards by
+  ``cubed_combine_partials`` in rank order;
+* ``broadcast`` -- assembling a computed result on every rank.
+
+With the ``gloo`` backend (CPU tests, or several ranks sharing one GPU in a
+test) device tensors are staged through host memory; the data path is
+otherwise identical.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+
+class Comm:
+    """A process group plus the backend-specific tensor plumbing."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("Comm needs an initialised torch.distributed process group")
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = str(dist.get_backend(group)).lower()
+        self.staged = self.backend == "gloo"
+
+    # -- helpers --------------------------------------------------------------
+    def _stage(self, t):
+        if self.staged and t.device.type != "cpu":
+            return t.cpu(), True
+        return t, False
+
+    def _unstage(self, host, dev, staged):
+        if staged:
+            dev.copy_(host)
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+    # -- collectives ------------------------------------------------------------
+    def all_to_all(self, recv, send, recv_splits: Sequence[int], send_splits: Sequence[int]):
+        """Byte exchange: rank r's ``send[sum(send_splits[:j]) : +send_splits[j]]``
+        lands in rank j's ``recv`` at ``sum(recv_splits[:r])``."""
+        rs, ss = list(map(int, recv_splits)), list(map(int, send_splits))
+        send, recv = send[:sum(ss)], recv[:sum(rs)]  # buffers may carry padding
+        s, _ = self._stage(send)
+        r, staged = self._stage(recv)
+        self.dist.all_to_all_single(r, s, rs, ss, group=self.group)
+        self._unstage(r, recv, staged)
+
+    def all_reduce_sum(self, t):
+        h, staged = self._stage(t)
+        self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+        self._unstage(h, t, staged)
+
+    def reduce_sum(self, t, dst: int):
+        h, staged = self._stage(t)
+        self.dist.reduce(h, dst=self._global(dst), op=self.dist.ReduceOp.SUM, group=self.group)
+        if self.rank == dst:
+            self._unstage(h, t, staged)
+
+    def all_gather(self, out, t):
+        """``out`` (world * t.numel() elements) receives every rank's ``t`` in
+        rank order."""
+        h, _ = self._stage(t)
+        o, staged = self._stage(out)
+        self.dist.all_gather_into_tensor(o, h, group=self.group)
+        self._unstage(o, out, staged)
+
+    def broadcast(self, t, src: int):
+        h, staged = self._stage(t)
+        self.dist.broadcast(h, src=self._global(src), group=self.group)
+        if self.rank != src:
+            self._unstage(h, t, staged)
+
+    def all_ok(self, ok: bool) -> bool:
+        """True iff every rank passes True (plan-time agreement, e.g. whether
+        a reduction chain could be fused on all ranks)."""
+        import torch
+
+        dev = "cpu" if self.staged else "cuda"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(t.item())
+
+    def _global(self, r: int) -> int:
+        if self.group is None:
+            return r
+        return self.dist.get_global_rank(self.group, r)
+
+
+def default_comm() -> Optional[Comm]:
+    """The world process group when torch.distributed runs with > 1 rank."""
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover
+        return None
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return Comm()
+    return None
+
+
+def splits_to_offsets(splits: List[int]) -> List[int]:
+    out, o = [], 0
+    for s in splits:
+        out.append(o)
+        o += s
+    return out

@@ -1,0 +1,234 @@
+"""Multi-GPU pieces of the MI355X executor (one process per GPU, RCCL).
+
+The reference scales by mapping independent tasks onto workers that share
+Zarr storage (runtime/executors/python_async.py:121-142, lithops.py); here
+each GPU owns a block-cyclic share of every array's chunks
+(cubed_amd/storage.py) and runs the tasks whose output chunk it owns.  Data
+crosses GPUs only where a task reads a chunk it does not own:
+
+* ``FetchLaunch``   -- whole chunks read by local tasks but owned elsewhere
+  (pack -> RCCL all-to-all -> the task views point into the receive buffer);
+* ``RechunkLaunch`` -- rechunk: local pieces copied in place, the rest packed,
+  exchanged with one all-to-all and unpacked into the target chunks;
+* ``PartialsLaunch``-- a fused reduction chain whose inputs are spread over
+  the ranks: every rank reduces its own chunks to per-field partials
+  (CUBED_MODE_PARTIALS), RCCL reduces them (SUM fields) or all-gathers them
+  (max/min/prod/any/all, folded in rank order by cubed_combine_partials), and
+  the owner(s) of the output run the epilogue (cubed_fused_finish).
+
+Every rank walks the same DAG in the same order and derives the same plans
+from chunk geometry alone, so the collectives always match.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ... import _native as nat
+from ...lowering import Box, CopyLaunch
+from ...storage import DeviceArray, c_strides
+from ..exchange import FetchExchange, RechunkExchange
+
+FETCH_ROW = 4096  # bytes per row of a whole-chunk pack copy (one wave moves 4 KiB)
+
+
+def _round(n, a):
+    return (n + a - 1) // a * a
+
+
+def chunk_nbytes(arr: DeviceArray, coords, field) -> int:
+    return math.prod(arr.chunk_extent(coords)) * arr.field_dtype(field).itemsize
+
+
+def _flat_boxes(pairs):
+    """Contiguous byte copies (src, dst, nbytes: a multiple of 256 that never
+    runs past the source slot) as 4 KiB-row boxes plus a tail row."""
+    boxes = []
+    for src, dst, nb in pairs:
+        rows, tail = divmod(nb, FETCH_ROW)
+        if rows:
+            boxes.append(Box(src, dst, [rows, FETCH_ROW], [FETCH_ROW, 1], [FETCH_ROW, 1]))
+        if tail:
+            o = rows * FETCH_ROW
+            boxes.append(Box(src + o, dst + o, [1, tail], [tail, 1], [tail, 1]))
+    return boxes
+
+
+class FetchLaunch:
+    """Brings the remote chunks one pipeline reads into a local buffer."""
+
+    def __init__(self, ctx, plan: FetchExchange, arrays: Dict[str, DeviceArray]):
+        import torch
+
+        self.ctx = ctx
+        self.plan = plan
+        self.send = torch.empty(max(sum(plan.send_splits), 16), dtype=torch.uint8, device=ctx.device)
+        self.recv = torch.empty(max(sum(plan.recv_splits), 16), dtype=torch.uint8, device=ctx.device)
+        sbase, rbase = self.send.data_ptr(), self.recv.data_ptr()
+        pairs = []
+        for lst in plan.send:
+            for (name, coords, field), off, nb in lst:
+                arr = arrays[name]
+                pairs.append((arr.chunk_addr(coords, field), sbase + off, nb))
+        self.pack = CopyLaunch(_flat_boxes(pairs), 1, ctx.device)
+        # remote chunk maps, installed on the arrays while the pipeline lowers
+        self.remote: Dict[str, Dict] = {}
+        for lst in plan.recv:
+            for (name, coords, field), off, nb in lst:
+                self.remote.setdefault(name, {})[(tuple(coords), field)] = rbase + off
+
+    def run(self, stream):
+        self.pack.run(stream)
+        self.ctx.comm.all_to_all(self.recv, self.send, self.plan.recv_splits, self.plan.send_splits)
+
+
+class RechunkLaunch:
+    """copy_read_to_write over all target chunks owned here."""
+
+    def __init__(self, ctx, plan: RechunkExchange, src: DeviceArray, dst: DeviceArray,
+                 src_replicated: bool):
+        import torch
+
+        self.ctx = ctx
+        self.plan = plan
+        isz = dst.dtype.itemsize
+        self.send = torch.empty(max(plan.send_bytes, 16), dtype=torch.uint8, device=ctx.device)
+        self.recv = torch.empty(max(plan.recv_bytes, 16), dtype=torch.uint8, device=ctx.device)
+        sbase, rbase = self.send.data_ptr(), self.recv.data_ptr()
+
+        def src_box(p):
+            ext = src.chunk_extent(p.src)
+            st = c_strides(ext)
+            return src.chunk_addr(p.src) + sum(a * s for a, s in zip(p.src_start, st)) * isz, list(st)
+
+        def dst_box(p):
+            ext = dst.chunk_extent(p.dst)
+            st = c_strides(ext)
+            return dst.chunk_addr(p.dst) + sum(a * s for a, s in zip(p.dst_start, st)) * isz, list(st)
+
+        local, pack, unpack = [], [], []
+        for p in plan.local:
+            s, ss = src_box(p)
+            d, ds = dst_box(p)
+            local.append(Box(s, d, list(p.extent), ss, ds))
+        for lst in plan.send:
+            for p, off in lst:
+                s, ss = src_box(p)
+                pack.append(Box(s, sbase + off, list(p.extent), ss, list(c_strides(p.extent))))
+        for lst in plan.recv:
+            for p, off in lst:
+                d, ds = dst_box(p)
+                unpack.append(Box(rbase + off, d, list(p.extent), list(c_strides(p.extent)), ds))
+        self.local = CopyLaunch(local, isz, ctx.device)
+        self.pack = CopyLaunch(pack, isz, ctx.device)
+        self.unpack = CopyLaunch(unpack, isz, ctx.device)
+        self.exchange = any(plan.send_splits) or any(plan.recv_splits)
+        self.collective = True  # every rank takes part, even with nothing to move
+
+    def run(self, stream):
+        self.pack.run(stream)
+        self.ctx.comm.all_to_all(self.recv, self.send, self.plan.recv_splits, self.plan.send_splits)
+        self.local.run(stream)
+        self.unpack.run(stream)
+
+
+SUM_ROPS = {"sum", "nansum", "count", "count_nonnan"}
+
+
+class PartialsLaunch:
+    """Cross-rank combine + epilogue of a reduction chain run in partials
+    mode (the FusedLaunch before it leaves SoA partials in its workspace)."""
+
+    def __init__(self, ctx, fused, rops: List[str], acc_int: List[bool], owners: List[int]):
+        import torch
+
+        self.ctx = ctx
+        self.fused = fused
+        self.nf = len(rops)
+        self.n = fused.ntasks * fused.max_kept
+        self.sum_only = all(r in SUM_ROPS for r in rops)
+        self.acc_int = acc_int
+        owners = sorted(set(owners))
+        # one owner for every output block (e.g. a full reduction): RCCL reduce
+        # to it; otherwise all-reduce and every rank finishes its own blocks
+        self.root = owners[0] if len(owners) == 1 else None
+        self.finish_here = ctx.rank in owners
+        if not self.sum_only:
+            self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8,
+                                        device=ctx.device)
+
+    def soa(self):
+        return self.fused.ws[: self.nf * self.n * 8]
+
+    def field_view(self, f):
+        import torch
+
+        raw = self.fused.ws[f * self.n * 8:(f + 1) * self.n * 8]
+        return raw.view(torch.int64 if self.acc_int[f] else torch.float64)
+
+    def run(self, stream):
+        comm = self.ctx.comm
+        L = nat.lib()
+        if self.sum_only:
+            for f in range(self.nf):
+                v = self.field_view(f)
+                if self.root is not None:
+                    comm.reduce_sum(v, self.root)
+                else:
+                    comm.all_reduce_sum(v)
+        else:
+            comm.all_gather(self.gathered, self.soa())
+            if self.finish_here:
+                nat.check(L.cubed_combine_partials(self.fused.prog, self.fused.d_prog.data_ptr(),
+                                                   self.gathered.data_ptr(), comm.world, self.n,
+                                                   self.fused.ws.data_ptr(), stream),
+                          "cubed_combine_partials")
+        if self.finish_here:
+            nat.check(L.cubed_fused_finish(self.fused.prog, self.fused.d_prog.data_ptr(),
+                                           self.fused.table.data_ptr(), self.fused.ntasks,
+                                           self.fused.max_kept, self.fused.ws.data_ptr(), stream),
+                      "cubed_fused_finish")
+
+
+def gather_distributed(arr: DeviceArray) -> np.ndarray:
+    """Assemble a block-cyclically stored array on every rank: each rank
+    broadcasts its slab (all its chunks), then chunks are decoded on the
+    host.  Used to return compute() results, not on the hot path."""
+    import itertools
+
+    import torch
+
+    comm = arr.comm
+    out = np.empty(arr.shape, dtype=arr.dtype)
+    if arr.size == 0:
+        return out
+    torch.cuda.synchronize(arr.device)
+    for r in range(arr.world):
+        nslots = (arr.nchunks - r + arr.world - 1) // arr.world if arr.nchunks > r else 0
+        if nslots == 0:
+            continue
+        for f in arr.fields:
+            nb = nslots * arr.slot_bytes(f)
+            if r == arr.rank:
+                buf = arr.slabs[f][:nb].clone()
+            else:
+                buf = torch.empty(nb, dtype=torch.uint8, device=arr.device)
+            comm.broadcast(buf, r)
+            host = buf.cpu().numpy()
+            dt = arr.field_dtype(f)
+            for coords in itertools.product(*[range(n) for n in arr.numblocks]):
+                if arr.chunk_offset(coords) % arr.world != r:
+                    continue
+                slot = arr.chunk_offset(coords) // arr.world
+                ext = arr.chunk_extent(coords)
+                start = slot * arr.slot_bytes(f)
+                vals = host[start:start + math.prod(ext) * dt.itemsize].view(dt).reshape(ext)
+                sl = tuple(slice(s, s + e) for s, e in zip(arr.chunk_start(coords), ext))
+                if f is None:
+                    out[sl] = vals
+                else:
+                    out[f][sl] = vals
+    return out

@@ -67,6 +67,10 @@ HBM_BYTES_PER_GPU = 288 * 10**9
 def gather_to_host(arr: DeviceArray) -> np.ndarray:
     import torch
 
+    if arr.world > 1:
+        from .dist import gather_distributed
+
+        return gather_distributed(arr)
     torch.cuda.synchronize(arr.device)
     return arr.to_numpy()
 
@@ -119,7 +123,11 @@ class _Upload:
 class GpuDagExecutor(DagExecutor):
     """Runs Cubed plans on one MI355X (one process per GPU)."""
 
-    def __init__(self, device=None, stream=None, check_memory: bool = True):
+    def __init__(self, device=None, stream=None, check_memory: bool = True, comm="auto"):
+        """``comm``: a ``cubed_amd.runtime.comm.Comm`` for multi-GPU execution
+        (one process per GPU; every rank runs the same plan), ``None`` for a
+        single GPU, or "auto" = the torch.distributed world group when it has
+        more than one rank."""
         import torch
 
         if not torch.cuda.is_available():
@@ -127,6 +135,15 @@ class GpuDagExecutor(DagExecutor):
         nat.lib()
         self._init_state(torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}"),
                          stream, check_memory)
+        if comm == "auto":
+            from ..comm import default_comm
+
+            comm = default_comm()
+        self.set_comm(comm)
+
+    def set_comm(self, comm):
+        self.comm = comm
+        self.rank, self.world = (comm.rank, comm.world) if comm is not None else (0, 1)
 
     def _init_state(self, device, stream, check_memory):
         self.device = device
@@ -136,10 +153,12 @@ class GpuDagExecutor(DagExecutor):
         self._uploads: Dict[int, DeviceArray] = {}
         self._scratch: List = []
         self.lowerer = Lowerer(self)
+        self.comm = None
         self.rank, self.world = 0, 1
         self.timing: Optional[LaunchTimer] = None
         self.fuse_reductions = True
         self._chains: Dict = {}
+        self._agreed = set()
         self.elided = set()
 
     # -- plumbing used by the lowerer ------------------------------------------
@@ -154,6 +173,7 @@ class GpuDagExecutor(DagExecutor):
     def allocate(self, t: DeviceArray):
         if not t.allocated:
             t.allocate(self.device, self.rank, self.world)
+            t.comm = self.comm
 
     def device_source(self, arr):
         """A readable device-side representation of an input array."""
@@ -169,7 +189,7 @@ class GpuDagExecutor(DagExecutor):
             if d is None:
                 d = DeviceArray(arr.shape, arr.dtype, arr.chunks if arr.ndim else (),
                                 name=f"virtual-{key}")
-                self.allocate(d)
+                d.allocate(self.device, 0, 1)  # small constants: replicated on every rank
                 if isinstance(arr, VirtualFullArray):
                     self._fill(d, arr.fill_value)
                 else:
@@ -200,6 +220,11 @@ class GpuDagExecutor(DagExecutor):
 
     def scratch(self, nbytes: int) -> int:
         import torch
+
+        from ...storage import _GEOMETRY_ONLY
+
+        if _GEOMETRY_ONLY[0]:
+            return 0
 
         buf = torch.empty(max(nbytes, 16) + 256, dtype=torch.uint8, device=self.device)
         self._scratch.append(buf)
@@ -271,11 +296,8 @@ class GpuDagExecutor(DagExecutor):
                 raise LoweringError(
                     f"op {name}: {program.func!r} cannot run on the MI355X executor "
                     "(not expressible as a fused chunk program)")
-            if isinstance(program, ir.ExprProgram):
-                launch = self.lowerer.lower_expr_pipeline(program, cfg, target, keys)
-                return _with_gathers(launch, self.device)
-            if isinstance(program, (ir.MatmulProgram, ir.TensordotProgram)):
-                return [self._lower_gemm(program, cfg, target, keys)]
+            if isinstance(program, (ir.ExprProgram, ir.MatmulProgram, ir.TensordotProgram)):
+                return self._lower_part(program, cfg, target, keys)
             if isinstance(program, ir.GemmThenProgram):
                 from types import SimpleNamespace
 
@@ -285,21 +307,113 @@ class GpuDagExecutor(DagExecutor):
                 self.allocate(gt)
                 gcfg = SimpleNamespace(block_function=program.gemm_block_function,
                                        reads_map=program.gemm_reads)
-                launches = [self._lower_gemm(program.gemm, gcfg, gt, self._task_keys(gt))]
+                launches = self._lower_part(program.gemm, gcfg, gt, self._task_keys(gt))
                 if not isinstance(program.then, ir.ExprProgram):
                     raise LoweringError(f"op {name}: GEMM consumer {program.then!r} is not lowerable")
                 tcfg = SimpleNamespace(block_function=program.then_block_function,
                                        reads_map={gt.name: CubedArrayProxy(gt, gt.chunks)},
                                        write=cfg.write)
-                launch = self.lowerer.lower_expr_pipeline(program.then, tcfg, target, keys)
-                return launches + _with_gathers(launch, self.device)
+                return launches + self._lower_part(program.then, tcfg, target, keys)
             raise LoweringError(f"op {name}: unsupported program {type(program).__name__}")
         raise LoweringError(f"op {name}: unknown stage function {getattr(fn, '__name__', fn)}")
+
+    # -- one blockwise part: (fetch of remote inputs) + its launch --------------
+    def _lower_part(self, program, cfg, target, keys):
+        """Launches of one blockwise program over the tasks this rank owns.
+        With several GPUs, chunks the owned tasks read from other ranks are
+        fetched first (FetchLaunch) and the task views point at the copies."""
+        if self.world == 1:
+            return self._lower_local(program, cfg, target, keys)
+        owned = [k for k in keys if target.owner(k) == self.rank]
+        fetch, arrays = self._plan_fetch(
+            {k: target.owner(k) for k in keys},
+            lambda k: self._task_reads(program, cfg, k))
+        out = [fetch] if fetch is not None else []
+        if not owned:
+            return out
+        with _remote_chunks(fetch, arrays):
+            out += self._lower_local(program, cfg, target, owned)
+        return out
+
+    def _lower_local(self, program, cfg, target, keys):
+        if isinstance(program, ir.ExprProgram):
+            return _with_gathers(self.lowerer.lower_expr_pipeline(program, cfg, target, keys), self.device)
+        return [self._lower_gemm(program, cfg, target, keys)]
+
+    def _task_reads(self, program, cfg, key):
+        """(array, chunk coords, field) of every distributed chunk one task
+        reads (the apply_blockwise key resolution, primitive/blockwise.py
+        :70-76, plus map_direct regions)."""
+        from ...lowering import collect_leaves, program_exprs, region_pieces
+        from ...utils import flatten_keys
+
+        args = cfg.block_function(("out",) + tuple(key))
+        args = [list(a) if not isinstance(a, (tuple, list, str)) else a for a in args]
+        out = []
+
+        def add_key(k, field):
+            src = self.device_source(cfg.reads_map[k[0]].array)
+            if isinstance(src, DeviceArray) and src.world > 1:
+                out.append((src, tuple(k[1:]), field))
+
+        if isinstance(program, (ir.MatmulProgram, ir.TensordotProgram)):
+            for a in args[:2]:
+                for k in ([a] if isinstance(a, tuple) else flatten_keys(a)):
+                    add_key(k, None)
+            return out
+        outs, fields = program_exprs(program)
+        for leaf in collect_leaves(outs + fields):
+            if isinstance(leaf, ir.Arg):
+                a = args[leaf.index]
+                if isinstance(a, str):
+                    continue
+                for k in ([a] if isinstance(a, tuple) else flatten_keys(a)):
+                    add_key(k, leaf.field)
+            elif isinstance(leaf, ir.Region):
+                src = self.device_source(leaf.target)
+                if isinstance(src, DeviceArray) and src.world > 1:
+                    block_id = tuple(args[leaf.block_arg][1:])
+                    for coords, _, _ in region_pieces(src, leaf.region(block_id)):
+                        out.append((src, tuple(coords), leaf.field))
+        return out
+
+    def _plan_fetch(self, task_owner, reads_of):
+        """FetchLaunch for the remote chunks of a set of tasks ({key: owner
+        rank}), or None when no rank reads a chunk it does not own."""
+        from ..exchange import plan_fetch
+        from .dist import FetchLaunch, chunk_nbytes
+
+        needs: Dict[int, set] = {}
+        arrays: Dict[str, DeviceArray] = {}
+        remote = False
+        for key, r in task_owner.items():
+            for arr, coords, field in reads_of(key):
+                if arr.name is None:
+                    raise LoweringError("distributed arrays need names")
+                prev = arrays.setdefault(arr.name, arr)
+                if prev is not arr:
+                    raise LoweringError(f"two arrays named {arr.name}")
+                needs.setdefault(r, set()).add((arr.name, coords, field))
+                remote = remote or arr.owner(coords) != r
+        if not remote:
+            return None, arrays
+        plan = plan_fetch(needs, lambda ref: arrays[ref[0]].owner(ref[1]),
+                          lambda ref: chunk_nbytes(arrays[ref[0]], ref[1], ref[2]),
+                          self.rank, self.world)
+        return FetchLaunch(self, plan, arrays), arrays
 
     def _lower_rechunk(self, cfg):
         src = self.device_source(cfg.read.array)
         dst = cfg.write.array
         self.allocate(dst)
+        if self.world > 1:
+            from ..exchange import plan_rechunk
+            from .dist import RechunkLaunch
+
+            replicated = src.world == 1
+            plan = plan_rechunk(src, dst, self.rank, self.world, dst.dtype.itemsize,
+                                src_world=1 if replicated else self.world)
+            return RechunkLaunch(self, plan, src, dst, replicated)
         boxes: List[Box] = []
         for key in self._task_keys(dst):
             region = tuple(slice(s, s + e) for s, e in zip(dst.chunk_start(key), dst.chunk_extent(key)))
@@ -340,7 +454,17 @@ class GpuDagExecutor(DagExecutor):
         entry = self._cache.get(id(pipeline))
         if entry is not None and entry[0]() is pipeline:
             return entry[1]
-        launches = self.lower_node(name, node)
+        err = None
+        try:
+            launches = self.lower_node(name, node)
+        except LoweringError as e:
+            err = e
+        if self.world > 1 and not self.comm.all_ok(err is None):
+            # a pipeline that cannot be lowered on one rank fails on all of them
+            # (instead of leaving the others waiting in a collective)
+            raise err or LoweringError(f"op {name} could not be lowered on another rank")
+        if err is not None:
+            raise err
         self._cache[id(pipeline)] = (weakref.ref(pipeline), launches)
         return launches
 
@@ -376,12 +500,53 @@ class GpuDagExecutor(DagExecutor):
         target = chain.final_target
         self.allocate(target)
         keys = self._task_keys(target)
+        if self.world > 1:
+            launches = self._compiled_chain_dist(chain, target, keys)
+            self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
+            return launches
         launch = self.lowerer.lower_expr_pipeline(
             chain.program, chain.first_spec, target, keys,
             rows_fn=lambda leaves, kinds: chain_rows(self.lowerer, chain, leaves, kinds, keys),
             sample_key=contributing_keys(chain, keys[0])[0])
         launches = _with_gathers(launch, self.device)
         self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
+        return launches
+
+    def _compiled_chain_dist(self, chain, target, keys):
+        """A reduction chain over chunks spread across the ranks: each rank
+        reduces the first-level tasks it owns (the chunks of the chain's
+        input it holds) for EVERY output block into SoA partials; RCCL then
+        combines the partials and the owners run the epilogue
+        (dist.PartialsLaunch).  Same fields and composition as the 1-GPU
+        chain, with the sum over ranks as the outermost association."""
+        from ...chains import chain_rows, contributing_keys
+        from .dist import PartialsLaunch
+
+        first = chain.first_target
+        world, rank = self.world, self.rank
+
+        def first_owner(t):
+            return first.chunk_offset(t) % world
+
+        contrib = {K: contributing_keys(chain, K) for K in keys}
+        p1 = chain.first_spec.function
+        task_owner = {t: first_owner(t) for K in keys for t in contrib[K]}
+        fetch, arrays = self._plan_fetch(task_owner,
+                                         lambda t: self._task_reads(p1, chain.first_spec, t))
+        discard = self.scratch(max(target.slot_bytes(f) for f in target.fields))
+        select = {K: [t for t in contrib[K] if first_owner(t) == rank] for K in keys}
+        with _remote_chunks(fetch, arrays):
+            launch = self.lowerer.lower_expr_pipeline(
+                chain.program, chain.first_spec, target, keys,
+                rows_fn=lambda leaves, kinds: chain_rows(
+                    self.lowerer, chain, leaves, kinds, keys, select=select,
+                    out_owned=lambda K: target.owner(K) == rank, discard=discard),
+                sample_key=contrib[keys[0]][0], partials=True)
+        launches = [fetch] if fetch is not None else []
+        launches += _with_gathers(launch, self.device)
+        rops = [f.rop for f in chain.program.reduce.fields]
+        acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
+        launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys]))
         return launches
 
     def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
@@ -402,7 +567,16 @@ class GpuDagExecutor(DagExecutor):
                 else:
                     try:
                         launches = self.compiled_chain(ch)
+                        ok = True
                     except LoweringError:
+                        ok = False
+                    if self.world > 1 and (name, id(ch)) not in self._agreed:
+                        # every rank must take the same path (their collectives pair up)
+                        ok = self.comm.all_ok(ok)
+                        self._agreed.add((name, id(ch)))
+                        if not ok:
+                            self._cache.pop(("chain", id(ch.first_spec)), None)
+                    if not ok:
                         # not fusable after all: run the chain's pipelines one by one
                         chains.pop(name)
                         for m in ch.nodes[1:]:
@@ -447,6 +621,25 @@ class GpuDagExecutor(DagExecutor):
         if total > HBM_BYTES_PER_GPU:
             raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")
+
+
+class _remote_chunks:
+    """Installs a FetchLaunch's chunk copies on the arrays while one pipeline
+    is lowered (DeviceArray.chunk_addr resolves non-owned chunks to them)."""
+
+    def __init__(self, fetch, arrays):
+        self.fetch, self.arrays = fetch, arrays
+
+    def __enter__(self):
+        if self.fetch is not None:
+            for name, m in self.fetch.remote.items():
+                self.arrays[name].remote = m
+        return self
+
+    def __exit__(self, *exc):
+        for arr in self.arrays.values():
+            arr.remote = None
+        return False
 
 
 def _with_gathers(launch, device):

@@ -32,6 +32,23 @@ from .utils import (
 
 SLOT_ALIGN = 256  # bytes; keeps every chunk base 16-byte (dwordx4) aligned
 
+_GEOMETRY_ONLY = [False]
+
+
+class geometry_only:
+    """Context in which chunks owned by other ranks have address 0 instead of
+    raising: the multi-GPU executor uses it to derive the shape of a task it
+    does not run (its extents and strides), never to read through it."""
+
+    def __enter__(self):
+        self._prev = _GEOMETRY_ONLY[0]
+        _GEOMETRY_ONLY[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _GEOMETRY_ONLY[0] = self._prev
+        return False
+
 
 class ChunkGrid:
     """Geometry shared by all chunked targets."""
@@ -106,6 +123,10 @@ class DeviceArray(ChunkGrid):
         self.written = False
         self.device = None
         self.alias: Optional["DeviceArray"] = None  # same values, other chunking
+        # multi-GPU: fetched copies of chunks owned by other ranks, visible
+        # while the executor lowers one pipeline ((coords, field) -> address)
+        self.remote: Optional[Dict] = None
+        self.comm = None
 
     # -- layout ---------------------------------------------------------------
     def field_dtype(self, field: Optional[str]) -> np.dtype:
@@ -167,6 +188,12 @@ class DeviceArray(ChunkGrid):
 
     def chunk_addr(self, coords, field=None) -> int:
         if self.owner(coords) != self.rank:
+            if self.remote is not None:
+                a = self.remote.get((tuple(coords), field))
+                if a is not None:
+                    return a
+            if _GEOMETRY_ONLY[0]:
+                return 0
             raise KeyError(f"chunk {coords} of {self.name} is owned by rank {self.owner(coords)}")
         return self.base_addr(field) + self.local_slot(coords) * self.slot_bytes(field)
 

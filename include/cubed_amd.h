@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 3
+#define CUBED_ABI_VERSION 4
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -56,6 +56,7 @@ extern "C" {
 
 /* error codes (negative); positive values are hipError_t */
 #define CUBED_MODE_STREAM 8
+#define CUBED_MODE_PARTIALS 16
 
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)
@@ -141,6 +142,11 @@ typedef struct {
                                  /* an ARRAY in the vtype's own dtype       */
                                  /* (f32/f64/i64) with packed kept dim and  */
                                  /* reduced strides that are multiples of 4 */
+                                 /* +16 (CUBED_MODE_PARTIALS): reductions   */
+                                 /* stop before the epilogue and leave the  */
+                                 /* per-field accumulators as SoA partials  */
+                                 /* at the start of the workspace (see      */
+                                 /* cubed_fused_finish)                     */
   int32_t nleaves;
   uint8_t leaf_kind[CUBED_MAX_LEAVES];
   uint8_t leaf_dtype[CUBED_MAX_LEAVES];
@@ -211,6 +217,27 @@ int64_t cubed_fused_code_bytes(const void* handle);
 int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
                                     int64_t max_kept, int64_t max_red);
 
+/* Multi-GPU reductions (partials mode, CUBED_MODE_PARTIALS in prog->mode).
+ * cubed_fused_chunks / _compiled then stop before the epilogue: the first
+ * nfields*ntasks*max_kept*8 bytes of the workspace receive the per-field
+ * accumulators as SoA, partials[f][t][k] (f64 or i64 per field_acc, the
+ * reduction identity for k past an edge task's extent), identical in layout
+ * on every rank so they can be combined with RCCL.  Replaces the last
+ * combine round + aggregate of reduction (cubed/core/ops.py:849-892,
+ * _mean_combine/_mean_aggregate statistical_functions.py:61-100) when the
+ * round's inputs live on different GPUs.
+ * cubed_fused_finish runs the epilogue + stores of the same program from
+ * combined SoA partials (same task table, ntasks, max_kept).
+ * cubed_combine_partials folds nparts SoA blocks (nfields*n accumulators
+ * each, n = ntasks*max_kept, block r at r*nfields*n) in block order into
+ * d_out with the fields' own combine ops (used for max/min/prod/any/all,
+ * whose NaN semantics RCCL's reductions do not follow). */
+int cubed_fused_finish(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                       const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                       const void* d_partials, void* stream);
+int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                           const void* d_parts, int32_t nparts, int64_t n, void* d_out,
+                           void* stream);
 /* Fill ntasks chunks with numpy Generator(Philox(key)).random() doubles:
  * d_out[i] (device pointers) gets counts[i] doubles from key (lo,hi)[i].
  * All three tables are device arrays of ntasks entries. */

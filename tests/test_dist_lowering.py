@@ -1,0 +1,145 @@
+"""Lowering of the multi-GPU executor, checked on CPU for every rank of a
+world (DryExecutor with a FakeComm: the task tables and exchange plans each
+rank would launch, no launches and no collectives)."""
+
+import random
+
+import numpy as np
+import pytest
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.random as crandom
+from cubed_amd.core.plan import arrays_to_plan
+from cubed_amd.lowering import MODE_PARTIALS, MODE_STREAM, FusedLaunch
+from cubed_amd.runtime.executors.dist import FetchLaunch, PartialsLaunch, RechunkLaunch
+from dryrun import DryExecutor, FakeComm
+
+
+def _quad(dry, T=80):
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(1)
+    u = xp.astype(crandom.random((T, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((T, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=dry, array_names=[u.name, v.name])
+    dry.launched.clear()
+    m = xp.mean(u * v, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    return u, v, m
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_quad_means_partials_per_rank(built, world):
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        u, v, m = _quad(dry)
+        kinds = [type(l).__name__ for l in dry.launched]
+        assert kinds == ["FusedLaunch", "PartialsLaunch"], kinds
+        fused, part = dry.launched
+        P = fused.prog
+        assert P.mode & MODE_PARTIALS and P.mode & MODE_STREAM
+        # this rank's share of the 8 time chunks, read in place (slot stride)
+        mine = len([c for c in range(8) if c % world == rank])
+        assert fused.ntasks == 1 and fused.max_red == 10 * mine or (mine == 0 and fused.max_red == 1)
+        assert part.sum_only and part.root == 0 and part.finish_here == (rank == 0)
+        assert u.zarray.local_nslots() == mine
+
+
+def test_rechunk_is_one_exchange_per_rank(built):
+    world = 4
+    x = np.arange(60 * 50, dtype=np.float32).reshape(60, 50)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem=10**9, executor=dry)
+        a = cubed.from_array(x, chunks=(10, 50), spec=spec)
+        b = a.rechunk((60, 10))
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        arrays_to_plan(b).execute(executor=dry, resume=True, array_names=[b.name])
+        rl = [l for l in dry.launched if isinstance(l, RechunkLaunch)]
+        assert len(rl) == 1
+        plan = rl[0].plan
+        # 6 source x 5 target chunks: 10x10 f32 pieces, 400 B padded to 512
+        assert sum(plan.send_splits) == sum(512 for d in range(world) for _ in plan.send[d])
+        assert rl[0].local.nboxes == len(plan.local)
+
+
+def test_misaligned_elementwise_fetches(built):
+    world = 2
+    y = np.ones((60, 50), dtype=np.float32)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem=10**9, executor=dry)
+        p = cubed.from_array(y, chunks=(10, 50), spec=spec)
+        q = cubed.from_array(y, chunks=(10, 50), spec=spec)
+        arrays_to_plan(p, q).execute(executor=dry, array_names=[p.name, q.name])
+        dry.launched.clear()
+        s = p + q  # same grid: no fetch
+        arrays_to_plan(s).execute(executor=dry, resume=True, array_names=[s.name])
+        assert not [l for l in dry.launched if isinstance(l, FetchLaunch)]
+        f = [l for l in dry.launched if isinstance(l, FusedLaunch)]
+        assert f and f[0].ntasks == 3  # 6 chunks, block-cyclic over 2 ranks
+
+
+def test_max_uses_gather_combine(built):
+    world = 2
+    x = np.random.default_rng(0).random((40, 64))
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+        a = cubed.from_array(x, chunks=(10, 64), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        m = xp.max(a, axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        part = [l for l in dry.launched if isinstance(l, PartialsLaunch)]
+        assert part and not part[0].sum_only
+
+
+# ------------------------------------------------ collective order agreement
+
+
+def _launch_sequence(rank, world):
+    """Lower a mixed program on this rank (lowering-time agreement runs over
+    the real gloo group) and return the sequence of cross-rank launches."""
+    from cubed_amd.runtime.comm import Comm
+
+    dry = DryExecutor(Comm())
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    seq = []
+
+    def go(*arrs, resume=None):
+        dry.launched.clear()
+        arrays_to_plan(*arrs).execute(executor=dry, resume=resume, array_names=[a.name for a in arrs])
+        seq.append([type(l).__name__ for l in dry.launched
+                    if isinstance(l, (FetchLaunch, RechunkLaunch, PartialsLaunch))])
+
+    random.seed(4)
+    u = xp.astype(crandom.random((60, 24, 40), chunks=(10, 24, 40), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((60, 24, 40), chunks=(10, 24, 40), spec=spec), xp.float32)
+    go(u, v)
+    go(xp.mean(u * v, axis=0), resume=True)
+    a = crandom.random((200, 200), chunks=(50, 50), spec=spec)
+    go(xp.mean((a + 1) * 2, axis=0))
+    x = np.random.default_rng(8).random((33, 500)) + 0.5
+    b = cubed.from_array(x, chunks=(10, 128), spec=spec)
+    go(xp.max(b, axis=0))
+    go(xp.min(b))
+    go(xp.sum(b, axis=1))  # edge chunk along the reduced axis on one rank only
+    y = np.ones((60, 50), dtype=np.float32)
+    go(cubed.from_array(y, chunks=(7, 9), spec=spec).rechunk((13, 4)))
+    go(cubed.from_array(y, chunks=(10, 50), spec=spec) + cubed.from_array(y, chunks=(20, 25), spec=spec))
+    A = cubed.from_array(np.ones((96, 80), np.float32), chunks=(32, 40), spec=spec)
+    B = cubed.from_array(np.ones((80, 64), np.float32), chunks=(40, 32), spec=spec)
+    go(xp.matmul(A, B))
+    return seq
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_issue_the_same_collectives(built, world):
+    from distutil import run_ranks
+
+    seqs = run_ranks(_launch_sequence, world)
+    for r in range(1, world):
+        assert seqs[r] == seqs[0], (r, seqs[0], seqs[r])
+    assert ["PartialsLaunch"] in seqs[0] and ["FetchLaunch"] in seqs[0]
