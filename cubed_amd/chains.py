@@ -35,6 +35,8 @@ from . import ir
 from .lowering import (
     LEAF_ARRAY,
     LEAF_IOTA,
+    LEAF_OFFSET,
+    LEAF_PHILOX,
     LoweringError,
     TaskRow,
     chunk_view,
@@ -252,6 +254,15 @@ def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys, select=None, ou
             r = layouts[t]
             if r.extent != r0.extent or r.lstrides != r0.lstrides:
                 raise LoweringError("chain tasks are not uniform (edge chunk along the reduced axis)")
+        # leaves whose value depends on the task itself (a Philox stream key,
+        # a block offset) cannot be folded into one strided pass
+        for t in tkeys:
+            r = layouts[t]
+            for kind in kinds:
+                if kind == LEAF_PHILOX and (r.key_lo, r.key_hi) != (r0.key_lo, r0.key_hi):
+                    raise LoweringError("chain over per-chunk random streams")
+                if kind == LEAF_OFFSET and r.block_offset != r0.block_offset:
+                    raise LoweringError("chain over per-chunk block offsets")
         coords = {a: sorted({t[a] for t in tkeys}) for a in axes}
         nq = [len(coords[a]) for a in axes]
         if math.prod(nq) != len(tkeys):
@@ -320,3 +331,173 @@ def _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard):
         obases.append(base0 if owned else discard)
         ostr.append(st)
     return obases, ostr
+
+
+# ------------------------------------------------------------ producer fusion
+
+
+def fuse_elementwise_producers(dag, array_names):
+    """Executor-side map fusion: an elementwise map whose output feeds exactly
+    one op (and is not requested) is fused into that op with the plan-level
+    ``fuse_multiple`` (primitive/blockwise.py, the reference's
+    primitive/blockwise.py:420-508), so its intermediate is never written to
+    HBM.  The reference's default optimizer (simple_optimize_dag,
+    core/optimization.py:11-68) leaves such maps unfused whenever the consumer
+    has more than one input -- e.g. ``(a + 1) * 2`` under a mean, where the
+    scalar operands make every op binary -- which costs a full write + read
+    of the intermediate per map.  Values are unchanged (the fused program
+    performs the same IEEE operations in the same order, with the same
+    intermediate dtypes), and each absorbed op still gets its TaskEndEvent
+    (recorded on the consumer node as ``fused_from``).
+
+    Returns the rewritten DAG (a copy) and the absorbed array targets."""
+    import networkx as nx
+
+    from .core.optimization import predecessors
+    from .lowering import program_fits
+    from .primitive.blockwise import fuse_multiple
+
+    requested = set(array_names or ())
+    dag = dag.copy()
+    absorbed_targets = []
+
+    def is_map(nd):
+        if "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
+            return False
+        p = nd["pipeline"].config.function
+        return isinstance(p, ir.ExprProgram) and p.reduce is None and not p.structured
+
+    for name in list(nx.topological_sort(dag)):
+        if name not in dag:
+            continue
+        nd = dag.nodes[name]
+        if "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
+            continue
+        if not isinstance(nd["pipeline"].config.function, ir.ExprProgram):
+            continue
+        op = nd["primitive_op"]
+        # the array each block-function argument reads, in argument order (a
+        # DAG copy does not keep in-edge order, so ask the key function)
+        inputs = _arg_arrays(nd["pipeline"].config, op.target_array)
+        if inputs is None or any(i not in dag for i in inputs):
+            continue
+        fuse_pre = {}
+        producer = []
+        for inp in inputs:
+            pres = list(predecessors(dag, inp))
+            producer.append(pres[0] if len(pres) == 1 else None)
+            if len(pres) != 1 or inp in requested or dag.out_degree(inp) != 1:
+                continue
+            pre = pres[0]
+            pn = dag.nodes[pre]
+            if not is_map(pn) or dag.out_degree(pre) != 1:
+                continue
+            if pn["primitive_op"].num_tasks != op.num_tasks:
+                continue
+            t = dag.nodes[inp].get("target")
+            if getattr(t, "written", False):
+                continue  # already materialised (resume): read it, do not recompute
+            fuse_pre[pre] = inp
+        if not fuse_pre:
+            continue
+        preds = [dag.nodes[p]["primitive_op"] if p in fuse_pre else None for p in producer]
+        fused = fuse_multiple(op, *preds)
+        fp = fused.pipeline.config.function
+        if not isinstance(fp, ir.ExprProgram):
+            continue
+        fp = _dedupe_args(fused.pipeline.config, fp, op.target_array)
+        if not program_fits(fp):
+            continue
+        if fp is not fused.pipeline.config.function:
+            fused = _with_program(fused, fp)
+        nd["primitive_op"] = fused
+        nd["pipeline"] = fused.pipeline
+        nd["fused_from"] = list(nd.get("fused_from", ())) + [
+            (p, dag.nodes[p]["primitive_op"].num_tasks) for p in fuse_pre]
+        for pre, inp in fuse_pre.items():
+            for src in list(predecessors(dag, pre)):
+                if src != "arrays":
+                    dag.add_edge(src, name)
+            t = dag.nodes[inp].get("target")
+            if t is not None:
+                absorbed_targets.append(t)
+            nd["fused_from"] = list(dag.nodes[pre].get("fused_from", ())) + nd["fused_from"]
+            dag.remove_node(inp)
+            dag.remove_node(pre)
+    return dag, absorbed_targets
+
+
+def _arg_arrays(spec, target):
+    """Array name read by each block-function argument (None if the key
+    function does not name one array per argument)."""
+    nb = getattr(target, "numblocks", ())
+    try:
+        args = spec.block_function(("out",) + (0,) * len(nb))
+    except Exception:  # noqa: BLE001 -- an unusual key function: leave it unfused
+        return None
+    names = []
+    for a in args:
+        while isinstance(a, list):
+            if not a:
+                return None
+            a = a[0]
+        if isinstance(a, tuple) and a and isinstance(a[0], str):
+            names.append(a[0])
+        elif isinstance(a, str):
+            names.append(a)
+        else:
+            return None
+    return names
+
+
+def _dedupe_args(spec, program, target, max_tasks=1 << 16):
+    """Point every argument that reads the same chunk as an earlier argument
+    in EVERY task at that earlier argument (e.g. ``where(a > 0.5, a, -a)``
+    fused: three reads of a's chunk become one leaf, one HBM read)."""
+    import dataclasses
+    import itertools
+
+    nb = tuple(getattr(target, "numblocks", ()))
+    if math.prod(nb) > max_tasks:
+        return program
+
+    def canon(a):
+        return tuple(canon(x) for x in a) if isinstance(a, list) else a
+
+    keys = itertools.product(*[range(n) for n in nb])
+    first = [canon(a) for a in spec.block_function(("out",) + next(keys))]
+    same = {j: i for j in range(len(first)) for i in range(j)
+            if first[i] == first[j] and not isinstance(first[i], str)}
+    same = {j: min(i for i in range(j) if first[i] == first[j]) for j in same}
+    for k in keys:
+        if not same:
+            return program
+        args = [canon(a) for a in spec.block_function(("out",) + k)]
+        same = {j: i for j, i in same.items() if args[i] == args[j]}
+    if not same:
+        return program
+
+    def fn(leaf):
+        if isinstance(leaf, ir.Arg) and leaf.index in same:
+            return dataclasses.replace(leaf, index=same[leaf.index])
+        return None
+
+    memo = {}
+    if program.structured:
+        outputs = tuple((n, ir.transform(e, fn, memo)) for n, e in program.outputs)
+    else:
+        outputs = ir.transform(program.outputs, fn, memo)
+    reduce = program.reduce
+    if reduce is not None:
+        reduce = dataclasses.replace(reduce, fields=tuple(
+            dataclasses.replace(f, expr=ir.transform(f.expr, fn, memo)) for f in reduce.fields))
+    return dataclasses.replace(program, outputs=outputs, reduce=reduce)
+
+
+def _with_program(op, program):
+    """A PrimitiveOperation whose pipeline runs ``program`` (same keys)."""
+    import dataclasses
+
+    spec = dataclasses.replace(op.pipeline.config, function=program)
+    pipeline = dataclasses.replace(op.pipeline, config=spec)
+    return dataclasses.replace(op, pipeline=pipeline)

@@ -188,8 +188,8 @@ int check_program(const cubed_program_t& P) {
   if ((P.mode & CUBED_MODE_PARTIALS) && P.nfields == 0) { set_err("cubed_fused_chunks: partials mode needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & 3) == 1 && P.nfields == 0) { set_err("cubed_fused_chunks: kernel B needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & CUBED_MODE_STREAM) &&
-      ((P.mode & 3) != 0 || !(P.mode & 4) || P.nred > 1 || P.ndim != P.nred + 1 || P.nleaves < 1)) {
-    set_err("cubed_fused_chunks: stream mode needs kernel A, VEC=4, one kept dim and <= 1 reduced dim");
+      ((P.mode & 3) != 0 || !(P.mode & 4) || P.nred > 2 || P.ndim != P.nred + 1 || P.nleaves < 1)) {
+    set_err("cubed_fused_chunks: stream mode needs kernel A, VEC=4, one kept dim and <= 2 reduced dims");
     return CUBED_E_LAYOUT;
   }
   if (P.mode & CUBED_MODE_STREAM) {

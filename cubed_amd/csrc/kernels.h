@@ -440,18 +440,23 @@ CUBED_DEV void stream_body(
   const int64_t t = rest / nsplit;
   if (t >= ntasks) return;
   const cubed_task_t* __restrict__ T = tasks + t;
-  const int nr = P.nred;  // 0 (map) or 1
+  // nr = 0 (map), 1 (rows) or 2 (chunks x rows: a reduction chain whose
+  // chunks sit at a slot stride that is not the rows' own continuation)
+  const int nr = P.nred;
   const int64_t nk = T->extent[nr];
-  const int64_t nrd = nr ? T->extent[0] : 1;
+  const int64_t nrow = nr ? T->extent[nr - 1] : 1;
+  const int64_t nq = nr == 2 ? T->extent[0] : 1;
+  const int64_t nrd = nq * nrow;
   const int64_t items = nk >> 2;
   const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
 
   const CUBED_G V* base[NL];
-  int64_t rs[NL];
+  int64_t rs[NL], qs[NL];
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
     base[l] = (const CUBED_G V*)(uintptr_t)T->leaf_base[l];
-    rs[l] = nr ? T->leaf_stride[l][0] : 0;
+    rs[l] = nr ? T->leaf_stride[l][nr - 1] : 0;
+    qs[l] = nr == 2 ? T->leaf_stride[l][0] : 0;
   }
 
   for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
@@ -482,34 +487,39 @@ CUBED_DEV void stream_body(
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
 
-    const CUBED_G V* p[NL];
+    // flattened reduced range [r0, r1) = (chunk q, row) pairs in order
+    for (int64_t q = nrow ? r0 / nrow : 0; q < nq && q * nrow < r1; ++q) {
+      const int64_t lo = (r0 > q * nrow ? r0 : q * nrow) - q * nrow;
+      const int64_t hi = (r1 < (q + 1) * nrow ? r1 : (q + 1) * nrow) - q * nrow;
+      const CUBED_G V* p[NL];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) p[l] = base[l] + k + r0 * rs[l];
-    int64_t r = r0;
-    for (; r + U <= r1; r += U) {
-      V buf[U][NL][4];
+      for (int l = 0; l < NL; ++l) p[l] = base[l] + k + q * qs[l] + lo * rs[l];
+      int64_t r = lo;
+      for (; r + U <= hi; r += U) {
+        V buf[U][NL][4];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int l = 0; l < NL; ++l) ld4(buf[u][l], p[l] + u * rs[l]);
+          for (int l = 0; l < NL; ++l) ld4(buf[u][l], p[l] + u * rs[l]);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        set_leaves<NL, V>(regs, buf[u]);
+        for (int u = 0; u < U; ++u) {
+          set_leaves<NL, V>(regs, buf[u]);
+          CUBED_RUN_PROLOGUE(V, 4, regs);
+          accumulate_nocount<V>(acc, regs, P);
+        }
+#pragma unroll
+        for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
+      }
+      for (; r < hi; ++r) {
+        V buf[NL][4];
+#pragma unroll
+        for (int l = 0; l < NL; ++l) ld4(buf[l], p[l]);
+        set_leaves<NL, V>(regs, buf);
         CUBED_RUN_PROLOGUE(V, 4, regs);
         accumulate_nocount<V>(acc, regs, P);
+#pragma unroll
+        for (int l = 0; l < NL; ++l) p[l] += rs[l];
       }
-#pragma unroll
-      for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
-    }
-    for (; r < r1; ++r) {
-      V buf[NL][4];
-#pragma unroll
-      for (int l = 0; l < NL; ++l) ld4(buf[l], p[l]);
-      set_leaves<NL, V>(regs, buf);
-      CUBED_RUN_PROLOGUE(V, 4, regs);
-      accumulate_nocount<V>(acc, regs, P);
-#pragma unroll
-      for (int l = 0; l < NL; ++l) p[l] += rs[l];
     }
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f)

@@ -546,6 +546,50 @@ def program_exprs(p: ir.ExprProgram):
     return outs, fields
 
 
+def program_fits(p: ir.ExprProgram) -> bool:
+    """Whether an expression program fits the VM (leaves, one random stream,
+    registers, instruction counts) -- checked before any constant folding,
+    so it is conservative.  Used by the executor's producer fusion to only
+    build fused programs it can lower."""
+    try:
+        outs, fields = program_exprs(p)
+        exprs = dedupe_leaves(outs + fields)
+        pre = exprs[:len(outs)] if p.reduce is None else exprs[len(outs):]
+        leaves = collect_leaves(pre)
+        if len(leaves) > nat.MAX_LEAVES or sum(isinstance(l, ir.Philox) for l in leaves) > 1:
+            return False
+        by_key = {_leaf_key(l): i for i, l in enumerate(leaves)}
+        leaf_regs = {}
+        for e in pre:
+            for lf in ir.leaves(e):
+                if not isinstance(lf, (ir.Const, ir.Field)):
+                    leaf_regs[id(lf)] = by_key[_leaf_key(lf)]
+        cg = Codegen(choose_vtype(pre, leaves), leaf_regs)
+        cg.count_uses(pre)
+        for e in pre:
+            cg.gen(e)
+        if len(cg.code) > nat.MAX_INSNS or len(cg.consts) > nat.MAX_CONSTS:
+            return False
+        if p.reduce is not None and not all(isinstance(e, ir.Field) for e in exprs[:len(outs)]):
+            ecg = Codegen(V_F64, {}, nregs=nat.NREGS)
+            nf = len(p.reduce.fields)
+            ecg.reserved = set(range(nf))
+            ecg.free = [r for r in range(nat.NREGS) if r not in ecg.reserved]
+            fidx = {f.name: i for i, f in enumerate(p.reduce.fields)}
+            for e in exprs[:len(outs)]:
+                for lf in ir.leaves(e):
+                    if isinstance(lf, ir.Field):
+                        ecg.leaf_regs[id(lf)] = fidx[lf.name]
+            ecg.count_uses(exprs[:len(outs)])
+            for e in exprs[:len(outs)]:
+                ecg.gen(e)
+            if len(ecg.code) > nat.MAX_EPI:
+                return False
+        return True
+    except (LoweringError, KeyError):
+        return False
+
+
 def is_pure_copy(p: ir.ExprProgram, out_dtype) -> bool:
     """A program that only moves one leaf's values (merge/index/squeeze)."""
     if p.reduce is not None or p.structured:
@@ -667,6 +711,9 @@ class Lowerer:
                 rfields = [ir.ReduceField(f.name, f.rop, e, f.dtype) for f, e in zip(rfields, pre_exprs)]
             leaves = collect_leaves(pre_exprs)
 
+        if sum(isinstance(l, ir.Philox) for l in leaves) > 1:
+            # cubed_task_t carries one Philox key per task
+            raise LoweringError("fused program draws from more than one random stream")
         vtype = choose_vtype(pre_exprs, leaves)
         leaf_regs = {}
         by_key = {_leaf_key(l): i for i, l in enumerate(leaves)}
@@ -1157,9 +1204,10 @@ _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64:
 
 def _stream_ok(layout: Layout, leaves, kinds, vtype) -> bool:
     """Geometry of the streaming fast path (stream.hip): kernel A with VEC=4,
-    one kept kernel dim (packed in every leaf and output) after at most one
-    reduced dim, every leaf an array chunk in the VM's own dtype."""
-    if layout.mode != 4 or layout.nred > 1 or layout.ndim != layout.nred + 1 or not leaves:
+    one kept kernel dim (packed in every leaf and output) after at most two
+    reduced dims (chunk index x rows), every leaf an array chunk in the VM's
+    own dtype."""
+    if layout.mode != 4 or layout.nred > 2 or layout.ndim != layout.nred + 1 or not leaves:
         return False
     want = _VTYPE_DTYPE.get(vtype)
     for l, kind in enumerate(kinds):
@@ -1170,8 +1218,9 @@ def _stream_ok(layout: Layout, leaves, kinds, vtype) -> bool:
         for l, st in enumerate(ls):
             if st[-1] != 1 or r.bases[l] % 16:
                 return False
-            if layout.nred and ext[0] != 1 and st[0] % 4:
-                return False
+            for d in range(layout.nred):
+                if ext[d] != 1 and st[d] % 4:
+                    return False
         for st in os_:
             if st[-1] != 1:
                 return False

@@ -158,6 +158,8 @@ class GpuDagExecutor(DagExecutor):
         self.timing: Optional[LaunchTimer] = None
         self.fuse_reductions = True
         self._chains: Dict = {}
+        self._exec_dags: Dict = {}
+        self.fuse_producers = True
         self._agreed = set()
         self.elided = set()
 
@@ -549,8 +551,28 @@ class GpuDagExecutor(DagExecutor):
         launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys]))
         return launches
 
+    def exec_dag(self, dag, array_names):
+        """The DAG this executor runs: the plan's finalized DAG with
+        single-consumer elementwise maps fused into their consumers
+        (chains.fuse_elementwise_producers), cached per plan DAG."""
+        if not self.fuse_producers:
+            return dag
+        key = (id(dag), tuple(array_names or ()))
+        entry = self._exec_dags.get(key)
+        if entry is not None and entry[0]() is dag:
+            return entry[1]
+        from ...chains import fuse_elementwise_producers
+
+        new, absorbed = fuse_elementwise_producers(dag, array_names)
+        for t in absorbed:
+            if isinstance(t, DeviceArray):
+                self.elided.add(id(t))
+        self._exec_dags[key] = (weakref.ref(dag), new)
+        return new
+
     def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
         stream = self.stream
+        dag = self.exec_dag(dag, array_names)
         nodes = dict(dag.nodes(data=True))
         if self.check_memory:
             self._check_hbm(dag)
@@ -605,6 +627,12 @@ class GpuDagExecutor(DagExecutor):
                     if isinstance(target, DeviceArray):
                         target.written = True
             if callbacks is not None:
+                for fname, ntasks in node.get("fused_from", ()):
+                    ev = TaskEndEvent(array_name=fname, num_tasks=ntasks, function_start_tstamp=t0,
+                                      function_end_tstamp=time.time())
+                    ev.task_result_tstamp = time.time()
+                    for cb in callbacks:
+                        cb.on_task_end(ev)
                 op = node.get("primitive_op")
                 ev = TaskEndEvent(array_name=name, num_tasks=op.num_tasks if op is not None else 1,
                                   function_start_tstamp=t0, function_end_tstamp=time.time())

@@ -138,7 +138,7 @@ typedef struct {
                                  /* (VEC=4 loads/stores; host-checked)      */
                                  /* +8 (CUBED_MODE_STREAM): streaming fast  */
                                  /* path, host-checked: kernel A, VEC=4,    */
-                                 /* ndim == nred + 1, nred <= 1, every leaf */
+                                 /* ndim == nred + 1, nred <= 2, every leaf */
                                  /* an ARRAY in the vtype's own dtype       */
                                  /* (f32/f64/i64) with packed kept dim and  */
                                  /* reduced strides that are multiples of 4 */

@@ -174,6 +174,22 @@ def test_config1_small(ex):
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
 
 
+def test_mean_of_unmaterialised_random(ex):
+    """random -> elementwise -> mean with nothing materialised: the Philox
+    map is fused into the reduction's first pass (one stream key per
+    chunk), the chain over chunks must not reuse one key."""
+    spec = mkspec(ex)
+    random.seed(17)
+    a = crandom.random((200, 120), chunks=(50, 40), spec=spec)
+    (s,) = seeds(17, 1)
+    x = R.random_array((200, 120), (50, 40), s)
+    got = xp.mean(a * 3 - 1, axis=0).compute()
+    exp = R.mean(x * 3 - 1, (50, 40), 0, allowed_mem=2_000_000_000)
+    assert np.allclose(got, exp, rtol=1e-12, atol=0)
+    got1 = xp.sum(a, axis=1).compute()
+    assert np.allclose(got1, x.sum(axis=1), rtol=1e-12, atol=0)
+
+
 @pytest.mark.parametrize("fn, npfn", [(xp.sum, np.sum), (xp.max, np.max), (xp.min, np.min), (xp.prod, np.prod)])
 @pytest.mark.parametrize("axis", [0, 1, None])
 def test_reductions_f64(ex, fn, npfn, axis):

@@ -111,3 +111,66 @@ def test_fused_programs_compile_specialised(built, dry):
         src = nat.program_source(L.handle)
         assert "jit_prologue" in src and "cubed_" in src
         assert nat.lib().cubed_fused_code_bytes(L.handle) > 0
+
+
+def test_config1_is_one_streaming_launch(built, dry):
+    """(a + 1) * 2 -> mean(axis=0) over a 4x4 chunk grid: the add map is fused
+    into the mean (executor producer fusion), the reduction rounds into one
+    pass, and the chunk index x rows reduction runs on the streaming kernel
+    with two reduced dims (the chunks of a column sit 4 slots apart)."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(3)
+    a = crandom.random((400, 400), chunks=(100, 100), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    m = xp.mean((a + 1) * 2, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    assert len(dry.launched) == 1 and len(fused) == 1
+    P = fused[0].prog
+    assert P.mode & MODE_STREAM
+    assert (P.ndim, P.nred, P.nleaves, P.nfields) == (3, 2, 1, 2)
+    assert fused[0].ntasks == 4 and fused[0].max_red == 400
+
+
+def test_producer_fusion_keeps_materialised_inputs(built, dry):
+    """A map whose output was already computed (resume) is read, not fused."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(3)
+    a = crandom.random((400, 400), chunks=(100, 100), spec=spec)
+    b = a + 1
+    arrays_to_plan(b).execute(executor=dry, array_names=[b.name])
+    dry.launched.clear()
+    m = xp.mean(b * 2, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    assert len(fused) == 1 and fused[0].prog.nleaves == 1
+    assert fused[0].prog.leaf_kind[0] == 0  # reads b's chunks (no Philox recompute)
+
+
+def test_two_random_streams_are_not_fused(built, dry):
+    """mean(u * v) over two unmaterialised random arrays: the Philox maps
+    are not fused into the mean (a task carries one stream key); they are
+    generated as maps and the mean reads them."""
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(42)
+    u = xp.astype(crandom.random((50, 37, 40), chunks=(10, 37, 40), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((50, 37, 40), chunks=(10, 37, 40), spec=spec), xp.float32)
+    m = xp.mean(u * v, axis=0)
+    arrays_to_plan(m).execute(executor=dry, array_names=[m.name])
+    for L in _fused(dry):
+        assert sum(L.prog.leaf_kind[i] == 1 for i in range(L.prog.nleaves)) <= 1
+
+
+def test_where_producers_fuse_into_one_read(built, dry):
+    """where(a > 0.5, a, -a): both maps fuse into the where, and the three
+    reads of a's chunk become one leaf (argument dedupe)."""
+    x = np.random.default_rng(6).random((40, 30))
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    a = cubed.from_array(x, chunks=(16, 16), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    w = xp.where(a > 0.5, a, -a)
+    arrays_to_plan(w).execute(executor=dry, resume=True, array_names=[w.name])
+    fused = _fused(dry)
+    assert len(fused) == 1 and fused[0].prog.nleaves == 1  # the 0.5 scalar is a constant
