@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--t-length", type=int, default=1000, help="time steps per GPU (quad-means)")
     p.add_argument("--no-extra", action="store_true", help="skip the rechunk/config-1 extras")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-matmul", action="store_true", help="skip the matmul extra")
     p.add_argument("--cpu-sample", type=int, default=300)
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
@@ -238,6 +239,45 @@ def config1_extra(ex, rank):
                 value=a.nbytes / dt / 1e9, ms=dt * 1e3)
 
 
+def matmul_extra(ex, rank, n=20000, c=5000):
+    """configs[4] shape of work, scaled to one GPU: xp.matmul of two f32
+    (n, n) arrays in (c, c) chunks -- (n/c)^3 chunk GEMMs on MFMA, then the
+    k-sum reduction.  Reports the whole plan's TFLOP/s and the GEMM launch's
+    own rate (HIP events on the executor stream)."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.executors.gpu import LaunchTimer
+
+    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+    random.seed(4000)
+    A = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xp.float32)
+    B = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xp.float32)
+    arrays_to_plan(A, B).execute(executor=ex, array_names=[A.name, B.name])
+    m = xp.matmul(A, B)
+    plan = arrays_to_plan(m)
+
+    def step():
+        _reset_targets(plan, (A, B))
+        plan.execute(executor=ex, resume=True, array_names=[m.name])
+
+    step()
+    ex.timing = LaunchTimer()
+    dt = timed(step, 2, ex.world)
+    timer, ex.timing = ex.timing, None
+    summ = timer.summary()
+    gemm = [v for k, v in summ.items() if k[2] == "GemmLaunch"]
+    flop = 2.0 * n ** 3
+    out = dict(metric="matmul f32 TFLOP/s (whole plan)", value=flop / dt / 1e12, ms=dt * 1e3,
+               n=n, chunk=c)
+    if gemm:
+        out["gemm_launch_ms"] = gemm[0][1]
+        out["gemm_tflops"] = flop / (gemm[0][1] * 1e-3) / 1e12 / ex.world
+        out["mfma_util_vs_157TF"] = out["gemm_tflops"] / 157.3
+    return out
+
+
 def _reset_targets(plan, keep):
     from cubed_amd.storage import DeviceArray
 
@@ -305,6 +345,11 @@ def main():
             extra["config1"] = config1_extra(ex, rank)
         except Exception as e:  # pragma: no cover
             extra["config1"] = {"error": repr(e)}
+        if not args.no_matmul:
+            try:
+                extra["matmul"] = matmul_extra(ex, rank)
+            except Exception as e:  # pragma: no cover
+                extra["matmul"] = {"error": repr(e)}
     line = {
         "metric": "effective input GB/s (node) for fused elementwise+mean (quad-means)",
         "value": round(value, 2),

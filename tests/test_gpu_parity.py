@@ -283,6 +283,27 @@ def test_matmul_f32(ex):
     assert np.allclose(got, exp, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("shape_a, shape_b, ca, cb", [
+    ((300, 256), (256, 190), (150, 128), (128, 95)),    # float4 rows, M/N tails
+    ((300, 257), (257, 190), (150, 129), (129, 95)),    # odd K: scalar operand path
+    ((520, 1040), (1040, 260), (260, 520), (520, 260)), # several 128-tiles and K tiles
+])
+def test_matmul_f32_tiles(ex, shape_a, shape_b, ca, cb):
+    """The 128x128x32 MFMA tile kernel against an f64 product (error bound
+    of an f32 fma chain + f32 k-chunk sums: rtol 1e-5 at these K)."""
+    r = np.random.default_rng(12)
+    x = r.random(shape_a).astype(np.float32) - 0.5
+    y = r.random(shape_b).astype(np.float32) - 0.5
+    spec = mkspec(ex)
+    a = cubed.from_array(x, chunks=ca, spec=spec)
+    b = cubed.from_array(y, chunks=cb, spec=spec)
+    got = xp.matmul(a, b).compute()
+    exp = x.astype(np.float64) @ y.astype(np.float64)
+    scale = np.abs(x).astype(np.float64) @ np.abs(y).astype(np.float64)
+    assert got.dtype == np.float32
+    assert np.all(np.abs(got - exp) <= 1e-6 * scale + 1e-30)
+
+
 def test_tensordot_golden(ex):
     c = json.load(open(os.path.join(GOLDEN, "reference_cases.json")))["tensordot_axes_1"]
     spec = mkspec(ex)
