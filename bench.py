@@ -278,6 +278,36 @@ def matmul_extra(ex, rank, n=20000, c=5000):
     return out
 
 
+def vorticity_extra(ex, rank, T=1000):
+    """configs[3]: the pangeo-vorticity expression of the reference example
+    (examples/pangeo-vorticity.ipynb cell 2) -- mean(a[1:] * x + b[1:] * y)
+    with a, b (1000, 900, 800) f64 and x, y (900, 800) f64, chunks 100."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    random.seed(5000)
+    a = crandom.random((T, 900, 800), chunks=100, spec=spec)
+    b = crandom.random((T, 900, 800), chunks=100, spec=spec)
+    x = crandom.random((900, 800), chunks=100, spec=spec)
+    y = crandom.random((900, 800), chunks=100, spec=spec)
+    arrays_to_plan(a, b, x, y).execute(executor=ex, array_names=[a.name, b.name, x.name, y.name])
+    m = xp.mean(a[1:] * x + b[1:] * y)
+    plan = arrays_to_plan(m)
+
+    def step():
+        _reset_targets(plan, (a, b, x, y))
+        plan.execute(executor=ex, resume=True, array_names=[m.name])
+
+    step()
+    dt = timed(step, 3, ex.world)
+    in_bytes = a.nbytes + b.nbytes + x.nbytes + y.nbytes
+    return dict(metric="vorticity mean(a[1:]*x + b[1:]*y) effective input GB/s",
+                value=in_bytes / dt / 1e9, ms=dt * 1e3)
+
+
 def _reset_targets(plan, keep):
     from cubed_amd.storage import DeviceArray
 
@@ -345,6 +375,10 @@ def main():
             extra["config1"] = config1_extra(ex, rank)
         except Exception as e:  # pragma: no cover
             extra["config1"] = {"error": repr(e)}
+        try:
+            extra["vorticity"] = vorticity_extra(ex, rank)
+        except Exception as e:  # pragma: no cover
+            extra["vorticity"] = {"error": repr(e)}
         if not args.no_matmul:
             try:
                 extra["matmul"] = matmul_extra(ex, rank)
