@@ -149,6 +149,17 @@ def quad_means(args, rank, world, ex):
     return dict(in_bytes=in_bytes, dt=dt, timer=timer, m=m, u=u, v=v)
 
 
+def timed_launches(ex, fn, steps, world):
+    """(seconds per call, {launch: mean ms}) -- the executor's per-launch HIP
+    events recorded during the timed calls."""
+    from cubed_amd.runtime.executors.gpu import LaunchTimer
+
+    ex.timing = LaunchTimer()
+    dt = timed(fn, steps, world)
+    timer, ex.timing = ex.timing, None
+    return dt, {f"{k[0]}#{k[1]}:{k[2]}": round(v[1], 4) for k, v in timer.summary().items()}
+
+
 def timed(fn, steps, world):
     """Mean seconds per call of fn over `steps` calls, barrier + synchronize
     on both sides, max over ranks."""
@@ -196,12 +207,12 @@ def rechunk_extra(ex, rank):
     plan = arrays_to_plan(y)
     for _ in range(2):
         _exec_only(plan, ex, y, x)
-    dt = timed(lambda: _exec_only(plan, ex, y, x), 5, ex.world)
+    dt, launches = timed_launches(ex, lambda: _exec_only(plan, ex, y, x), 5, ex.world)
     nops = sum(1 for _, d in plan._finalize_dag().nodes(data=True)
                if d.get("op_name") == "rechunk")
     # correctness spot check: a few columns
     return dict(metric="rechunk effective input GB/s", value=x.nbytes / dt / 1e9,
-                ms=dt * 1e3, ops=nops, bytes_moved_per_op=2 * x.nbytes)
+                ms=dt * 1e3, ops=nops, bytes_moved_per_op=2 * x.nbytes, launches_ms=launches)
 
 
 def _exec_only(plan, ex, y, x):
@@ -234,9 +245,9 @@ def config1_extra(ex, rank):
 
     for _ in range(2):
         step()
-    dt = timed(step, 5, ex.world)
+    dt, launches = timed_launches(ex, step, 5, ex.world)
     return dict(metric="config1 (a+1)*2 -> mean(axis=0) effective input GB/s",
-                value=a.nbytes / dt / 1e9, ms=dt * 1e3)
+                value=a.nbytes / dt / 1e9, ms=dt * 1e3, launches_ms=launches)
 
 
 def matmul_extra(ex, rank, n=20000, c=5000):
@@ -302,10 +313,10 @@ def vorticity_extra(ex, rank, T=1000):
         plan.execute(executor=ex, resume=True, array_names=[m.name])
 
     step()
-    dt = timed(step, 3, ex.world)
+    dt, launches = timed_launches(ex, step, 3, ex.world)
     in_bytes = a.nbytes + b.nbytes + x.nbytes + y.nbytes
     return dict(metric="vorticity mean(a[1:]*x + b[1:]*y) effective input GB/s",
-                value=in_bytes / dt / 1e9, ms=dt * 1e3)
+                value=in_bytes / dt / 1e9, ms=dt * 1e3, launches_ms=launches)
 
 
 def _reset_targets(plan, keep):

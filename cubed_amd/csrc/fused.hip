@@ -65,6 +65,13 @@ __global__ __launch_bounds__(kBlock) void k_finish_soa(
   finish_soa_body(*Pd, tasks, ntasks, max_kept, soa, kd0, kd1);
 }
 
+__global__ __launch_bounds__(kBlock) void k_finish_groups(
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    int kd0, int kd1) {
+  finish_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, kd0, kd1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_combine_parts(
     const cubed_program_t* __restrict__ Pd, const Acc* __restrict__ parts, int32_t nparts, int64_t n,
     Acc* __restrict__ out) {
@@ -137,10 +144,10 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
   } else {
     const int64_t base = ntasks * max_kept;
     if (base < target && max_red >= 8192) {
-      int64_t s = (target + base - 1) / base;
-      if (s > max_red / 4096) s = max_red / 4096;
-      if (s > 4096) s = 4096;
-      if (s > 1) L.nsplit = (int32_t)s;
+      // whole rounds of workgroups, >= 4 of them: rows of one launch can
+      // differ a lot in size (pieces of a task cut at chunk boundaries), and
+      // with several rounds the short ones no longer leave a ragged tail
+      L.nsplit = (int32_t)choose_split(base, max_red / 4096, 4 * target);
     }
     L.blocks = ntasks * max_kept * L.nsplit;
   }
@@ -263,6 +270,27 @@ extern "C" int cubed_fused_finish(const cubed_program_t* prog, const cubed_progr
   const int64_t n = ntasks * max_kept;
   hipLaunchKernelGGL(k_finish_soa, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
                      d_prog, d_tasks, ntasks, max_kept, (const Acc*)d_partials, kd0, kd1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+extern "C" int cubed_fused_finish_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                         const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                                         const void* d_partials, const int64_t* d_group_start,
+                                         int64_t ngroups, void* stream) {
+  if (!prog || !d_prog || !d_partials || !d_group_start || (!d_tasks && ntasks > 0)) {
+    set_err("cubed_fused_finish_groups: null argument");
+    return CUBED_E_ARG;
+  }
+  if (ntasks == 0 || ngroups == 0) return 0;
+  if (int rc = check_program(*prog)) return rc;
+  if (prog->nfields == 0 || max_kept <= 0 || ngroups > ntasks) { set_err("cubed_fused_finish_groups: bad shape"); return CUBED_E_ARG; }
+  int kd0, kd1;
+  kept_dims(*prog, kd0, kd1);
+  const int64_t n = ngroups * max_kept;
+  hipLaunchKernelGGL(k_finish_groups, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
+                     d_prog, d_tasks, ntasks, max_kept, (const Acc*)d_partials, d_group_start, ngroups, kd0, kd1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   return 0;

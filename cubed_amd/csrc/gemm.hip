@@ -42,7 +42,14 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const cubed_gemm_task_t* __res
   if (t >= ntasks) return;
   const cubed_gemm_task_t* __restrict__ T = tasks + t;
   const int64_t M = T->m, N = T->n, K = T->k;
-  const int64_t m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  // group-M swizzle: tiles walk 8 tile-rows at a time, column by column, so
+  // the blocks resident on one XCD share 8 A panels and 8 B panels in L2
+  constexpr int64_t GM = 8;
+  const int64_t per_group = GM * tiles_n;
+  const int64_t grp = tile / per_group, first_m = grp * GM;
+  const int64_t gsz = (tiles_m - first_m) < GM ? (tiles_m - first_m) : GM;
+  const int64_t in_g = tile - grp * per_group;
+  const int64_t m0 = (first_m + in_g % gsz) * BM, n0 = (in_g / gsz) * BN;
   if (m0 >= M || n0 >= N) return;
   const int64_t lda = T->lda, ldb = T->ldb;
   // float4 operand loads where every row of the operand is 16-B aligned

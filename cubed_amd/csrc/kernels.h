@@ -229,25 +229,59 @@ CUBED_DEV void fused_b_body(
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
 
+  // Two-level walk of the split's flattened reduced range: outer reduced
+  // index o (dims [nkd, nd-1), decomposed once per o), inner dim nd-1 strided
+  // by the workgroup (no per-element index decomposition).
   Regs<V, VEC> regs;
-  for (int64_t p = r0 + (int64_t)threadIdx.x * VEC; p < r1; p += (int64_t)kBlock * VEC) {
-    int64_t off[CUBED_MAX_LEAVES];
+  const int64_t nin = T->extent[nd - 1];
+  const int64_t stepw = (int64_t)kBlock * VEC;
+  if (nin < 2 * stepw) {
+    // short inner rows: one flattened walk keeps every lane busy
+    for (int64_t p = r0 + (int64_t)threadIdx.x * VEC; p < r1; p += stepw) {
+      int64_t off[CUBED_MAX_LEAVES];
 #pragma unroll
-    for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l];
-    int64_t rr = p;
+      for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = loff[l];
+      int64_t rr = p;
 #pragma unroll
-    for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
-      if (d < nd && d >= nkd) {
+      for (int d = CUBED_MAX_DIMS - 1; d >= 0; --d) {
+        if (d < nd && d >= nkd) {
+          int64_t q, c;
+          if (d == nkd) { q = 0; c = rr; } else divmod64(rr, T->extent[d], q, c);
+          rr = q;
+#pragma unroll
+          for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] += c * T->leaf_stride[l][d];
+        }
+      }
+      load_leaves<V, VEC>(regs, P, T, off, inner);
+      CUBED_RUN_PROLOGUE(V, VEC, regs);
+      accumulate<V, VEC>(acc, regs, P);
+    }
+  }
+  for (int64_t o = nin ? r0 / nin : 0; nin >= 2 * stepw && o * nin < r1; ++o) {
+    const int64_t lo = (r0 > o * nin ? r0 - o * nin : 0);
+    const int64_t hi = (r1 < (o + 1) * nin ? r1 - o * nin : nin);
+    int64_t ooffs[CUBED_MAX_LEAVES];
+#pragma unroll
+    for (int l = 0; l < CUBED_MAX_LEAVES; ++l) ooffs[l] = loff[l];
+    int64_t rr = o;
+#pragma unroll
+    for (int d = CUBED_MAX_DIMS - 2; d >= 0; --d) {
+      if (d < nd - 1 && d >= nkd) {
         int64_t q, c;
         if (d == nkd) { q = 0; c = rr; } else divmod64(rr, T->extent[d], q, c);
         rr = q;
 #pragma unroll
-        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] += c * T->leaf_stride[l][d];
+        for (int l = 0; l < CUBED_MAX_LEAVES; ++l) ooffs[l] += c * T->leaf_stride[l][d];
       }
     }
-    load_leaves<V, VEC>(regs, P, T, off, inner);
-    CUBED_RUN_PROLOGUE(V, VEC, regs);
-    accumulate<V, VEC>(acc, regs, P);
+    for (int64_t i = lo + (int64_t)threadIdx.x * VEC; i < hi; i += stepw) {
+      int64_t off[CUBED_MAX_LEAVES];
+#pragma unroll
+      for (int l = 0; l < CUBED_MAX_LEAVES; ++l) off[l] = ooffs[l] + i * inner[l];
+      load_leaves<V, VEC>(regs, P, T, off, inner);
+      CUBED_RUN_PROLOGUE(V, VEC, regs);
+      accumulate<V, VEC>(acc, regs, P);
+    }
   }
   // combine VEC lanes, then the 64-wide wave, then the 4 waves
   Acc a[CUBED_MAX_FIELDS];
@@ -368,6 +402,42 @@ CUBED_DEV void finish_soa_body(
   Acc fin[CUBED_MAX_FIELDS][1];
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
     fin[f][0] = f < P.nfields ? soa[f * n + i] : acc_init(CUBED_R_NONE, 0);
+  finish<1>(P, T, fin, ooff);
+}
+
+// Grouped finish: tasks [gs[g], gs[g+1]) are pieces of one output box (a
+// task split where its inputs straddle source chunks along a reduced dim);
+// their SoA partials are combined in piece order and the first piece's
+// output views receive the epilogue.
+CUBED_DEV void finish_groups_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    int kd0, int kd1) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t g = i / max_kept, k = i % max_kept;
+  if (g >= ngroups) return;
+  const int64_t t0 = gs[g], t1 = gs[g + 1];
+  const cubed_task_t* __restrict__ T = tasks + t0;
+  int64_t nk = 1;
+  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+  if (k >= nk) return;
+  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t kk = k;
+  for (int d = kd1 - 1; d >= kd0; --d) {
+    int64_t q, c;
+    divmod64(kk, T->extent[d], q, c);
+    kk = q;
+    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
+  }
+  const int64_t n = ntasks * max_kept;
+  Acc fin[CUBED_MAX_FIELDS][1];
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+    if (f >= P.nfields) { fin[f][0] = acc_init(CUBED_R_NONE, 0); continue; }
+    Acc x = soa[f * n + t0 * max_kept + k];
+    for (int64_t t = t0 + 1; t < t1; ++t)
+      x = acc_combine(x, soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+    fin[f][0] = x;
+  }
   finish<1>(P, T, fin, ooff);
 }
 

@@ -620,7 +620,25 @@ class FusedLaunch:
         self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device) if ws_bytes else None
         self.ws_bytes = ws_bytes
 
+    groups = None
+
+    def set_groups(self, group_start):
+        """Rows are pieces; group_start (ngroups + 1) delimits the pieces of
+        each output box (partials mode: run() adds the grouped finish)."""
+        import torch
+
+        self.ngroups = len(group_start) - 1
+        self.groups = torch.from_numpy(np.ascontiguousarray(group_start)).to(self.d_prog.device)
+
     def run(self, stream):
+        self._run(stream)
+        if self.groups is not None:
+            nat.check(nat.lib().cubed_fused_finish_groups(
+                self.prog, self.d_prog.data_ptr(), self.table.data_ptr(), self.ntasks, self.max_kept,
+                self.ws.data_ptr(), self.groups.data_ptr(), self.ngroups, stream),
+                "cubed_fused_finish_groups")
+
+    def _run(self, stream):
         for g in self.gathers:
             g.run(stream)
         L = nat.lib()
@@ -810,16 +828,25 @@ class Lowerer:
         # ---- per-task views
         kinds = [self.leaf_kind(l) for l in leaves]
         gathers = []
+        group_start = None
         if rows_fn is not None:
             rows, red_axes = rows_fn(leaves, kinds)
             n = len(rows[0].extent)
         else:
             red_axes = set(program.reduce.axes) if program.reduce is not None else set()
             n = program.ndim
-            rows = []
+            rows, group_keys = [], []
             for key in task_keys:
-                rows.append(self.task_layout(program, spec, target, key, leaves, out_items,
-                                             structured_out, gathers))
+                r, gk = self.task_pieces(program, spec, target, key, leaves, out_items,
+                                         structured_out, gathers)
+                rows += r
+                group_keys += gk
+            if program.reduce is not None and len(set(group_keys)) < len(group_keys):
+                # pieces reduce into shared outputs: partials + grouped finish
+                partials = True
+                starts = [i for i in range(len(group_keys))
+                          if i == 0 or group_keys[i] != group_keys[i - 1]]
+                group_start = np.array(starts + [len(group_keys)], dtype=np.int64)
         layout = canonicalize(rows, n, red_axes, leaves, kinds)
         P.ndim = layout.ndim
         P.nred = layout.nred
@@ -832,8 +859,11 @@ class Lowerer:
             P.mode |= MODE_PARTIALS
         table = layout.table(self.ctx.device)
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
-        return FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
-                           gathers, self.ctx.device)
+        launch = FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
+                             gathers, self.ctx.device)
+        if group_start is not None:
+            launch.set_groups(group_start)
+        return launch
 
     def leaf_kind(self, leaf) -> int:
         if isinstance(leaf, ir.Philox):
@@ -866,14 +896,25 @@ class Lowerer:
         return None
 
     # -- one task's views (program space order) --------------------------------
-    def task_layout(self, program, spec, target, key, leaves, out_items, structured_out, gathers):
+    def task_layout(self, program, spec, target, key, leaves, out_items, structured_out, gathers,
+                    straddles=None):
+        """One task's TaskRow.  With ``straddles`` (a list), Region leaves
+        whose region spans several source chunks are not gathered: they get
+        a placeholder view (the region's own C strides, base 0) and are
+        recorded as (leaf index, array, region, field) for task_pieces."""
         n = program.ndim
         key = tuple(key)
         args = spec.block_function(("out",) + key)
         args = [list(a) if not isinstance(a, (tuple, list, str)) else a for a in args]
         extent = [None] * n
         leaf_views = []
-        for leaf in leaves:
+        for i, leaf in enumerate(leaves):
+            if straddles is not None and isinstance(leaf, ir.Region):
+                sv = self.straddle_view(leaf, args)
+                if sv is not None:
+                    straddles.append((i,) + sv[1:])
+                    leaf_views.append((LEAF_ARRAY, sv[0]))
+                    continue
             leaf_views.append(self.leaf_view(leaf, args, spec, gathers, key))
         # output views
         out_views = []
@@ -932,6 +973,115 @@ class Lowerer:
             if kind in (LEAF_PHILOX, LEAF_OFFSET):
                 block_offset = v.block_offset
         return TaskRow(extent, bases, lstrides, obases, ostrides, key_lo, key_hi, block_offset)
+
+    def straddle_view(self, leaf, args):
+        """(placeholder view, array, region, field) for a Region leaf whose
+        unit-step slice region spans several chunks, else None."""
+        block_id = tuple(args[leaf.block_arg][1:])
+        region = leaf.region(block_id)
+        if any(isinstance(r, list) or (isinstance(r, slice) and (r.step or 1) != 1) for r in region):
+            return None
+        arr = self.ctx.device_source(leaf.target)
+        if not isinstance(arr, DeviceArray):
+            return None
+        if region_view(arr, region, leaf.field) is not None:
+            return None
+        keys = region_chunk_keys(arr, region)
+        if keys is not None and merged_view(arr, keys, leaf.field) is not None:
+            return None
+        ext = []
+        for d, r in enumerate(region):
+            if isinstance(r, slice):
+                start, stop = r.start or 0, r.stop if r.stop is not None else arr.shape[d]
+                ext.append(max(0, stop - start))
+            else:
+                ext.append(1)
+        v = ArrView(0, ext, list(c_strides(ext)), arr.field_dtype(leaf.field))
+        return v, arr, region, leaf.field
+
+    def task_pieces(self, program, spec, target, key, leaves, out_items, structured_out, gathers):
+        """The task as one or more TaskRows: when Region leaves straddle
+        source chunks (``a[1:]`` of index, core/ops.py:374-486, whose output
+        chunks overlap two input chunks), the task's space is cut at the
+        chunk boundaries into pieces that each read single chunks in place --
+        instead of gathering the region into scratch (a full extra write +
+        read).  Returns (rows, group keys): pieces of one task with equal
+        kept-dim intervals form one group, whose partials (if the program
+        reduces across a cut) are combined before the epilogue."""
+        straddles = [] if not any(isinstance(l, ir.Philox) for l in leaves) else None
+        row = self.task_layout(program, spec, target, key, leaves, out_items, structured_out,
+                               gathers, straddles=straddles)
+        if not straddles:
+            return [row], [(tuple(key), ())]
+        n = program.ndim
+        red = set(program.reduce.axes) if program.reduce is not None else set()
+        cuts = [{0, row.extent[d]} for d in range(n)]
+        piece_lists = []
+        for l, arr, region, field in straddles:
+            axes = leaves[l].axes
+            plist = []
+            for coords, local, offs in region_pieces(arr, region):
+                off_d, k = [], 0
+                for d, r in enumerate(region):
+                    if isinstance(r, slice):
+                        off_d.append(offs[k])
+                        k += 1
+                    else:
+                        off_d.append(0)
+                iv = {}
+                for d, sd in enumerate(axes):
+                    if sd is not None and isinstance(region[d], slice):
+                        lo, cnt = off_d[d], local[d][1]
+                        iv[sd] = (lo, lo + cnt, d)
+                        cuts[sd].update((lo, lo + cnt))
+                plist.append((coords, local, iv))
+            piece_lists.append(plist)
+        bounds = [sorted(c) for c in cuts]
+        intervals = [list(zip(b[:-1], b[1:])) for b in bounds]
+        rows, groups = [], []
+        kept = [d for d in range(n) if d not in red]
+        for box in itertools.product(*intervals):
+            lo = [b[0] for b in box]
+            ext = [b[1] - b[0] for b in box]
+            bases = list(row.bases)
+            lstr = [list(st) for st in row.lstrides]
+            for l in range(len(leaves)):
+                if isinstance(leaves[l], (ir.Arg, ir.Region)) or isinstance(leaves[l], ir.Iota):
+                    isz = np.dtype(leaves[l].dtype).itemsize if not isinstance(leaves[l], ir.Iota) else 1
+                    bases[l] = row.bases[l] + sum(lo[d] * row.lstrides[l][d] for d in range(n)) * isz
+            for (l, arr, region, field), plist in zip(straddles, piece_lists):
+                hit = None
+                for coords, local, iv in plist:
+                    if all(iv[sd][0] <= lo[sd] and lo[sd] + ext[sd] <= iv[sd][1] for sd in iv):
+                        hit = (coords, local, iv)
+                        break
+                if hit is None:
+                    raise LoweringError("region piece not found for a task sub-box")
+                coords, local, iv = hit
+                inner = c_strides(arr.chunk_extent(coords))
+                isz = arr.field_dtype(field).itemsize
+                axes = leaves[l].axes
+                off = 0
+                st = [0] * n
+                for d, r in enumerate(region):
+                    ls, _, step = local[d]
+                    sd = axes[d]
+                    pos = ls
+                    if sd is not None and sd in iv:
+                        pos += (lo[sd] - iv[sd][0]) * step
+                        st[sd] = inner[d] * step if ext[sd] != 1 else 0
+                    off += pos * inner[d]
+                bases[l] = arr.chunk_addr(coords, field) + off * isz
+                lstr[l] = st
+            obases = [row.obases[o] + sum(lo[d] * row.ostrides[o][d] for d in range(n)) *
+                      np.dtype(_out_dtype(target, out_items[o][0], structured_out)).itemsize
+                      for o in range(len(row.obases))]
+            rows.append(TaskRow(ext, bases, lstr, obases, [list(x) for x in row.ostrides],
+                                row.key_lo, row.key_hi, row.block_offset))
+            groups.append((tuple(key), tuple(lo[d] for d in kept)))
+        # pieces of one group contiguous, in order along the cut reduced dims
+        order = sorted(range(len(rows)), key=lambda i: (groups[i][1], i))
+        return [rows[i] for i in order], [groups[i] for i in order]
 
     def leaf_view(self, leaf, args, spec, gathers, out_key):
         """(kind, view) for one leaf of one task."""
@@ -1013,6 +1163,10 @@ class Lowerer:
                     boxes.append(Box(sv.base, dst.base + _merged_offset(src, keys, k, dstr) * target.dtype.itemsize,
                                      sv.extent, sv.stride, dstr[:len(sv.extent)]))
         return CopyLaunch(boxes, target.dtype.itemsize, self.ctx.device)
+
+
+def _out_dtype(target, name, structured):
+    return target.field_dtype(name if structured else None)
 
 
 def _merged_offset(src, keys, k, dstr):

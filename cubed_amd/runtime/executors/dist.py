@@ -122,6 +122,8 @@ class RechunkLaunch:
             for p, off in lst:
                 d, ds = dst_box(p)
                 unpack.append(Box(rbase + off, d, list(p.extent), list(c_strides(p.extent)), ds))
+        local.sort(key=lambda b: b.src)
+        pack.sort(key=lambda b: b.src)
         self.local = CopyLaunch(local, isz, ctx.device)
         self.pack = CopyLaunch(pack, isz, ctx.device)
         self.unpack = CopyLaunch(unpack, isz, ctx.device)

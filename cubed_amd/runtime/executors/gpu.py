@@ -421,6 +421,9 @@ class GpuDagExecutor(DagExecutor):
             region = tuple(slice(s, s + e) for s, e in zip(dst.chunk_start(key), dst.chunk_extent(key)))
             dv = chunk_view(dst, key)
             boxes += boxes_for_region(src, region, dv.base, dv.stride)
+        # source order: workgroups in flight together read neighbouring source
+        # rows (measured 3.6 vs 4.05 ms on the 50000^2 rows -> columns case)
+        boxes.sort(key=lambda b: b.src)
         return CopyLaunch(boxes, dst.dtype.itemsize, self.device)
 
     def _lower_gemm(self, program, cfg, target, keys):
@@ -644,8 +647,11 @@ class GpuDagExecutor(DagExecutor):
         total = 0
         for _, d in dag.nodes(data=True):
             t = d.get("target")
-            if isinstance(t, DeviceArray):
-                total += t.device_bytes()
+            if isinstance(t, DeviceArray) and id(t) not in self.elided:
+                if t.allocated:
+                    total += t.device_bytes()
+                else:  # this rank's block-cyclic share, at most
+                    total += -(-t.nchunks // self.world) * sum(t.slot_bytes(f) for f in t.fields)
         if total > HBM_BYTES_PER_GPU:
             raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")

@@ -235,6 +235,16 @@ int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
 int cubed_fused_finish(const cubed_program_t* prog, const cubed_program_t* d_prog,
                        const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                        const void* d_partials, void* stream);
+/* Grouped finish (partials mode): tasks [group_start[g], group_start[g+1]) are
+ * pieces of ONE output box -- a task split where its inputs straddle source
+ * chunks along a reduced dim (e.g. the a[1:] regions of index/map_direct,
+ * core/ops.py:374-486, feeding a reduction) -- whose partials are combined in
+ * piece order; the first piece's output views get the epilogue.
+ * d_group_start: ngroups + 1 int64 in device memory. */
+int cubed_fused_finish_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                              const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                              const void* d_partials, const int64_t* d_group_start,
+                              int64_t ngroups, void* stream);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);

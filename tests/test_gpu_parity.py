@@ -332,6 +332,36 @@ def test_index_slice_and_mean(ex):
     assert np.isclose(got, exp, rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("expr", ["map", "sum0", "sum1", "mean_all", "max0"])
+def test_straddling_regions_as_pieces(ex, expr):
+    """index regions that straddle source chunks run as per-chunk pieces
+    (no scratch gather): maps write disjoint sub-boxes; reductions across a
+    cut combine the pieces' partials in order (grouped finish)."""
+    rng = np.random.default_rng(13)
+    A = rng.random((23, 17, 9))
+    B = rng.random((23, 17, 9))
+    spec = mkspec(ex)
+    a = cubed.from_array(A, chunks=(5, 6, 9), spec=spec)
+    b = cubed.from_array(B, chunks=(5, 6, 9), spec=spec)
+    sa, sb = a[2:, 1:], b[:-2, :-1]
+    SA, SB = A[2:, 1:], B[:-2, :-1]
+    if expr == "map":
+        got, exp = (sa * 2 + sb).compute(), SA * 2 + SB
+        assert np.array_equal(got, exp)
+        return
+    if expr == "sum0":
+        got, exp = xp.sum(sa * sb, axis=0).compute(), (SA * SB).sum(axis=0)
+    elif expr == "sum1":
+        got, exp = xp.sum(sa - sb, axis=1).compute(), (SA - SB).sum(axis=1)
+    elif expr == "mean_all":
+        got, exp = xp.mean(sa + sb).compute(), np.mean(SA + SB)
+    else:
+        got, exp = xp.max(sa * sb, axis=0).compute(), (SA * SB).max(axis=0)
+        assert np.array_equal(got, exp)
+        return
+    assert np.allclose(got, exp, rtol=1e-12, atol=0)
+
+
 # ----------------------------------------------------------- callbacks / resume
 
 

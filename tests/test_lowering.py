@@ -174,3 +174,24 @@ def test_where_producers_fuse_into_one_read(built, dry):
     arrays_to_plan(w).execute(executor=dry, resume=True, array_names=[w.name])
     fused = _fused(dry)
     assert len(fused) == 1 and fused[0].prog.nleaves == 1  # the 0.5 scalar is a constant
+
+
+def test_vorticity_regions_are_pieces_not_gathers(built, dry):
+    """mean(a[1:] * x + b[1:] * y) (config 4 shape): each a[1:] chunk
+    straddles two source chunks along the reduced time axis -> two pieces
+    per task reading in place, partials combined per task; no scratch."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(1)
+    a = crandom.random((40, 18, 16), chunks=(10, 9, 8), spec=spec)
+    b = crandom.random((40, 18, 16), chunks=(10, 9, 8), spec=spec)
+    x = crandom.random((18, 16), chunks=(9, 8), spec=spec)
+    y = crandom.random((18, 16), chunks=(9, 8), spec=spec)
+    arrays_to_plan(a, b, x, y).execute(executor=dry, array_names=[a.name, b.name, x.name, y.name])
+    dry.launched.clear()
+    m = xp.mean(a[1:] * x + b[1:] * y)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    first = fused[0]
+    assert not first.gathers and first.groups is not None
+    assert first.prog.mode & 16  # partials + grouped finish
+    assert first.ntasks > first.ngroups
