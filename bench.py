@@ -215,6 +215,35 @@ def rechunk_extra(ex, rank):
                 ms=dt * 1e3, ops=nops, bytes_moved_per_op=2 * x.nbytes, launches_ms=launches)
 
 
+def rechunk_mean_extra(ex, rank):
+    """configs[2] "rechunk+reduce": mean(x.rechunk(columns), axis=0) with x
+    50000^2 f32 in row chunks.  The rechunk feeds only the mean, so the
+    executor reads it through (rewrites.elide_rechunks): each GPU reduces the
+    row-chunk pieces it holds; with N GPUs the partials are combined over
+    RCCL.  value = x bytes / time."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    N = 50000
+    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+    random.seed(2000)
+    x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+    m = xp.mean(x.rechunk((N, 1000)), axis=0)
+    plan = arrays_to_plan(m)
+
+    def step():
+        _reset_targets(plan, x)
+        plan.execute(executor=ex, resume=True, array_names=[m.name])
+
+    step()
+    dt, launches = timed_launches(ex, step, 5, ex.world)
+    return dict(metric="rechunk+mean effective input GB/s", value=x.nbytes / dt / 1e9,
+                ms=dt * 1e3, launches_ms=launches)
+
+
 def _exec_only(plan, ex, y, x):
     # re-run every rechunk op (x stays resident)
     from cubed_amd.storage import DeviceArray
@@ -382,6 +411,10 @@ def main():
             extra["rechunk"] = rechunk_extra(ex, rank)
         except Exception as e:  # pragma: no cover - reported, not fatal
             extra["rechunk"] = {"error": repr(e)}
+        try:
+            extra["rechunk_mean"] = rechunk_mean_extra(ex, rank)
+        except Exception as e:  # pragma: no cover
+            extra["rechunk_mean"] = {"error": repr(e)}
         try:
             extra["config1"] = config1_extra(ex, rank)
         except Exception as e:  # pragma: no cover

@@ -1,0 +1,130 @@
+"""Executor-side rewrites of a finalized DAG that remove whole passes over
+HBM without changing any value.
+
+``elide_rechunks``: a rechunk (cubed/core/ops.py:702-758 ->
+primitive/rechunk.py:23-98, one copy op or two through an intermediate)
+whose result feeds exactly ONE blockwise op and is not requested is not
+materialised.  The consumer reads the rechunk's SOURCE instead: each of its
+tasks reads the box its input chunk covers, as a ``Region`` of the source
+(the same leaf kind as ``index``/``merge_chunks``' map_direct regions,
+core/ops.py:374-517, 646-699).  The lowering cuts such tasks at the source
+chunk boundaries into pieces that read in place (lowering.task_pieces); a
+reduction combines its pieces' partials before the epilogue.  Rechunk is a
+pure layout change (values bit-identical), so the consumer computes the same
+elementwise values; reductions regroup their per-field sums at the source's
+chunk boundaries (within the DESIGN.md tolerances).
+
+The copy (2 x the array in HBM traffic) and the consumer's re-read of the
+copy disappear: ``rechunk + mean`` reads the source once.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import List
+
+from . import ir
+from .primitive.blockwise import apply_blockwise
+from .primitive.rechunk import copy_read_to_write
+from .primitive.types import CubedArrayProxy
+from .storage import DeviceArray
+
+
+def _box_of(grid):
+    def region(block_id):
+        return tuple(slice(s, s + e) for s, e in zip(grid.chunk_start(block_id), grid.chunk_extent(block_id)))
+    return region
+
+
+def elide_rechunks(dag, array_names):
+    """Returns (rewritten DAG copy, elided targets)."""
+    import networkx as nx
+
+    from .chains import _arg_arrays
+    from .core.optimization import predecessors
+
+    requested = set(array_names or ())
+    dag = dag.copy()
+    elided: List = []
+    for name in list(nx.topological_sort(dag)):
+        if name not in dag:
+            continue
+        nd = dag.nodes[name]
+        if "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
+            continue
+        spec = nd["pipeline"].config
+        program = spec.function
+        if not isinstance(program, ir.ExprProgram):
+            continue
+        target = nd["primitive_op"].target_array
+        args_names = _arg_arrays(spec, target)
+        if args_names is None:
+            continue
+        sample = spec.block_function(("out",) + (0,) * len(getattr(target, "numblocks", ())))
+        for i, yname in enumerate(args_names):
+            if yname not in dag or yname in requested or dag.out_degree(yname) != 1:
+                continue
+            if not isinstance(sample[i], tuple):
+                continue  # the consumer reads several chunks per task: keep the rechunk
+            # walk back through the rechunk's copy op(s): y <- R [<- int <- R1] <- x
+            removed, cur, x_name, x_target = [], yname, None, None
+            while True:
+                pres = list(predecessors(dag, cur))
+                if len(pres) != 1:
+                    break
+                op = pres[0]
+                od = dag.nodes[op]
+                if "pipeline" not in od or od["pipeline"].function is not copy_read_to_write:
+                    break
+                srcs = [p for p in predecessors(dag, op) if p != "arrays"]
+                if len(srcs) != 1:
+                    break
+                removed += [op, cur]
+                cur = srcs[0]
+                x_name, x_target = cur, od["pipeline"].config.read.array
+                cd = dag.nodes[cur]
+                is_int = any("pipeline" in dag.nodes[p] and
+                             dag.nodes[p]["pipeline"].function is copy_read_to_write
+                             for p in predecessors(dag, cur))
+                if not (is_int and dag.out_degree(cur) == 1 and cur not in requested):
+                    break
+            if x_name is None or not isinstance(x_target, DeviceArray):
+                continue
+            y_target = dag.nodes[yname].get("target")
+            if y_target is None or tuple(y_target.shape) != tuple(x_target.shape):
+                continue
+            region_fn = _box_of(y_target)
+
+            def swap(leaf, i=i, region_fn=region_fn, x_name=x_name, x_target=x_target):
+                if isinstance(leaf, ir.Arg) and leaf.index == i:
+                    return ir.Region(x_name, leaf.dtype, leaf.axes, region_fn, i, leaf.field, x_target)
+                return None
+
+            memo = {}
+            if program.structured:
+                outputs = tuple((n, ir.transform(e, swap, memo)) for n, e in program.outputs)
+            else:
+                outputs = ir.transform(program.outputs, swap, memo)
+            reduce = program.reduce
+            if reduce is not None:
+                reduce = dataclasses.replace(reduce, fields=tuple(
+                    dataclasses.replace(f, expr=ir.transform(f.expr, swap, memo)) for f in reduce.fields))
+            program = dataclasses.replace(program, outputs=outputs, reduce=reduce)
+            reads = dict(spec.reads_map)
+            reads[x_name] = CubedArrayProxy(x_target, x_target.chunks)
+            spec = dataclasses.replace(spec, function=program, reads_map=reads)
+            pipeline = dataclasses.replace(nd["pipeline"], config=spec)
+            nd["pipeline"] = pipeline
+            nd["primitive_op"] = dataclasses.replace(nd["primitive_op"], pipeline=pipeline)
+            fused_from = list(nd.get("fused_from", ()))
+            for n2 in removed:
+                d2 = dag.nodes[n2]
+                if "primitive_op" in d2:
+                    fused_from.append((n2, d2["primitive_op"].num_tasks))
+                elif isinstance(d2.get("target"), DeviceArray):
+                    elided.append(d2["target"])
+            nd["fused_from"] = fused_from
+            for n2 in removed:
+                dag.remove_node(n2)
+            dag.add_edge(x_name, name)
+    return dag, elided

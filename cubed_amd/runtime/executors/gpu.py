@@ -160,6 +160,7 @@ class GpuDagExecutor(DagExecutor):
         self._chains: Dict = {}
         self._exec_dags: Dict = {}
         self.fuse_producers = True
+        self.elide_rechunks = True
         self._agreed = set()
         self.elided = set()
 
@@ -556,17 +557,25 @@ class GpuDagExecutor(DagExecutor):
 
     def exec_dag(self, dag, array_names):
         """The DAG this executor runs: the plan's finalized DAG with
-        single-consumer elementwise maps fused into their consumers
-        (chains.fuse_elementwise_producers), cached per plan DAG."""
-        if not self.fuse_producers:
+        single-consumer rechunks read through by their consumer
+        (rewrites.elide_rechunks) and single-consumer elementwise maps fused
+        into their consumers (chains.fuse_elementwise_producers), cached per
+        plan DAG."""
+        if not (self.fuse_producers or self.elide_rechunks):
             return dag
         key = (id(dag), tuple(array_names or ()))
         entry = self._exec_dags.get(key)
         if entry is not None and entry[0]() is dag:
             return entry[1]
         from ...chains import fuse_elementwise_producers
+        from ...rewrites import elide_rechunks
 
-        new, absorbed = fuse_elementwise_producers(dag, array_names)
+        new, absorbed = dag, []
+        if self.elide_rechunks:
+            new, absorbed = elide_rechunks(new, array_names)
+        if self.fuse_producers:
+            new, more = fuse_elementwise_producers(new, array_names)
+            absorbed += more
         for t in absorbed:
             if isinstance(t, DeviceArray):
                 self.elided.add(id(t))

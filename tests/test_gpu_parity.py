@@ -362,6 +362,29 @@ def test_straddling_regions_as_pieces(ex, expr):
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("mem", [10**9, 60_000])
+@pytest.mark.parametrize("op", ["mean0", "sum1", "map", "both"])
+def test_rechunk_read_through(ex, mem, op):
+    """A rechunk consumed by one op is read through (rewrites.elide_rechunks):
+    the consumer reads the source's chunks in place, values unchanged (maps
+    bit-exact, reductions rtol 1e-12).  mem=60 kB forces the reference's
+    two-op rechunk through an intermediate."""
+    x = np.random.default_rng(14).random((60, 50))
+    spec = cubed.Spec(allowed_mem=mem, executor=ex)
+    a = cubed.from_array(x, chunks=(10, 50), spec=spec)
+    b = a.rechunk((60, 10))
+    if op == "mean0":
+        assert np.allclose(xp.mean(b, axis=0).compute(), x.mean(axis=0), rtol=1e-12, atol=0)
+    elif op == "sum1":
+        assert np.allclose(xp.sum(b, axis=1).compute(), x.sum(axis=1), rtol=1e-12, atol=0)
+    elif op == "map":
+        assert np.array_equal((b * 3 + 1).compute(), x * 3 + 1)
+    else:  # the rechunked array is also requested: not elided
+        c = b * 2
+        got_b, got_c = cubed.compute(b, c) if hasattr(cubed, "compute") else (b.compute(), c.compute())
+        assert np.array_equal(got_b, x) and np.array_equal(got_c, x * 2)
+
+
 # ----------------------------------------------------------- callbacks / resume
 
 

@@ -195,3 +195,30 @@ def test_vorticity_regions_are_pieces_not_gathers(built, dry):
     assert not first.gathers and first.groups is not None
     assert first.prog.mode & 16  # partials + grouped finish
     assert first.ntasks > first.ngroups
+
+
+def test_rechunk_then_mean_reads_the_source(built, dry):
+    """rechunk rows -> columns then mean(axis=0): no copy launch; the mean's
+    tasks are cut into per-source-chunk pieces (partials + grouped finish)."""
+    spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+    random.seed(1)
+    x = xp.astype(crandom.random((500, 500), chunks=(10, 500), spec=spec), xp.float32)
+    arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
+    dry.launched.clear()
+    m = xp.mean(x.rechunk((500, 10)), axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    assert not [l for l in dry.launched if isinstance(l, CopyLaunch)]
+    fused = _fused(dry)
+    assert len(fused) == 1 and fused[0].ntasks == 50 * 50 and fused[0].ngroups == 50
+    assert not fused[0].gathers
+
+
+def test_requested_rechunk_is_kept(built, dry):
+    spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+    x = cubed.from_array(np.ones((60, 50)), chunks=(10, 50), spec=spec)
+    arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
+    dry.launched.clear()
+    y = x.rechunk((60, 10))
+    z = y * 2
+    arrays_to_plan(y, z).execute(executor=dry, resume=True, array_names=[y.name, z.name])
+    assert [l for l in dry.launched if isinstance(l, CopyLaunch)]

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from cubed_amd.runtime.executors.gpu import GpuDagExecutor  # noqa: E402
 
-FUNCS = {"rechunk": bench.rechunk_extra, "config1": bench.config1_extra,
+FUNCS = {"rechunk": bench.rechunk_extra, "rechunk_mean": bench.rechunk_mean_extra, "config1": bench.config1_extra,
          "vorticity": bench.vorticity_extra, "matmul": bench.matmul_extra}
 
 if __name__ == "__main__":
