@@ -441,6 +441,33 @@ CUBED_DEV void finish_groups_body(
   finish<1>(P, T, fin, ooff);
 }
 
+// Per-group combine without the epilogue (multi-GPU pieces): rows
+// [gs[g], gs[g+1]) of the row partials fold, in row order, into
+// out[f][g][k] (max_kept_out per group, identity past a group's extent) --
+// the same layout on every rank, for the cross-rank combine.
+CUBED_DEV void combine_groups_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    int64_t max_kept_out, Acc* __restrict__ out, int kd0, int kd1) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t g = i / max_kept_out, k = i % max_kept_out;
+  if (g >= ngroups) return;
+  const int64_t t0 = gs[g], t1 = gs[g + 1];
+  const cubed_task_t* __restrict__ T = tasks + t0;
+  int64_t nk = 1;
+  for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+  const int64_t n = ntasks * max_kept, no = ngroups * max_kept_out;
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+    Acc x = acc_init(P.field_rop[f], P.field_acc[f]);
+    if (k < nk) {
+      x = soa[f * n + t0 * max_kept + k];
+      for (int64_t t = t0 + 1; t < t1; ++t)
+        x = acc_combine(x, soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+    }
+    out[f * no + i] = x;
+  }
+}
+
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in
 // part order: out[f][i] = part0 (+) part1 (+) ...  Used for the fields RCCL
 // cannot reduce with numpy's semantics (max/min with NaN, prod, any/all).

@@ -653,3 +653,11 @@ def acc_is_int(rop: str, dtype) -> bool:
     if rop in ("count", "count_nonnan", "any", "all"):
         return True
     return dtype.kind in "iub"
+
+
+def leaves_of_program(p) -> List[Expr]:
+    """Every leaf of an ExprProgram's outputs and reduced fields."""
+    out: List[Expr] = []
+    for e in p.all_exprs():
+        leaves(e, out)
+    return out

@@ -861,6 +861,7 @@ class Lowerer:
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
         launch = FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
                              gathers, self.ctx.device)
+        launch.layout = layout
         if group_start is not None:
             launch.set_groups(group_start)
         return launch
@@ -999,7 +1000,8 @@ class Lowerer:
         v = ArrView(0, ext, list(c_strides(ext)), arr.field_dtype(leaf.field))
         return v, arr, region, leaf.field
 
-    def task_pieces(self, program, spec, target, key, leaves, out_items, structured_out, gathers):
+    def task_pieces(self, program, spec, target, key, leaves, out_items, structured_out, gathers,
+                    reads_out=None):
         """The task as one or more TaskRows: when Region leaves straddle
         source chunks (``a[1:]`` of index, core/ops.py:374-486, whose output
         chunks overlap two input chunks), the task's space is cut at the
@@ -1007,11 +1009,17 @@ class Lowerer:
         instead of gathering the region into scratch (a full extra write +
         read).  Returns (rows, group keys): pieces of one task with equal
         kept-dim intervals form one group, whose partials (if the program
-        reduces across a cut) are combined before the epilogue."""
+        reduces across a cut) are combined before the epilogue.
+
+        ``reads_out`` (a list) receives, per returned row, the
+        (array, chunk coords, field) of every Region chunk the row reads
+        (the multi-GPU executor runs each piece where that chunk lives)."""
         straddles = [] if not any(isinstance(l, ir.Philox) for l in leaves) else None
         row = self.task_layout(program, spec, target, key, leaves, out_items, structured_out,
                                gathers, straddles=straddles)
         if not straddles:
+            if reads_out is not None:
+                reads_out.append([r[:3] for r in self._region_chunks(leaves, spec, key)])
             return [row], [(tuple(key), ())]
         n = program.ndim
         red = set(program.reduce.axes) if program.reduce is not None else set()
@@ -1038,9 +1046,12 @@ class Lowerer:
             piece_lists.append(plist)
         bounds = [sorted(c) for c in cuts]
         intervals = [list(zip(b[:-1], b[1:])) for b in bounds]
-        rows, groups = [], []
+        rows, groups, reads = [], [], []
         kept = [d for d in range(n) if d not in red]
+        straddled = {l for l, *_ in straddles}
+        fixed = [r for r in self._region_chunks(leaves, spec, key) if r[3] not in straddled]
         for box in itertools.product(*intervals):
+            row_reads = [r[:3] for r in fixed]
             lo = [b[0] for b in box]
             ext = [b[1] - b[0] for b in box]
             bases = list(row.bases)
@@ -1058,6 +1069,7 @@ class Lowerer:
                 if hit is None:
                     raise LoweringError("region piece not found for a task sub-box")
                 coords, local, iv = hit
+                row_reads.append((arr, tuple(coords), field))
                 inner = c_strides(arr.chunk_extent(coords))
                 isz = arr.field_dtype(field).itemsize
                 axes = leaves[l].axes
@@ -1079,9 +1091,28 @@ class Lowerer:
             rows.append(TaskRow(ext, bases, lstr, obases, [list(x) for x in row.ostrides],
                                 row.key_lo, row.key_hi, row.block_offset))
             groups.append((tuple(key), tuple(lo[d] for d in kept)))
+            reads.append(row_reads)
         # pieces of one group contiguous, in order along the cut reduced dims
         order = sorted(range(len(rows)), key=lambda i: (groups[i][1], i))
+        if reads_out is not None:
+            reads_out += [reads[i] for i in order]
         return [rows[i] for i in order], [groups[i] for i in order]
+
+    def _region_chunks(self, leaves, spec, key):
+        """(array, coords, field, leaf index) of every chunk the task's
+        Region leaves read."""
+        args = spec.block_function(("out",) + tuple(key))
+        args = [list(a) if not isinstance(a, (tuple, list, str)) else a for a in args]
+        out = []
+        for l, leaf in enumerate(leaves):
+            if isinstance(leaf, ir.Region):
+                arr = self.ctx.device_source(leaf.target)
+                if not isinstance(arr, DeviceArray):
+                    continue
+                region = leaf.region(tuple(args[leaf.block_arg][1:]))
+                for coords, _, _ in region_pieces(arr, region):
+                    out.append((arr, tuple(coords), leaf.field, l))
+        return out
 
     def leaf_view(self, leaf, args, spec, gathers, out_key):
         """(kind, view) for one leaf of one task."""

@@ -234,3 +234,64 @@ def gather_distributed(arr: DeviceArray) -> np.ndarray:
                 else:
                     out[f][sl] = vals
     return out
+
+
+class DistPiecesLaunch:
+    """A reduction whose tasks are cut into pieces at source-chunk boundaries
+    (index regions, rechunk read-through) run where the pieces' chunks live:
+    each rank reduces its pieces of EVERY output group in partials mode,
+    folds them per group (cubed_combine_groups), the per-group partials are
+    combined over RCCL, and the owners of the outputs run the epilogue
+    (cubed_fused_finish over one row per group)."""
+
+    def __init__(self, ctx, fused, group_start, group_table, max_kept_out, rops, acc_int, owners):
+        import torch
+
+        self.ctx = ctx
+        self.fused = fused
+        self.ngroups = len(group_start) - 1
+        self.gs = torch.from_numpy(np.ascontiguousarray(group_start, dtype=np.int64)).to(ctx.device)
+        self.group_table = group_table
+        self.mko = max_kept_out
+        self.nf = len(rops)
+        self.n = self.ngroups * max_kept_out
+        self.gsoa = torch.empty(max(self.nf * self.n * 8, 16), dtype=torch.uint8, device=ctx.device)
+        self.sum_only = all(r in SUM_ROPS for r in rops)
+        self.acc_int = acc_int
+        uniq = sorted(set(owners))
+        self.root = uniq[0] if len(uniq) == 1 else None
+        self.finish_here = ctx.rank in uniq
+        if not self.sum_only:
+            self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8, device=ctx.device)
+
+    def field_view(self, f):
+        import torch
+
+        raw = self.gsoa[f * self.n * 8:(f + 1) * self.n * 8]
+        return raw.view(torch.int64 if self.acc_int[f] else torch.float64)
+
+    def run(self, stream):
+        F = self.fused
+        L = nat.lib()
+        F.run(stream)
+        nat.check(L.cubed_combine_groups(F.prog, F.d_prog.data_ptr(), F.table.data_ptr(), F.ntasks,
+                                         F.max_kept, F.ws.data_ptr(), self.gs.data_ptr(), self.ngroups,
+                                         self.mko, self.gsoa.data_ptr(), stream), "cubed_combine_groups")
+        comm = self.ctx.comm
+        if self.sum_only:
+            for f in range(self.nf):
+                v = self.field_view(f)
+                if self.root is not None:
+                    comm.reduce_sum(v, self.root)
+                else:
+                    comm.all_reduce_sum(v)
+        else:
+            comm.all_gather(self.gathered, self.gsoa[: self.nf * self.n * 8])
+            if self.finish_here:
+                nat.check(L.cubed_combine_partials(F.prog, F.d_prog.data_ptr(), self.gathered.data_ptr(),
+                                                   comm.world, self.n, self.gsoa.data_ptr(), stream),
+                          "cubed_combine_partials")
+        if self.finish_here:
+            nat.check(L.cubed_fused_finish(F.prog, F.d_prog.data_ptr(), self.group_table.data_ptr(),
+                                           self.ngroups, self.mko, self.gsoa.data_ptr(), stream),
+                      "cubed_fused_finish")

@@ -327,6 +327,12 @@ class GpuDagExecutor(DagExecutor):
         fetched first (FetchLaunch) and the task views point at the copies."""
         if self.world == 1:
             return self._lower_local(program, cfg, target, keys)
+        if isinstance(program, ir.ExprProgram) and program.reduce is not None and \
+                any(isinstance(l, ir.Region) for l in ir.leaves_of_program(program)):
+            launches = self._lower_pieces_dist(program, cfg, target, keys)
+            # every rank must take the same path (their collectives pair up)
+            if self.comm.all_ok(launches is not None):
+                return launches
         owned = [k for k in keys if target.owner(k) == self.rank]
         fetch, arrays = self._plan_fetch(
             {k: target.owner(k) for k in keys},
@@ -338,12 +344,99 @@ class GpuDagExecutor(DagExecutor):
             out += self._lower_local(program, cfg, target, owned)
         return out
 
+    def _lower_pieces_dist(self, program, cfg, target, keys):
+        """A reduction over Region leaves (index / merge regions, a rechunk
+        read through) on several GPUs: every task is cut into pieces at the
+        source chunk boundaries and each piece runs on the rank that holds its
+        chunk (dist.DistPiecesLaunch), so the source never crosses xGMI --
+        only per-group partials do.  None when the program does not fit this
+        shape (the caller then fetches whole chunks instead)."""
+        import dataclasses
+
+        from ...storage import geometry_only
+        from .dist import DistPiecesLaunch
+
+        rank = self.rank
+        low = self.lowerer
+        red = set(program.reduce.axes)
+        meta = {"discard": self.scratch(max(target.slot_bytes(f) for f in target.fields))}
+
+        def home_of(reads, key):
+            for arr, coords, _ in reads:
+                if arr.world > 1:
+                    return arr.owner(coords)
+            return target.owner(key)
+
+        def rows_fn(leaves, kinds):
+            out_items = list(program.output_items())
+            # pass 1: geometry of every piece of every task -> homes, fetch needs
+            per_task = {}
+            with geometry_only():
+                for key in keys:
+                    reads, gathers = [], []
+                    r, g = low.task_pieces(program, cfg, target, key, leaves, out_items,
+                                           program.structured, gathers, reads_out=reads)
+                    if gathers:
+                        raise LoweringError("pieces need a scratch gather")
+                    per_task[key] = reads
+            arg_reads = {key: self._task_reads(program, cfg, key, regions=False) for key in keys}
+            home = {(key, i): home_of(rd, key) for key, reads in per_task.items()
+                    for i, rd in enumerate(reads)}
+            fetch, arrays = self._plan_fetch(
+                home, lambda item: list(per_task[item[0]][item[1]]) + arg_reads[item[0]])
+            meta["fetch"] = fetch
+            # pass 2: this rank's pieces with real addresses (fetched chunks
+            # resolved); other ranks' pieces only give their group's shape
+            rows, gkeys = [], []
+            mko = 1
+            with _remote_chunks(fetch, arrays), geometry_only():
+                for key in keys:
+                    r, g = low.task_pieces(program, cfg, target, key, leaves, out_items,
+                                           program.structured, [])
+                    owned_out = target.owner(key) == rank
+                    by_group = {}
+                    for i, (row, gk) in enumerate(zip(r, g)):
+                        by_group.setdefault(gk, []).append((i, row))
+                    for gk, items in by_group.items():
+                        first = items[0][1]
+                        mko = max(mko, math.prod(first.extent[d] for d in range(len(first.extent))
+                                                 if d not in red))
+                        mine = [row for i, row in items if home[(key, i)] == rank]
+                        if not mine:  # no piece here: an empty row yields the identity
+                            e = list(first.extent)
+                            for d in red:
+                                e[d] = 0
+                            mine = [dataclasses.replace(first, extent=e, bases=[0] * len(first.bases))]
+                        for row in mine:
+                            if not owned_out:
+                                row = dataclasses.replace(row, obases=[meta["discard"]] * len(row.obases))
+                            rows.append(row)
+                            gkeys.append((key, gk))
+            meta["starts"] = [i for i in range(len(gkeys)) if i == 0 or gkeys[i] != gkeys[i - 1]]
+            meta["mko"] = mko
+            return rows, red
+
+        try:
+            launch = low.lower_expr_pipeline(program, cfg, target, keys, rows_fn=rows_fn,
+                                             sample_key=keys[0], partials=True)
+        except LoweringError:
+            return None
+        starts = meta["starts"]
+        lay = launch.layout
+        table = dataclasses.replace(lay, rows=[lay.rows[i] for i in starts]).table(self.device)
+        rops = [f.rop for f in program.reduce.fields]
+        acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
+        out = [meta["fetch"]] if meta.get("fetch") is not None else []
+        out.append(DistPiecesLaunch(self, launch, np.array(starts + [len(lay.rows)], dtype=np.int64),
+                                    table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys]))
+        return out
+
     def _lower_local(self, program, cfg, target, keys):
         if isinstance(program, ir.ExprProgram):
             return _with_gathers(self.lowerer.lower_expr_pipeline(program, cfg, target, keys), self.device)
         return [self._lower_gemm(program, cfg, target, keys)]
 
-    def _task_reads(self, program, cfg, key):
+    def _task_reads(self, program, cfg, key, regions=True):
         """(array, chunk coords, field) of every distributed chunk one task
         reads (the apply_blockwise key resolution, primitive/blockwise.py
         :70-76, plus map_direct regions)."""
@@ -372,7 +465,7 @@ class GpuDagExecutor(DagExecutor):
                     continue
                 for k in ([a] if isinstance(a, tuple) else flatten_keys(a)):
                     add_key(k, leaf.field)
-            elif isinstance(leaf, ir.Region):
+            elif isinstance(leaf, ir.Region) and regions:
                 src = self.device_source(leaf.target)
                 if isinstance(src, DeviceArray) and src.world > 1:
                     block_id = tuple(args[leaf.block_arg][1:])

@@ -245,6 +245,16 @@ int cubed_fused_finish_groups(const cubed_program_t* prog, const cubed_program_t
                               const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                               const void* d_partials, const int64_t* d_group_start,
                               int64_t ngroups, void* stream);
+/* Multi-GPU form of the grouped finish: fold each group's rows into
+ * d_group_partials[f][g][k] (max_kept_out per group, identity past a group's
+ * kept extent) WITHOUT the epilogue, so the per-rank group partials -- pieces
+ * of one output box run on the GPUs that hold their source chunks -- can be
+ * combined over RCCL and finished by cubed_fused_finish on the owner. */
+int cubed_combine_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                         const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                         const void* d_row_partials, const int64_t* d_group_start,
+                         int64_t ngroups, int64_t max_kept_out, void* d_group_partials,
+                         void* stream);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);

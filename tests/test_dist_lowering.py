@@ -12,7 +12,12 @@ import cubed_amd.array_api as xp
 import cubed_amd.random as crandom
 from cubed_amd.core.plan import arrays_to_plan
 from cubed_amd.lowering import MODE_PARTIALS, MODE_STREAM, FusedLaunch
-from cubed_amd.runtime.executors.dist import FetchLaunch, PartialsLaunch, RechunkLaunch
+from cubed_amd.runtime.executors.dist import (
+    DistPiecesLaunch,
+    FetchLaunch,
+    PartialsLaunch,
+    RechunkLaunch,
+)
 from dryrun import DryExecutor, FakeComm
 
 
@@ -112,7 +117,7 @@ def _launch_sequence(rank, world):
         dry.launched.clear()
         arrays_to_plan(*arrs).execute(executor=dry, resume=resume, array_names=[a.name for a in arrs])
         seq.append([type(l).__name__ for l in dry.launched
-                    if isinstance(l, (FetchLaunch, RechunkLaunch, PartialsLaunch))])
+                    if isinstance(l, (FetchLaunch, RechunkLaunch, PartialsLaunch, DistPiecesLaunch))])
 
     random.seed(4)
     u = xp.astype(crandom.random((60, 24, 40), chunks=(10, 24, 40), spec=spec), xp.float32)
@@ -129,6 +134,7 @@ def _launch_sequence(rank, world):
     y = np.ones((60, 50), dtype=np.float32)
     go(cubed.from_array(y, chunks=(7, 9), spec=spec).rechunk((13, 4)))
     go(cubed.from_array(y, chunks=(10, 50), spec=spec) + cubed.from_array(y, chunks=(20, 25), spec=spec))
+    go(xp.mean(cubed.from_array(y, chunks=(7, 50), spec=spec).rechunk((60, 9)), axis=0))
     A = cubed.from_array(np.ones((96, 80), np.float32), chunks=(32, 40), spec=spec)
     B = cubed.from_array(np.ones((80, 64), np.float32), chunks=(40, 32), spec=spec)
     go(xp.matmul(A, B))
@@ -143,3 +149,29 @@ def test_ranks_issue_the_same_collectives(built, world):
     for r in range(1, world):
         assert seqs[r] == seqs[0], (r, seqs[0], seqs[r])
     assert ["PartialsLaunch"] in seqs[0] and ["FetchLaunch"] in seqs[0]
+
+
+def test_rechunk_mean_runs_pieces_where_chunks_live(built):
+    """rechunk rows -> columns read through by mean(axis=0) on 4 ranks: each
+    rank runs only the pieces of the source chunks it holds (no fetch, no
+    all-to-all), one partials row per piece plus an identity row for groups
+    without local pieces."""
+    world = 4
+    x = np.ones((500, 500), dtype=np.float32)
+    total = 0
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+        a = cubed.from_array(x, chunks=(10, 500), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        m = xp.mean(a.rechunk((500, 10)), axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        kinds = [type(l).__name__ for l in dry.launched]
+        assert kinds == ["DistPiecesLaunch"], kinds
+        dp = dry.launched[0]
+        assert dp.ngroups == 50 and dp.root is None
+        mine = len([c for c in range(50) if c % world == rank])  # source chunks held here
+        assert dp.fused.ntasks == mine * 50
+        total += dp.fused.ntasks
+    assert total == 50 * 50

@@ -102,6 +102,13 @@ def _cases(rank, world):
     y3 = cubed.from_array(Y, chunks=(3, 4), spec=spec)
     out["vort"] = xp.mean(a3[1:] * x3 + b3[1:] * y3).compute()
     note("vort")
+
+    # rechunk read through by a reduction: pieces run where their chunks live
+    z = np.random.default_rng(15).random((60, 50))
+    zc = cubed.from_array(z, chunks=(7, 50), spec=spec)
+    out["rechunk_mean"] = xp.mean(zc.rechunk((60, 9)), axis=0).compute()
+    out["rechunk_max"] = xp.max(zc.rechunk((60, 9)), axis=0).compute()
+    note("rechunk_mean")
     torch.cuda.synchronize()
     return out
 
@@ -147,3 +154,7 @@ def test_distributed_executor_matches_oracle(world):
     AA, BB = rng.random((30, 9, 8)), rng.random((30, 9, 8))
     X, Y = rng.random((9, 8)), rng.random((9, 8))
     assert np.isclose(got["vort"], np.mean(AA[1:] * X + BB[1:] * Y), rtol=1e-12, atol=0)
+
+    z = np.random.default_rng(15).random((60, 50))
+    assert np.allclose(got["rechunk_mean"], z.mean(axis=0), rtol=1e-12, atol=0)
+    assert np.array_equal(got["rechunk_max"], z.max(axis=0))
