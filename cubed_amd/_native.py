@@ -143,6 +143,9 @@ def lib():
     L.cubed_combine_groups.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                        c_void_p, c_int64, c_int64, c_void_p, c_void_p]
     L.cubed_combine_groups.restype = c_int
+    L.cubed_fold_groups.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                    c_void_p, c_int64, c_void_p, c_void_p]
+    L.cubed_fold_groups.restype = c_int
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]
     L.cubed_combine_partials.restype = c_int
@@ -166,7 +169,7 @@ EXPORTED_SYMBOLS = (
     "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
-    "cubed_fused_finish_groups", "cubed_combine_groups",
+    "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups",
 )
 
 

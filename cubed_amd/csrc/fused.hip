@@ -79,6 +79,13 @@ __global__ __launch_bounds__(kBlock) void k_combine_groups(
   combine_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, max_kept_out, out, kd0, kd1);
 }
 
+__global__ __launch_bounds__(kBlock) void k_fold_groups(
+    const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    Acc* __restrict__ out, int kd0, int kd1) {
+  fold_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_combine_parts(
     const cubed_program_t* __restrict__ Pd, const Acc* __restrict__ parts, int32_t nparts, int64_t n,
     Acc* __restrict__ out) {
@@ -123,8 +130,12 @@ static int64_t choose_split(int64_t base, int64_t max_split, int64_t resident) {
     if (eff >= 0.9) return s;
     if (eff > best_eff) { best_eff = eff; best = s; }
   }
-  if (best_eff == 0.0) {  // even max_split cannot fill the chip: use it
-    int64_t s = (resident + base - 1) / base;
+  if (best_eff == 0.0) {
+    // few, long tasks (e.g. one output block): as many splits as one round
+    // of resident workgroups holds -- rounding up would start a second round
+    // for a handful of workgroups and double the kernel's time
+    int64_t s = resident / base;
+    if (s < 1) s = 1;
     return s > max_split ? max_split : s;
   }
   return best;
@@ -325,6 +336,28 @@ extern "C" int cubed_combine_groups(const cubed_program_t* prog, const cubed_pro
   hipLaunchKernelGGL(k_combine_groups, grid_of((n + kBlock - 1) / kBlock), dim3(kBlock), 0, (hipStream_t)stream,
                      d_prog, d_tasks, ntasks, max_kept, (const Acc*)d_row_partials, d_group_start, ngroups,
                      max_kept_out, (Acc*)d_group_partials, kd0, kd1);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+extern "C" int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                                 const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                                 const void* d_row_partials, const int64_t* d_group_start,
+                                 int64_t ngroups, void* d_group_partials, void* stream) {
+  if (!prog || !d_prog || !d_row_partials || !d_group_start || !d_group_partials ||
+      (!d_tasks && ntasks > 0)) {
+    set_err("cubed_fold_groups: null argument");
+    return CUBED_E_ARG;
+  }
+  if (ngroups == 0) return 0;
+  if (int rc = check_program(*prog)) return rc;
+  if (prog->nfields == 0 || max_kept <= 0 || ngroups > ntasks) { set_err("cubed_fold_groups: bad shape"); return CUBED_E_ARG; }
+  int kd0, kd1;
+  kept_dims(*prog, kd0, kd1);
+  hipLaunchKernelGGL(k_fold_groups, grid_of(ngroups), dim3(kBlock), 0, (hipStream_t)stream, d_prog, d_tasks,
+                     ntasks, max_kept, (const Acc*)d_row_partials, d_group_start, ngroups,
+                     (Acc*)d_group_partials, kd0, kd1);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   return 0;

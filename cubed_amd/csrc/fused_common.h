@@ -87,6 +87,14 @@ CUBED_DEV void finish(const cubed_program_t& P, const cubed_task_t* T,
   }
 }
 
+// Rows in flight per lane in the streaming kernel: about 128 B of loads per
+// lane whatever the leaf count (a 1-leaf mean needs twice the rows of a
+// 2-leaf quad-means product to keep the same bytes in flight).
+__host__ __device__ constexpr int stream_unroll(int itemsize, int nleaves) {
+  return itemsize == 4 ? (nleaves <= 1 ? 8 : nleaves == 2 ? 4 : 2)
+                       : (nleaves <= 1 ? 4 : 2);
+}
+
 #ifndef __HIPCC_RTC__
 // ---------------------------------------------------------------- launch plan
 struct LaunchPlan {

@@ -468,6 +468,53 @@ CUBED_DEV void combine_groups_body(
   }
 }
 
+// Full reductions run "lifted": the innermost reduced dims are walked as if
+// kept (kernel A / streaming, one lane per element, rows in flight), leaving
+// per-element partials; this fold then reduces each group's rows AND kept
+// elements to one accumulator per field: one workgroup per group, a strided
+// pass per thread, then the 64-wide shuffle tree and LDS across the waves.
+CUBED_DEV void fold_groups_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    Acc* __restrict__ out, int kd0, int kd1) {
+  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  if (g >= ngroups) return;
+  const int64_t n = ntasks * max_kept;
+  Acc a[CUBED_MAX_FIELDS];
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
+  for (int64_t t = gs[g]; t < gs[g + 1]; ++t) {
+    const cubed_task_t* __restrict__ T = tasks + t;
+    int64_t nk = 1;
+    for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+    for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
+#pragma unroll
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < P.nfields)
+          a[f] = acc_combine(a[f], soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) red[wave][f] = a[f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+      Acc x = red[0][f];
+      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
+      out[f * ngroups + g] = x;
+    }
+  }
+}
+
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in
 // part order: out[f][i] = part0 (+) part1 (+) ...  Used for the fields RCCL
 // cannot reduce with numpy's semantics (max/min with NaN, prod, any/all).
@@ -494,10 +541,34 @@ CUBED_DEV void ld4(double (&o)[4], const CUBED_G double* p) {
   const f64x2 b = __builtin_nontemporal_load((const CUBED_G f64x2*)(p + 2));
   o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
 }
+// Cached form for leaves re-read along the reduced dim (reduced stride 0:
+// a broadcast operand such as x in a[1:] * x): non-temporal loads would send
+// every re-read back to HBM.
+template <typename V>
+CUBED_DEV void ld4c(V (&o)[4], const CUBED_G V* p) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = p[j];
+}
+template <>
+CUBED_DEV void ld4c<float>(float (&o)[4], const CUBED_G float* p) {
+  const f32x4 v = *(const CUBED_G f32x4*)p;
+  o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+}
+template <>
+CUBED_DEV void ld4c<double>(double (&o)[4], const CUBED_G double* p) {
+  const f64x2 a = *(const CUBED_G f64x2*)p;
+  const f64x2 b = *(const CUBED_G f64x2*)(p + 2);
+  o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
 CUBED_DEV void ld4(int64_t (&o)[4], const CUBED_G int64_t* p) {
   const i64x2 a = __builtin_nontemporal_load((const CUBED_G i64x2*)p);
   const i64x2 b = __builtin_nontemporal_load((const CUBED_G i64x2*)(p + 2));
   o[0] = a.x; o[1] = a.y; o[2] = b.x; o[3] = b.y;
+}
+
+template <typename V>
+CUBED_DEV void ld4s(V (&o)[4], const CUBED_G V* p, bool streamed) {
+  if (streamed) ld4(o, p); else ld4c<V>(o, p);
 }
 
 template <int NL, typename V>
@@ -523,6 +594,46 @@ CUBED_DEV void accumulate_nocount(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& r
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
     }
+  }
+}
+
+// Rows [lo, hi) of one kept VEC group: U rows of loads in flight, then the
+// program and the accumulation; MIXED: some leaves are re-read (cached loads).
+template <typename V, int NL, int U, bool MIXED>
+CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
+                           const cubed_program_t& P, const CUBED_G V* (&p)[NL],
+                           const int64_t (&rs)[NL], int64_t lo, int64_t hi) {
+  int64_t r = lo;
+  for (; r + U <= hi; r += U) {
+    V buf[U][NL][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {
+        if (MIXED) ld4s<V>(buf[u][l], p[l] + u * rs[l], rs[l] != 0);
+        else ld4(buf[u][l], p[l] + u * rs[l]);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      set_leaves<NL, V>(regs, buf[u]);
+      CUBED_RUN_PROLOGUE(V, 4, regs);
+      accumulate_nocount<V>(acc, regs, P);
+    }
+#pragma unroll
+    for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
+  }
+  for (; r < hi; ++r) {
+    V buf[NL][4];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      if (MIXED) ld4s<V>(buf[l], p[l], rs[l] != 0);
+      else ld4(buf[l], p[l]);
+    }
+    set_leaves<NL, V>(regs, buf);
+    CUBED_RUN_PROLOGUE(V, 4, regs);
+    accumulate_nocount<V>(acc, regs, P);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) p[l] += rs[l];
   }
 }
 
@@ -555,6 +666,12 @@ CUBED_DEV void stream_body(
     rs[l] = nr ? T->leaf_stride[l][nr - 1] : 0;
     qs[l] = nr == 2 ? T->leaf_stride[l][0] : 0;
   }
+
+  // leaves re-read along the rows (stride 0) take cached loads; the common
+  // all-streamed case keeps the loop free of per-leaf branches
+  bool all_streamed = true;
+#pragma unroll
+  for (int l = 0; l < NL; ++l) all_streamed = all_streamed && rs[l] != 0;
 
   for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
     const int64_t k = item * 4;
@@ -591,32 +708,10 @@ CUBED_DEV void stream_body(
       const CUBED_G V* p[NL];
 #pragma unroll
       for (int l = 0; l < NL; ++l) p[l] = base[l] + k + q * qs[l] + lo * rs[l];
-      int64_t r = lo;
-      for (; r + U <= hi; r += U) {
-        V buf[U][NL][4];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int l = 0; l < NL; ++l) ld4(buf[u][l], p[l] + u * rs[l]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          set_leaves<NL, V>(regs, buf[u]);
-          CUBED_RUN_PROLOGUE(V, 4, regs);
-          accumulate_nocount<V>(acc, regs, P);
-        }
-#pragma unroll
-        for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
-      }
-      for (; r < hi; ++r) {
-        V buf[NL][4];
-#pragma unroll
-        for (int l = 0; l < NL; ++l) ld4(buf[l], p[l]);
-        set_leaves<NL, V>(regs, buf);
-        CUBED_RUN_PROLOGUE(V, 4, regs);
-        accumulate_nocount<V>(acc, regs, P);
-#pragma unroll
-        for (int l = 0; l < NL; ++l) p[l] += rs[l];
-      }
+      if (all_streamed)
+        stream_rows<V, NL, U, false>(acc, regs, P, p, rs, lo, hi);
+      else
+        stream_rows<V, NL, U, true>(acc, regs, P, p, rs, lo, hi);
     }
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f)

@@ -32,13 +32,13 @@ __global__ __launch_bounds__(kBlock) void k_stream(
 template <typename V>
 void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L, const cubed_task_t* d_tasks,
                    int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
-  constexpr int U = sizeof(V) == 4 ? 4 : 2;
+  constexpr int S = (int)sizeof(V);
   const dim3 grid = grid_of(L.blocks);
   switch (P.nleaves) {
-    case 1: hipLaunchKernelGGL((k_stream<V, 1, U>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 2: hipLaunchKernelGGL((k_stream<V, 2, U>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 3: hipLaunchKernelGGL((k_stream<V, 3, U>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    default: hipLaunchKernelGGL((k_stream<V, 4, U>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 1: hipLaunchKernelGGL((k_stream<V, 1, stream_unroll(S, 1)>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 2: hipLaunchKernelGGL((k_stream<V, 2, stream_unroll(S, 2)>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 3: hipLaunchKernelGGL((k_stream<V, 3, stream_unroll(S, 3)>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    default: hipLaunchKernelGGL((k_stream<V, 4, stream_unroll(S, 4)>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
   }
 }
 

@@ -23,6 +23,7 @@ other multi-chunk read -- a per-task gather into a contiguous scratch buffer.
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 import itertools
 import math
 from dataclasses import dataclass, field
@@ -622,17 +623,38 @@ class FusedLaunch:
 
     groups = None
 
-    def set_groups(self, group_start):
+    fold = None
+
+    def set_groups(self, group_start, fold=None):
         """Rows are pieces; group_start (ngroups + 1) delimits the pieces of
-        each output box (partials mode: run() adds the grouped finish)."""
+        each output box (partials mode: run() adds the grouped finish).
+        ``fold = (epilogue program, one task row per group)``: a lifted full
+        reduction -- rows and kept elements fold to one value per group
+        (cubed_fold_groups), then the epilogue runs per group."""
         import torch
 
         self.ngroups = len(group_start) - 1
         self.groups = torch.from_numpy(np.ascontiguousarray(group_start)).to(self.d_prog.device)
+        if fold is not None:
+            prog_fin, table = fold
+            raw = np.frombuffer(ctypes.string_at(ctypes.addressof(prog_fin), ctypes.sizeof(prog_fin)),
+                                dtype=np.uint8)
+            self.fold = (prog_fin, torch.from_numpy(raw.copy()).to(self.d_prog.device), table,
+                         torch.empty(max(8 * self.prog.nfields * self.ngroups, 16), dtype=torch.uint8,
+                                     device=self.d_prog.device))
 
     def run(self, stream):
         self._run(stream)
-        if self.groups is not None:
+        if self.fold is not None:
+            prog_fin, d_fin, table, gsoa = self.fold
+            L = nat.lib()
+            nat.check(L.cubed_fold_groups(self.prog, self.d_prog.data_ptr(), self.table.data_ptr(),
+                                          self.ntasks, self.max_kept, self.ws.data_ptr(),
+                                          self.groups.data_ptr(), self.ngroups, gsoa.data_ptr(), stream),
+                      "cubed_fold_groups")
+            nat.check(L.cubed_fused_finish(prog_fin, d_fin.data_ptr(), table.data_ptr(), self.ngroups, 1,
+                                           gsoa.data_ptr(), stream), "cubed_fused_finish")
+        elif self.groups is not None:
             nat.check(nat.lib().cubed_fused_finish_groups(
                 self.prog, self.d_prog.data_ptr(), self.table.data_ptr(), self.ntasks, self.max_kept,
                 self.ws.data_ptr(), self.groups.data_ptr(), self.ngroups, stream),
@@ -686,7 +708,7 @@ class Lowerer:
         return self.ctx.device_source(proxy.array)
 
     def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
-                            rows_fn=None, sample_key=None, partials=False):
+                            rows_fn=None, sample_key=None, partials=False, lift=True):
         """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
         ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
         per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
@@ -847,11 +869,24 @@ class Lowerer:
                 starts = [i for i in range(len(group_keys))
                           if i == 0 or group_keys[i] != group_keys[i - 1]]
                 group_start = np.array(starts + [len(group_keys)], dtype=np.int64)
-        layout = canonicalize(rows, n, red_axes, leaves, kinds)
+        # full reductions with long inner rows run "lifted": the inner dims
+        # are walked as kept dims (every lane streams), then folded per task
+        lifted = set()
+        if lift and LIFT_ENABLED and program.reduce is not None and n >= 2 and set(range(n)) <= set(red_axes):
+            lifted = _lift_dims(rows, n)
+        if lifted:
+            partials = True
+            # the main kernel writes no output (the fold + epilogue do), so
+            # output strides must not stop the inner dims from coalescing
+            rows = [dataclasses.replace(r, ostrides=[[0] * len(st) for st in r.ostrides]) for r in rows]
+            if group_start is None:
+                group_start = np.arange(len(rows) + 1, dtype=np.int64)
+        layout = canonicalize(rows, n, set(red_axes) - lifted, leaves, kinds,
+                              check_outputs=not lifted)
         P.ndim = layout.ndim
         P.nred = layout.nred
         P.mode = layout.mode
-        if _stream_ok(layout, leaves, kinds, P.vtype):
+        if _stream_ok(layout, leaves, kinds, P.vtype, check_outputs=not lifted):
             P.mode |= MODE_STREAM
         if partials:
             if P.nfields == 0:
@@ -862,7 +897,15 @@ class Lowerer:
         launch = FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
                              gathers, self.ctx.device)
         launch.layout = layout
-        if group_start is not None:
+        if lifted:
+            # the epilogue program: same instructions, every dim reduced (one output per task)
+            fin = nat.Program()
+            ctypes.memmove(ctypes.addressof(fin), ctypes.addressof(P), ctypes.sizeof(P))
+            fin.nred = fin.ndim
+            fin.mode = 0
+            gt = dataclasses.replace(layout, rows=[layout.rows[i] for i in group_start[:-1]])
+            launch.set_groups(group_start, fold=(fin, gt.table(self.ctx.device)))
+        elif group_start is not None:
             launch.set_groups(group_start)
         return launch
 
@@ -1308,7 +1351,7 @@ def _apply_groups(r: TaskRow, groups):
     return ext, ls, os_
 
 
-def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout:
+def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds, check_outputs=True) -> Layout:
     if n == 0:
         groups = []
     else:
@@ -1364,7 +1407,7 @@ def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout
     # vectorisation (VEC=4) along the innermost kernel dim
     inner = groups[-1]
     mode = 1 if use_b else 0
-    if inner and _vec_ok(rows, inner, kinds, leaves, use_b):
+    if inner and _vec_ok(rows, inner, kinds, leaves, use_b or not check_outputs):
         mode |= 4
     rows2 = []
     for r in rows:
@@ -1382,12 +1425,36 @@ def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds) -> Layout
     return lay
 
 
+LIFT_MIN_ELEMS = 4096  # inner elements per task for a lifted full reduction
+LIFT_MIN_ROWS = 64     # outer (reduced) rows per kept element: partials stay small
+
+
+def _lift_dims(rows, n):
+    """Innermost dims a full reduction walks as kept dims: the shortest
+    innermost run with >= LIFT_MIN_ELEMS elements in the largest task, if the
+    remaining outer dims still give >= LIFT_MIN_ROWS rows on average (so the
+    per-element partials cost little next to the rows they summarise)."""
+    big = max(rows, key=lambda r: math.prod(r.extent))
+    inner, prod = [], 1
+    for d in range(n - 1, 0, -1):
+        inner.append(d)
+        prod *= big.extent[d]
+        if prod >= LIFT_MIN_ELEMS:
+            break
+    if prod < LIFT_MIN_ELEMS:
+        return set()
+    vol = sum(math.prod(r.extent) for r in rows)
+    kept = sum(math.prod(r.extent[d] for d in inner) for r in rows)
+    if not kept or vol / kept < LIFT_MIN_ROWS:
+        return set()
+    return set(inner)
+LIFT_ENABLED = __import__("os").environ.get("CUBED_AMD_LIFT", "1") != "0"
 MODE_STREAM = 8  # include/cubed_amd.h CUBED_MODE_STREAM
 MODE_PARTIALS = 16  # include/cubed_amd.h CUBED_MODE_PARTIALS
 _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64: np.dtype(np.int64)}
 
 
-def _stream_ok(layout: Layout, leaves, kinds, vtype) -> bool:
+def _stream_ok(layout: Layout, leaves, kinds, vtype, check_outputs=True) -> bool:
     """Geometry of the streaming fast path (stream.hip): kernel A with VEC=4,
     one kept kernel dim (packed in every leaf and output) after at most two
     reduced dims (chunk index x rows), every leaf an array chunk in the VM's
@@ -1407,7 +1474,7 @@ def _stream_ok(layout: Layout, leaves, kinds, vtype) -> bool:
                 if ext[d] != 1 and st[d] % 4:
                     return False
         for st in os_:
-            if st[-1] != 1:
+            if check_outputs and st[-1] != 1:
                 return False
     return True
 

@@ -418,7 +418,7 @@ class GpuDagExecutor(DagExecutor):
 
         try:
             launch = low.lower_expr_pipeline(program, cfg, target, keys, rows_fn=rows_fn,
-                                             sample_key=keys[0], partials=True)
+                                             sample_key=keys[0], partials=True, lift=False)
         except LoweringError:
             return None
         starts = meta["starts"]
@@ -640,7 +640,7 @@ class GpuDagExecutor(DagExecutor):
                 rows_fn=lambda leaves, kinds: chain_rows(
                     self.lowerer, chain, leaves, kinds, keys, select=select,
                     out_owned=lambda K: target.owner(K) == rank, discard=discard),
-                sample_key=contrib[keys[0]][0], partials=True)
+                sample_key=contrib[keys[0]][0], partials=True, lift=False)
         launches = [fetch] if fetch is not None else []
         launches += _with_gathers(launch, self.device)
         rops = [f.rop for f in chain.program.reduce.fields]

@@ -255,6 +255,15 @@ int cubed_combine_groups(const cubed_program_t* prog, const cubed_program_t* d_p
                          const void* d_row_partials, const int64_t* d_group_start,
                          int64_t ngroups, int64_t max_kept_out, void* d_group_partials,
                          void* stream);
+/* Fold each group's rows AND their kept elements into one accumulator per
+ * field: d_group_partials[f][g].  For full reductions run "lifted" (the
+ * innermost reduced dims walked as kept dims so every lane streams, e.g.
+ * mean(a[1:] * x + b[1:] * y) of the vorticity example); the epilogue then
+ * runs through cubed_fused_finish with the program's nred = ndim. */
+int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
+                      const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
+                      const void* d_row_partials, const int64_t* d_group_start,
+                      int64_t ngroups, void* d_group_partials, void* stream);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);

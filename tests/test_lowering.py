@@ -222,3 +222,18 @@ def test_requested_rechunk_is_kept(built, dry):
     z = y * 2
     arrays_to_plan(y, z).execute(executor=dry, resume=True, array_names=[y.name, z.name])
     assert [l for l in dry.launched if isinstance(l, CopyLaunch)]
+
+
+def test_full_reduction_is_lifted_to_the_stream_kernel(built, dry):
+    """mean over all axes: the inner dims are walked as kept dims by the
+    streaming kernel (partials), then folded per task + epilogue."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(2)
+    a = crandom.random((400, 64, 64), chunks=(100, 64, 64), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    m = xp.mean(a * 2)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    first = _fused(dry)[0]
+    assert first.fold is not None and first.prog.mode & MODE_STREAM
+    assert first.max_kept == 64 * 64 and first.max_red == 4 * 100  # inner dims lifted; chunks x rows reduced
