@@ -752,7 +752,57 @@ def squeeze(x, /, axis):
 
 
 def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
-    raise NotImplementedError("argmax/argmin are not lowered to MI355X kernels yet (SURVEY §8f)")
+    """argmax / argmin along one axis (core/ops.py:1093-1153).
+
+    The reference maps every block to a structured {i, v} pair with
+    take_along_axis and reduces the pairs.  The VM's accumulators are one
+    8-byte value per field, so the same result is produced as two fused
+    reductions over x: the max (min) along the axis, then the smallest index
+    whose element equals it -- where(x == m, index, INT64_MAX) reduced with
+    min.  NaN follows numpy: a NaN anywhere makes m NaN and the first NaN's
+    index is returned (isnan(x) & isnan(m) counts as equal).  Ties give the
+    first index, as numpy's argmax/argmin."""
+    from ..array_api import creation_functions as cf
+    from ..array_api import elementwise_functions as ef
+    from ..array_api import manipulation_functions as mf
+    from ..array_api import searching_functions as sf
+    from ..array_api import statistical_functions as stf
+
+    def index_along(d):
+        """The index along dim d, broadcastable against x."""
+        idx = cf.arange(x.shape[d], dtype=np.int64, chunks=(x.chunks[d],), spec=x.spec)
+        for e in range(x.ndim):
+            if e != d:
+                idx = mf.expand_dims(idx, axis=e)
+        return idx
+
+    reduce_max = stf.max if arg_func == "argmax" else stf.min
+    if axis is None and x.ndim > 1:
+        # the reference flattens with reshape (argmax(x) on an n-d array);
+        # here the flat C-order index is built from the per-dim indexes
+        m = reduce_max(x, keepdims=True)
+        flat = None
+        for d in range(x.ndim):
+            stride = int(np.prod(x.shape[d + 1:], dtype=np.int64))
+            term = ef.multiply(index_along(d), cf.asarray(np.int64(stride), spec=x.spec))
+            flat = term if flat is None else ef.add(flat, term)
+        target_axis, idx = None, flat
+    else:
+        if axis is None:
+            axis = 0
+        axis = validate_axis(axis, x.ndim)
+        if isinstance(axis, tuple):
+            if len(axis) != 1:
+                raise ValueError("argmax/argmin take a single axis")
+            axis = axis[0]
+        m = reduce_max(x, axis=axis, keepdims=True)
+        target_axis, idx = axis, index_along(axis)
+    eq = ef.equal(x, m)
+    if x.dtype.kind == "f":
+        eq = ef.logical_or(eq, ef.logical_and(ef.isnan(x), ef.isnan(m)))
+    big = cf.asarray(np.int64(np.iinfo(np.int64).max), spec=x.spec)
+    cand = sf.where(eq, idx, big)
+    return stf.min(cand, axis=target_axis, keepdims=keepdims)
 
 
 def unify_chunks(*args: "Array", **kwargs):

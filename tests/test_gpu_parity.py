@@ -385,6 +385,34 @@ def test_rechunk_read_through(ex, mem, op):
         assert np.array_equal(got_b, x) and np.array_equal(got_c, x * 2)
 
 
+ARG_A = [[11, 12, 13], [11, 11, 14], [10, 13, 11]]
+
+
+@pytest.mark.parametrize("fn, axis", [("argmax", None), ("argmax", 0), ("argmin", 0),
+                                      ("argmax", 1), ("argmin", None)])
+def test_arg_reductions_reference_cases(ex, fn, axis):
+    """test_array_api.py:524-548: argmax/argmin of a 3x3 int array in 2x2 chunks."""
+    spec = mkspec(ex)
+    a = xp.asarray(ARG_A, chunks=(2, 2), spec=spec)
+    got = getattr(xp, fn)(a, axis=axis).compute()
+    exp = getattr(np.array(ARG_A), fn)(axis=axis)
+    assert np.array_equal(got, exp) and np.asarray(got).dtype == np.int64
+
+
+@pytest.mark.parametrize("fn", ["argmax", "argmin"])
+def test_arg_reductions_ties_and_nans(ex, fn):
+    """First index on ties; the first NaN wins (numpy's rule), across chunks."""
+    x = np.round(np.random.default_rng(16).random((41, 37)) * 4) / 4  # many ties
+    x[5, 3] = np.nan
+    x[20, 3] = np.nan
+    x[7, 30] = np.nan
+    spec = mkspec(ex)
+    a = cubed.from_array(x, chunks=(6, 8), spec=spec)
+    for axis in (0, 1, None):
+        got = getattr(xp, fn)(a, axis=axis).compute()
+        assert np.array_equal(got, getattr(x, fn)(axis=axis)), axis
+
+
 # ----------------------------------------------------------- callbacks / resume
 
 
