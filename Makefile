@@ -3,7 +3,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := cubed_amd/csrc
 SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm.hip
-OBJS := $(SRCS:.hip=.o)
+CPPSRCS := $(CSRC)/codec.cpp
+OBJS := $(SRCS:.hip=.o) $(CPPSRCS:.cpp=.o)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Wno-unused-result -Iinclude
 LIB := cubed_amd/libcubed_amd.so
@@ -13,8 +14,11 @@ all: $(LIB) oracle
 $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h $(CSRC)/kernels.h include/cubed_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(CSRC)/%.o: $(CSRC)/%.cpp include/cubed_amd.h
+	g++ -O3 -fPIC -std=c++17 -Iinclude -c $< -o $@
+
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -L/opt/rocm/lib -lhiprtc -lz -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 4  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 5  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -149,6 +149,15 @@ def lib():
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]
     L.cubed_combine_partials.restype = c_int
+    L.cubed_blosc_header.argtypes = [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64),
+                                     POINTER(c_int), POINTER(c_int)]
+    L.cubed_blosc_header.restype = c_int
+    L.cubed_blosc_decompress.argtypes = [c_void_p, c_int64, c_void_p, c_int64]
+    L.cubed_blosc_decompress.restype = c_int
+    L.cubed_blosc_max_compressed.argtypes = [c_int64]
+    L.cubed_blosc_max_compressed.restype = c_int64
+    L.cubed_blosc_compress.argtypes = [c_void_p, c_int64, c_int, c_int, c_void_p, c_int64]
+    L.cubed_blosc_compress.restype = c_int64
     L.cubed_abi_version.restype = c_int
     L.cubed_last_error.restype = c_char_p
     L.cubed_device_count.restype = c_int
@@ -170,6 +179,8 @@ EXPORTED_SYMBOLS = (
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups",
+    "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
+    "cubed_blosc_compress",
 )
 
 

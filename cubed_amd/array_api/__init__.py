@@ -13,6 +13,7 @@ from .creation_functions import (
     full,
     full_like,
     linspace,
+    meshgrid,
     ones,
     ones_like,
     tril,
@@ -39,13 +40,18 @@ from .dtypes import (
 from .elementwise_functions import *  # noqa: F401,F403
 from .elementwise_functions import abs, round  # noqa: F401
 from .linear_algebra_functions import matmul, matrix_transpose, outer, tensordot, vecdot
+from .indexing_functions import take
 from .manipulation_functions import (
     broadcast_arrays,
     broadcast_to,
+    concat,
     expand_dims,
+    flatten,
     moveaxis,
     permute_dims,
+    reshape,
     squeeze,
+    stack,
 )
 from .searching_functions import argmax, argmin, where
 from .statistical_functions import max, mean, min, prod, sum

@@ -224,3 +224,26 @@ def _like_args(x, dtype=None, device=None, chunks=None, spec=None):
     if spec is None:
         spec = x.spec
     return dict(shape=x.shape, dtype=dtype, device=device, chunks=chunks, spec=spec)
+
+
+def meshgrid(*arrays, indexing="xy"):
+    """array_api/creation_functions.py:228-256: each 1-d input indexed with
+    new axes, then broadcast together (views of index/broadcast programs)."""
+    from .manipulation_functions import broadcast_arrays
+
+    if len({a.dtype for a in arrays}) > 1:
+        raise ValueError("meshgrid inputs must all have the same dtype")
+    if indexing not in ("ij", "xy"):
+        raise ValueError("`indexing` must be `'ij'` or `'xy'`")
+    arrs = list(arrays)
+    if indexing == "xy" and len(arrs) > 1:
+        arrs[0], arrs[1] = arrs[1], arrs[0]
+    grid = []
+    for i in range(len(arrs)):
+        s = [None] * len(arrs)
+        s[i] = slice(None)
+        grid.append(arrs[i][tuple(s)])
+    grid = list(broadcast_arrays(*grid))
+    if indexing == "xy" and len(arrs) > 1:
+        grid[0], grid[1] = grid[1], grid[0]
+    return grid

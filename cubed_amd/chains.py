@@ -432,9 +432,17 @@ def _arg_arrays(spec, target):
     function does not name one array per argument)."""
     nb = getattr(target, "numblocks", ())
     try:
-        args = spec.block_function(("out",) + (0,) * len(nb))
+        first = _arg_arrays_at(spec, (0,) * len(nb))
+        # key functions that switch arrays per task (stack) are left unfused
+        if first is None or first != _arg_arrays_at(spec, tuple(n - 1 for n in nb)):
+            return None
     except Exception:  # noqa: BLE001 -- an unusual key function: leave it unfused
         return None
+    return first
+
+
+def _arg_arrays_at(spec, coords):
+    args = spec.block_function(("out",) + tuple(coords))
     names = []
     for a in args:
         while isinstance(a, list):

@@ -499,14 +499,51 @@ def map_direct(func, *args: "Array", shape, dtype, chunks, extra_projected_mem, 
         axes = tuple(range(src.ndim))
 
     def build(block_arg):
-        leaf = ir.Region(src.name, src.dtype, axes, region_fn, block_arg,
-                         target=src.zarray_maybe_lazy)
+        if isinstance(region_fn, ConcatRegions):
+            leaf = ir.Concat(src.name, np.dtype(dtype), tuple(range(ndim)), region_fn, block_arg,
+                             sources=tuple(a.zarray_maybe_lazy for a in args), axis=region_fn.axis)
+        else:
+            leaf = ir.Region(src.name, src.dtype, axes, region_fn, block_arg,
+                             target=src.zarray_maybe_lazy)
         return ir.ExprProgram(ndim=ndim, nargs=block_arg + 1, outputs=leaf,
                               out_axes=tuple(range(ndim)), name="map_direct")
 
     return map_blocks(_BlockIdProgram(build, 1), out, dtype=dtype, chunks=chunks,
                       extra_source_arrays=args, extra_projected_mem=extra_projected_mem,
                       fusable=False, **kwargs)
+
+
+class ConcatRegions:
+    """Regions read by output block ``block_id`` of ``concat(arrays, axis)``
+    (_read_concat_chunk / _array_slices, array_api/manipulation_functions.py
+    :107-132): a list of (array index, region of that array, offset along
+    ``axis`` inside the output block).  The block spans
+    [block_id[axis] * chunk, + its extent) of the concatenated axis."""
+
+    def __init__(self, out_chunks, axis, offsets):
+        self.out_chunks = out_chunks
+        self.axis = axis
+        self.offsets = offsets
+
+    def __call__(self, block_id):
+        from bisect import bisect
+
+        starts = [tuple(np.cumsum((0,) + c[:-1])) for c in self.out_chunks]
+        base = [slice(int(starts[d][b]), int(starts[d][b]) + self.out_chunks[d][b])
+                for d, b in enumerate(block_id)]
+        ax = self.axis
+        lo, hi = base[ax].start, base[ax].stop
+        parts = []
+        pos = lo
+        while pos < hi:
+            i = bisect(self.offsets, pos) - 1
+            stop = min(hi, self.offsets[i + 1])
+            if stop > pos:
+                region = list(base)
+                region[ax] = slice(pos - self.offsets[i], stop - self.offsets[i], 1)
+                parts.append((i, tuple(region), pos - lo))
+            pos = stop
+        return parts
 
 
 # ------------------------------------------------------------------ rechunk / merge

@@ -1,0 +1,312 @@
+// Host-side Zarr v2 chunk codecs for the source/sink I/O path (SURVEY.md
+// §8f rank 1; reference: cubed/storage/zarr.py:8-103 creates Zarr v2 arrays
+// with zarr's default compressor, numcodecs Blosc(cname="lz4", clevel=5,
+// shuffle=SHUFFLE)).  zarr/numcodecs are not part of this image, so the
+// container format is restated here from the published Blosc 1.x frame
+// layout and the LZ4 block format:
+//
+//   Blosc frame: 16-byte header
+//     [0] format version (2)  [1] codec format version  [2] flags
+//     [3] typesize  [4..7] nbytes  [8..11] blocksize  [12..15] cbytes
+//   flags: 0x01 byte shuffle, 0x02 memcpyed (raw payload follows the header),
+//          0x04 bit shuffle, 0x10 blocks not split into typesize streams,
+//          bits 5-7 codec (0 blosclz, 1 lz4/lz4hc, 2 snappy, 3 zlib, 4 zstd)
+//   then one int32 start offset per block; each block holds nsplits streams
+//   of [int32 csize][csize bytes]; csize == stream size means stored raw.
+//   A block is split into typesize streams unless flagged 0x10, it is the
+//   leftover (last, short) block, typesize > 16 or blocksize/typesize < 128.
+//   Byte shuffle transposes each block as a (blocksize/typesize, typesize)
+//   byte matrix; the trailing blocksize % typesize bytes stay in place.
+//
+// Decoding supports lz4 and zlib streams with byte or no shuffle (what
+// zarr's defaults and the zlib codec write); the encoder writes lz4 with
+// byte shuffle and unsplit blocks (flag 0x10), which every Blosc >= 1.x
+// decoder reads.  Plain C ABI (include/cubed_amd.h); no GPU code.
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include <zlib.h>
+
+#include "cubed_amd.h"
+
+namespace {
+
+constexpr int kHeader = 16;
+constexpr int kMaxSplits = 16;
+constexpr int kMinBuffer = 128;
+
+inline uint32_t rd32(const uint8_t* p) {
+    return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+inline void wr32(uint8_t* p, uint32_t v) {
+    p[0] = uint8_t(v);
+    p[1] = uint8_t(v >> 8);
+    p[2] = uint8_t(v >> 16);
+    p[3] = uint8_t(v >> 24);
+}
+
+// ---------------------------------------------------------------- shuffle
+
+void byte_shuffle(const uint8_t* in, uint8_t* out, int64_t n, int ts) {
+    const int64_t rows = n / ts;
+    for (int64_t j = 0; j < rows; ++j)
+        for (int i = 0; i < ts; ++i) out[int64_t(i) * rows + j] = in[j * ts + i];
+    std::memcpy(out + rows * ts, in + rows * ts, size_t(n - rows * ts));
+}
+
+void byte_unshuffle(const uint8_t* in, uint8_t* out, int64_t n, int ts) {
+    const int64_t rows = n / ts;
+    if (ts == 4) {
+        const uint8_t *a = in, *b = in + rows, *c = in + 2 * rows, *d = in + 3 * rows;
+        for (int64_t j = 0; j < rows; ++j) {
+            out[4 * j] = a[j];
+            out[4 * j + 1] = b[j];
+            out[4 * j + 2] = c[j];
+            out[4 * j + 3] = d[j];
+        }
+    } else {
+        for (int i = 0; i < ts; ++i) {
+            const uint8_t* s = in + int64_t(i) * rows;
+            for (int64_t j = 0; j < rows; ++j) out[j * ts + i] = s[j];
+        }
+    }
+    std::memcpy(out + rows * ts, in + rows * ts, size_t(n - rows * ts));
+}
+
+// ---------------------------------------------------------------- LZ4 block
+
+// Decode one LZ4 block into exactly ``cap`` bytes; returns bytes written or -1.
+int64_t lz4_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+    int64_t ip = 0, op = 0;
+    while (ip < n) {
+        const int token = src[ip++];
+        int64_t lit = token >> 4;
+        if (lit == 15) {
+            int b;
+            do {
+                if (ip >= n) return -1;
+                b = src[ip++];
+                lit += b;
+            } while (b == 255);
+        }
+        if (ip + lit > n || op + lit > cap) return -1;
+        std::memcpy(dst + op, src + ip, size_t(lit));
+        ip += lit;
+        op += lit;
+        if (ip >= n) break;  // the last sequence carries literals only
+        if (ip + 2 > n) return -1;
+        const int64_t off = int64_t(src[ip]) | int64_t(src[ip + 1]) << 8;
+        ip += 2;
+        if (off == 0 || off > op) return -1;
+        int64_t len = token & 15;
+        if (len == 15) {
+            int b;
+            do {
+                if (ip >= n) return -1;
+                b = src[ip++];
+                len += b;
+            } while (b == 255);
+        }
+        len += 4;
+        if (op + len > cap) return -1;
+        const uint8_t* m = dst + op - off;
+        if (off >= len) {
+            std::memcpy(dst + op, m, size_t(len));
+        } else {
+            for (int64_t k = 0; k < len; ++k) dst[op + k] = m[k];  // overlapping copy
+        }
+        op += len;
+    }
+    return op;
+}
+
+void put_len(std::vector<uint8_t>& o, int64_t v) {
+    while (v >= 255) {
+        o.push_back(255);
+        v -= 255;
+    }
+    o.push_back(uint8_t(v));
+}
+
+void put_seq(std::vector<uint8_t>& o, const uint8_t* lit, int64_t nlit, int64_t off, int64_t mlen) {
+    const int64_t ml = mlen - 4;
+    const uint8_t tok = uint8_t((nlit >= 15 ? 15 : nlit) << 4 | (mlen ? (ml >= 15 ? 15 : ml) : 0));
+    o.push_back(tok);
+    if (nlit >= 15) put_len(o, nlit - 15);
+    o.insert(o.end(), lit, lit + nlit);
+    if (!mlen) return;
+    o.push_back(uint8_t(off));
+    o.push_back(uint8_t(off >> 8));
+    if (ml >= 15) put_len(o, ml - 15);
+}
+
+// Greedy single-probe LZ4 block encoder (format-conformant: the last 5 bytes
+// are literals and no match starts within the last 12 bytes).
+void lz4_encode(const uint8_t* src, int64_t n, std::vector<uint8_t>& out) {
+    constexpr int kHashLog = 16;
+    constexpr int64_t kMfLimit = 12, kLastLiterals = 5;
+    out.clear();
+    if (n < kMfLimit + 1) {
+        put_seq(out, src, n, 0, 0);
+        return;
+    }
+    std::vector<int64_t> table(size_t(1) << kHashLog, -1);
+    auto hash = [](uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); };
+    const int64_t limit = n - kMfLimit, match_end = n - kLastLiterals;
+    int64_t ip = 0, anchor = 0;
+    uint32_t miss = 0;
+    while (ip < limit) {
+        uint32_t seq;
+        std::memcpy(&seq, src + ip, 4);
+        const uint32_t h = hash(seq);
+        const int64_t ref = table[h];
+        table[h] = ip;
+        uint32_t rseq = 0;
+        if (ref >= 0) std::memcpy(&rseq, src + ref, 4);
+        if (ref < 0 || ip - ref > 65535 || rseq != seq) {
+            ip += 1 + (miss++ >> 6);  // skip faster through incompressible data
+            continue;
+        }
+        miss = 0;
+        int64_t len = 4;
+        while (ip + len < match_end && src[ref + len] == src[ip + len]) ++len;
+        put_seq(out, src + anchor, ip - anchor, ip - ref, len);
+        ip += len;
+        anchor = ip;
+    }
+    put_seq(out, src + anchor, n - anchor, 0, 0);
+}
+
+// ---------------------------------------------------------------- Blosc frame
+
+int decode_stream(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, int64_t size) {
+    if (csize == size) {
+        std::memcpy(dst, src, size_t(size));
+        return 0;
+    }
+    if (codec == 1) return lz4_decode(src, csize, dst, size) == size ? 0 : CUBED_E_CODEC;
+    if (codec == 3) {
+        uLongf got = uLongf(size);
+        if (uncompress(dst, &got, src, uLong(csize)) != Z_OK || int64_t(got) != size) return CUBED_E_CODEC;
+        return 0;
+    }
+    return CUBED_E_UNSUPPORTED;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cubed_blosc_header(const void* src, int64_t srclen, int64_t* nbytes, int64_t* cbytes, int* typesize,
+                       int* flags) {
+    if (!src || srclen < kHeader) return CUBED_E_ARG;
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    if (s[0] == 0 || s[0] > 4) return CUBED_E_CODEC;
+    if (nbytes) *nbytes = rd32(s + 4);
+    if (cbytes) *cbytes = rd32(s + 12);
+    if (typesize) *typesize = s[3];
+    if (flags) *flags = s[2];
+    return 0;
+}
+
+int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen) {
+    if (!src || !dst || srclen < kHeader) return CUBED_E_ARG;
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    const int flags = s[2], ts = s[3] ? s[3] : 1;
+    const int64_t nbytes = rd32(s + 4), blocksize = rd32(s + 8), cbytes = rd32(s + 12);
+    if (nbytes != dstlen || cbytes > srclen) return CUBED_E_ARG;
+    if (flags & 0x04) return CUBED_E_UNSUPPORTED;  // bit shuffle
+    if (flags & 0x02) {
+        if (kHeader + nbytes > srclen) return CUBED_E_CODEC;
+        std::memcpy(d, s + kHeader, size_t(nbytes));
+        return 0;
+    }
+    if (nbytes == 0) return 0;
+    if (blocksize <= 0) return CUBED_E_CODEC;
+    const int codec = flags >> 5;
+    const bool shuffled = (flags & 0x01) && ts > 1;
+    const int64_t nblocks = (nbytes + blocksize - 1) / blocksize;
+    if (kHeader + 4 * nblocks > srclen) return CUBED_E_CODEC;
+    std::vector<uint8_t> tmp(shuffled ? size_t(blocksize) : 0);
+    for (int64_t b = 0; b < nblocks; ++b) {
+        const bool leftover = (b == nblocks - 1) && (nbytes % blocksize);
+        const int64_t bsize = leftover ? nbytes % blocksize : blocksize;
+        const bool split = !(flags & 0x10) && !leftover && ts <= kMaxSplits && blocksize / ts >= kMinBuffer;
+        const int nsplits = split ? ts : 1;
+        const int64_t neblock = bsize / nsplits;
+        int64_t pos = rd32(s + kHeader + 4 * b);
+        uint8_t* out = shuffled ? tmp.data() : d + b * blocksize;
+        for (int j = 0; j < nsplits; ++j) {
+            if (pos + 4 > srclen) return CUBED_E_CODEC;
+            const int64_t csize = rd32(s + pos);
+            pos += 4;
+            if (pos + csize > srclen) return CUBED_E_CODEC;
+            const int rc = decode_stream(codec, s + pos, csize, out + j * neblock, neblock);
+            if (rc) return rc;
+            pos += csize;
+        }
+        if (shuffled) byte_unshuffle(tmp.data(), d + b * blocksize, bsize, ts);
+    }
+    return 0;
+}
+
+int64_t cubed_blosc_max_compressed(int64_t nbytes) { return nbytes + kHeader + 64; }
+
+int64_t cubed_blosc_compress(const void* src, int64_t nbytes, int typesize, int shuffle, void* dst,
+                             int64_t dstcap) {
+    if (!src || !dst || nbytes < 0 || nbytes > INT32_MAX - 1024 || typesize < 1 || typesize > 255)
+        return CUBED_E_ARG;
+    if (dstcap < cubed_blosc_max_compressed(nbytes)) return CUBED_E_ARG;
+    const uint8_t* in = static_cast<const uint8_t*>(src);
+    uint8_t* o = static_cast<uint8_t*>(dst);
+    // blocks of 256 KiB (a multiple of typesize), like Blosc's clevel-5 sizes
+    int64_t blocksize = (int64_t(1) << 18) / typesize * typesize;
+    if (blocksize <= 0) blocksize = typesize;
+    if (blocksize > nbytes) blocksize = nbytes;
+    const int64_t nblocks = blocksize ? (nbytes + blocksize - 1) / blocksize : 0;
+    const bool shuffled = shuffle && typesize > 1;
+    uint8_t flags = uint8_t(0x10 | (1 << 5) | (shuffled ? 0x01 : 0));
+    auto header = [&](uint8_t f, int64_t bs, int64_t cb) {
+        o[0] = 2;
+        o[1] = 1;
+        o[2] = f;
+        o[3] = uint8_t(typesize);
+        wr32(o + 4, uint32_t(nbytes));
+        wr32(o + 8, uint32_t(bs));
+        wr32(o + 12, uint32_t(cb));
+    };
+    int64_t pos = kHeader + 4 * nblocks;
+    bool raw = nbytes < kMinBuffer;
+    std::vector<uint8_t> sh(shuffled ? size_t(blocksize) : 0), enc;
+    for (int64_t b = 0; b < nblocks && !raw; ++b) {
+        const int64_t bsize = (b == nblocks - 1 && nbytes % blocksize) ? nbytes % blocksize : blocksize;
+        const uint8_t* blk = in + b * blocksize;
+        if (shuffled) {
+            byte_shuffle(blk, sh.data(), bsize, typesize);
+            blk = sh.data();
+        }
+        lz4_encode(blk, bsize, enc);
+        const bool store = int64_t(enc.size()) >= bsize;
+        const int64_t csize = store ? bsize : int64_t(enc.size());
+        if (pos + 4 + csize > nbytes + kHeader) {
+            raw = true;
+            break;
+        }
+        wr32(o + kHeader + 4 * b, uint32_t(pos));
+        wr32(o + pos, uint32_t(csize));
+        std::memcpy(o + pos + 4, store ? blk : enc.data(), size_t(csize));
+        pos += 4 + csize;
+    }
+    if (raw) {  // incompressible: header + the bytes as they are
+        header(uint8_t(flags | 0x02), blocksize, kHeader + nbytes);
+        std::memcpy(o + kHeader, in, size_t(nbytes));
+        return kHeader + nbytes;
+    }
+    header(flags, blocksize, pos);
+    return pos;
+}
+
+}  // extern "C"

@@ -125,6 +125,29 @@ class Region(Expr):
 
 
 @dataclass(frozen=True, eq=False)
+class ReshapeArg(Arg):
+    """Input chunk ``index`` read as a chunk of the reshaped array
+    (reshape_chunks' ``_reshape_chunk``, array_api/manipulation_functions.py
+    :249-275): C-order chunk bytes are unchanged, only the extents change.
+    The task's input block (``in_numblocks`` grid) maps to the output block
+    of the same linear offset in the ``out_chunks`` grid; ``axes`` index the
+    output chunk's dims."""
+    in_numblocks: Tuple[int, ...] = ()
+    out_chunks: Tuple[Tuple[int, ...], ...] = ()
+
+
+@dataclass(frozen=True, eq=False)
+class Concat(Region):
+    """concat's ``_read_concat_chunk`` (array_api/manipulation_functions.py
+    :107-121): the output block is assembled along ``axis`` from regions of
+    several side inputs.  ``region(block_id)`` returns a list of
+    (source index, region of that source, offset along ``axis`` inside the
+    output block); ``sources`` are the side inputs' targets."""
+    sources: Tuple[Any, ...] = ()
+    axis: int = 0
+
+
+@dataclass(frozen=True, eq=False)
 class Philox(Expr):
     """numpy ``Generator(Philox(key=root_seed + block_offset)).random()``
     stream over one block of the random array in C order
@@ -519,6 +542,8 @@ def fuse_programs(consumer: Program, producers: Sequence[Optional[Program]],
         # consumer space dim -> producer space dim, through the consumer's leaf
         # axes of arg pi and the producer's out_axes
         def sub(leaf):
+            if isinstance(leaf, ReshapeArg):
+                raise FusionError("reshape of a reduction result")
             if isinstance(leaf, Arg):
                 if leaf.index != pi:
                     raise FusionError("epilogue reads an array other than the reduction result")
@@ -561,6 +586,10 @@ def fuse_programs(consumer: Program, producers: Sequence[Optional[Program]],
             p = producers[leaf.index]
             if p is None:
                 return replace(leaf, index=offsets[leaf.index])
+            if isinstance(leaf, ReshapeArg):
+                # the producer's space is the input chunk's shape, not the
+                # reshaped one: keep its output materialised
+                raise FusionError("producer fused into a chunk reshape")
             outs = _output_map(p)
             src = outs.get(leaf.field) if leaf.field is not None else outs.get(None)
             if src is None and leaf.field is not None and isinstance(outs.get(None), (Arg, Region)) \

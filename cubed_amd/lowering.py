@@ -42,7 +42,7 @@ from .storage import (
     VirtualOffsetsArray,
     c_strides,
 )
-from .utils import block_id_to_offset, flatten_keys
+from .utils import block_id_to_offset, flatten_keys, offset_to_block_id
 
 
 class LoweringError(RuntimeError):
@@ -511,6 +511,10 @@ def collect_leaves(exprs) -> List[Any]:
 
 
 def _leaf_key(leaf):
+    if isinstance(leaf, ir.ReshapeArg):
+        return ("reshape", leaf.index, leaf.field, leaf.axes)
+    if isinstance(leaf, ir.Concat):
+        return ("concat", leaf.field, leaf.axes, id(leaf.region), leaf.block_arg)
     if isinstance(leaf, ir.Arg):
         return ("arg", leaf.index, leaf.field, leaf.axes)
     if isinstance(leaf, ir.Region):
@@ -723,7 +727,10 @@ class Lowerer:
         # pure copies go through the box-copy kernel
         if rows_fn is None and program.reduce is None and not program.structured and \
                 is_pure_copy(program, target.dtype):
-            return self.lower_copy_program(program, spec, target, task_keys)
+            try:
+                return self.lower_copy_program(program, spec, target, task_keys)
+            except _NotACopy:
+                pass  # a constant source: the fused path materialises it
 
         pre_exprs = [e for _, e in out_items] if program.reduce is None else [f.expr for f in rfields]
         leaves = collect_leaves(pre_exprs)
@@ -1021,6 +1028,8 @@ class Lowerer:
     def straddle_view(self, leaf, args):
         """(placeholder view, array, region, field) for a Region leaf whose
         unit-step slice region spans several chunks, else None."""
+        if isinstance(leaf, ir.Concat):
+            return None
         block_id = tuple(args[leaf.block_arg][1:])
         region = leaf.region(block_id)
         if any(isinstance(r, list) or (isinstance(r, slice) and (r.step or 1) != 1) for r in region):
@@ -1148,7 +1157,13 @@ class Lowerer:
         args = [list(a) if not isinstance(a, (tuple, list, str)) else a for a in args]
         out = []
         for l, leaf in enumerate(leaves):
-            if isinstance(leaf, ir.Region):
+            if isinstance(leaf, ir.Concat):
+                for ai, region, _ in leaf.region(tuple(args[leaf.block_arg][1:])):
+                    arr = self.ctx.device_source(leaf.sources[ai])
+                    if isinstance(arr, DeviceArray):
+                        for coords, _, _ in region_pieces(arr, region):
+                            out.append((arr, tuple(coords), leaf.field, l))
+            elif isinstance(leaf, ir.Region):
                 arr = self.ctx.device_source(leaf.target)
                 if not isinstance(arr, DeviceArray):
                     continue
@@ -1159,6 +1174,16 @@ class Lowerer:
 
     def leaf_view(self, leaf, args, spec, gathers, out_key):
         """(kind, view) for one leaf of one task."""
+        if isinstance(leaf, ir.ReshapeArg):
+            a = args[leaf.index]
+            arr = self.resolve_target(a[0], spec.reads_map)
+            v = chunk_view(arr, a[1:], leaf.field)
+            return LEAF_ARRAY, _reshaped_view(leaf, a[1:], v)
+        if isinstance(leaf, ir.Concat):
+            block_id = tuple(args[leaf.block_arg][1:])
+            srcs = [self.ctx.device_source(t) for t in leaf.sources]
+            return LEAF_ARRAY, self.ctx.gather_concat(srcs, leaf.region(block_id), leaf.axis,
+                                                      leaf.field, gathers)
         if isinstance(leaf, ir.Arg):
             a = args[leaf.index]
             if isinstance(a, tuple):
@@ -1216,7 +1241,26 @@ class Lowerer:
             key = tuple(key)
             args = spec.block_function(("out",) + key)
             dst = chunk_view(target, key) if target.ndim else ArrView(target.chunk_addr(()), [], [], target.dtype)
-            if isinstance(leaf, ir.Region):
+            if isinstance(leaf, ir.Concat):
+                block_id = tuple(args[leaf.block_arg][1:])
+                dstr = _dst_strides_for(leaf.axes, program.out_axes, dst)
+                isz = target.dtype.itemsize
+                for ai, region, off in leaf.region(block_id):
+                    src = self.ctx.device_source(leaf.sources[ai])
+                    if not isinstance(src, DeviceArray):
+                        raise _NotACopy()
+                    boxes += boxes_for_region(src, region, dst.base + off * dstr[leaf.axis] * isz,
+                                              dstr, leaf.field)
+            elif isinstance(leaf, ir.ReshapeArg):
+                a = args[leaf.index]
+                src = self.resolve_target(a[0], spec.reads_map)
+                if not isinstance(src, DeviceArray):
+                    raise _NotACopy()
+                sv = _reshaped_view(leaf, a[1:], chunk_view(src, a[1:], leaf.field))
+                n = math.prod(sv.extent)
+                if n:
+                    boxes.append(Box(sv.base, dst.base, [n], [1], [1]))
+            elif isinstance(leaf, ir.Region):
                 block_id = tuple(args[leaf.block_arg][1:])
                 region = leaf.region(block_id)
                 src = self.ctx.device_source(leaf.target)
@@ -1230,6 +1274,9 @@ class Lowerer:
                 keys = [a] if isinstance(a, tuple) else flatten_keys(a)
                 src = self.resolve_target(keys[0][0], spec.reads_map)
                 dstr = _dst_strides_for(leaf.axes, program.out_axes, dst)
+                n_src = sum(math.prod(src.chunk_extent(k[1:])) if src.ndim else 1 for k in keys)
+                if n_src != (math.prod(dst.extent) if target.ndim else 1):
+                    raise _NotACopy()  # a broadcast (broadcast_to, meshgrid): the fused path
                 for k in keys:
                     sv = chunk_view(src, k[1:], leaf.field) if src.ndim else \
                         ArrView(src.chunk_addr((), leaf.field), [], [], src.dtype)
@@ -1237,6 +1284,22 @@ class Lowerer:
                     boxes.append(Box(sv.base, dst.base + _merged_offset(src, keys, k, dstr) * target.dtype.itemsize,
                                      sv.extent, sv.stride, dstr[:len(sv.extent)]))
         return CopyLaunch(boxes, target.dtype.itemsize, self.ctx.device)
+
+
+class _NotACopy(Exception):
+    """A copy program whose source is not an HBM array (constant, offsets)."""
+
+
+def _reshaped_view(leaf, in_coords, v: ArrView) -> ArrView:
+    """The input chunk (compact C order in its slot) seen with the extents
+    of the reshaped output chunk of the same linear block offset
+    (reshape_chunks' block_function, manipulation_functions.py:258-265)."""
+    off = block_id_to_offset(tuple(in_coords), leaf.in_numblocks)
+    oc = offset_to_block_id(off, tuple(len(c) for c in leaf.out_chunks))
+    ext = [leaf.out_chunks[d][b] for d, b in enumerate(oc)]
+    if math.prod(ext) != math.prod(v.extent):
+        raise LoweringError(f"reshape of a {v.extent} chunk into {ext}")
+    return ArrView(v.base, ext, list(c_strides(ext)), v.dtype)
 
 
 def _out_dtype(target, name, structured):

@@ -208,6 +208,14 @@ def fuse(op1: PrimitiveOperation, op2: PrimitiveOperation) -> PrimitiveOperation
                                      nargs=p1.config.function_nargs)
     else:
         program = _fuse_program(p2.config.function, [p1.config.function], [p1.config.function_nargs])
+        if isinstance(program, ir.OpaqueProgram) and isinstance(p1.config.function, ir.ExprProgram) \
+                and isinstance(p2.config.function, ir.ExprProgram):
+            # not expressible as one program (e.g. a consumer of a chunk
+            # reshape): one task still runs both, through op1's chunk
+            program = ir.GemmThenProgram(gemm=p1.config.function, gemm_block_function=p1.config.block_function,
+                                         gemm_reads=p1.config.reads_map, gemm_target=op1.target_array,
+                                         then=p2.config.function, then_block_function=p2.config.block_function,
+                                         nargs=p1.config.function_nargs, name="seq")
     spec = BlockwiseSpec(fused_block_function, program, p1.config.function_nargs,
                          p1.config.reads_map, p2.config.write)
     pipeline = CubedPipeline(apply_blockwise, gensym("fused_apply_blockwise"), p2.mappable, spec)

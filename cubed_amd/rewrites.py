@@ -66,6 +66,8 @@ def elide_rechunks(dag, array_names):
                 continue
             if not isinstance(sample[i], tuple):
                 continue  # the consumer reads several chunks per task: keep the rechunk
+            if any(isinstance(l, ir.ReshapeArg) and l.index == i for l in ir.leaves_of_program(program)):
+                continue  # a chunk reshape needs the rechunked chunk's bytes in C order
             # walk back through the rechunk's copy op(s): y <- R [<- int <- R1] <- x
             removed, cur, x_name, x_target = [], yname, None, None
             while True:

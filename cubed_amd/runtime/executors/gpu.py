@@ -116,8 +116,13 @@ class _Upload:
         self.cfg = cfg
 
     def run(self, stream):
+        from ...zarr_io import ZarrV2Array, upload_zarr
+
         self.ctx.allocate(self.cfg.target)
-        self.cfg.target.from_numpy(np.asarray(self.cfg.source.array))
+        if isinstance(self.cfg.source, ZarrV2Array):
+            upload_zarr(self.cfg.source, self.cfg.target)
+        else:
+            self.cfg.target.from_numpy(np.asarray(self.cfg.source.array))
 
 
 class GpuDagExecutor(DagExecutor):
@@ -262,6 +267,25 @@ class GpuDagExecutor(DagExecutor):
                 strides_all.append(0)
         return ArrView(base, ext_all, strides_all, dt)
 
+    def gather_concat(self, srcs, parts, axis, field, gathers) -> ArrView:
+        """Assemble a concat output block (parts = (source index, region,
+        offset along ``axis``)) into contiguous scratch."""
+        dt = srcs[parts[0][0]].field_dtype(field)
+        ext = None
+        for ai, region, off in parts:
+            e = [max(0, (s.stop - (s.start or 0))) for s in region]
+            if ext is None:
+                ext = list(e)
+                ext[axis] = 0
+            ext[axis] = max(ext[axis], off + e[axis])
+        base = self.scratch(max(1, math.prod(ext)) * dt.itemsize)
+        dstr = list(c_strides(ext))
+        boxes = []
+        for ai, region, off in parts:
+            boxes += boxes_for_region(srcs[ai], region, base + off * dstr[axis] * dt.itemsize, dstr, field)
+        gathers.append((boxes, dt.itemsize))
+        return ArrView(base, ext, dstr, dt)
+
     def gather_keys(self, arr: DeviceArray, keys, field, gathers) -> ArrView:
         coords = [k[1:] for k in keys]
         region = []
@@ -328,7 +352,8 @@ class GpuDagExecutor(DagExecutor):
         if self.world == 1:
             return self._lower_local(program, cfg, target, keys)
         if isinstance(program, ir.ExprProgram) and program.reduce is not None and \
-                any(isinstance(l, ir.Region) for l in ir.leaves_of_program(program)):
+                any(isinstance(l, ir.Region) for l in ir.leaves_of_program(program)) and \
+                not any(isinstance(l, ir.Concat) for l in ir.leaves_of_program(program)):
             launches = self._lower_pieces_dist(program, cfg, target, keys)
             # every rank must take the same path (their collectives pair up)
             if self.comm.all_ok(launches is not None):
@@ -465,6 +490,13 @@ class GpuDagExecutor(DagExecutor):
                     continue
                 for k in ([a] if isinstance(a, tuple) else flatten_keys(a)):
                     add_key(k, leaf.field)
+            elif isinstance(leaf, ir.Concat):
+                block_id = tuple(args[leaf.block_arg][1:])
+                for ai, region, _ in leaf.region(block_id):
+                    src = self.device_source(leaf.sources[ai])
+                    if isinstance(src, DeviceArray) and src.world > 1:
+                        for coords, _, _ in region_pieces(src, region):
+                            out.append((src, tuple(coords), leaf.field))
             elif isinstance(leaf, ir.Region) and regions:
                 src = self.device_source(leaf.target)
                 if isinstance(src, DeviceArray) and src.world > 1:

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 4
+#define CUBED_ABI_VERSION 5
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -63,6 +63,8 @@ extern "C" {
 #define CUBED_E_LAYOUT (-3)
 #define CUBED_E_WORKSPACE (-4)
 #define CUBED_E_JIT (-5)
+#define CUBED_E_CODEC (-6)       /* malformed compressed chunk */
+#define CUBED_E_UNSUPPORTED (-7) /* codec / shuffle this build does not decode */
 
 /* element dtypes (numpy kinds); bool is 1 byte 0/1 */
 enum cubed_dtype {
@@ -313,6 +315,21 @@ int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntasks,
                       void* stream);
 
 /* library info */
+/* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
+ * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and
+ * writes (storage/zarr.py:8-103 LazyZarrArray.create/open; the chunk I/O of
+ * core/ops.py:88-182 from_zarr / store / to_zarr).  Reentrant, no GPU calls.
+ * cubed_blosc_decompress: dst must hold exactly the frame's nbytes.
+ * cubed_blosc_compress: lz4 + byte shuffle (shuffle != 0), unsplit blocks;
+ * dst must hold cubed_blosc_max_compressed(nbytes); returns the frame size
+ * or a negative error. */
+int cubed_blosc_header(const void* src, int64_t srclen, int64_t* nbytes, int64_t* cbytes,
+                       int* typesize, int* flags);
+int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen);
+int64_t cubed_blosc_max_compressed(int64_t nbytes);
+int64_t cubed_blosc_compress(const void* src, int64_t nbytes, int typesize, int shuffle, void* dst,
+                             int64_t dstcap);
+
 int cubed_abi_version(void);
 const char* cubed_last_error(void);
 int cubed_device_count(void);

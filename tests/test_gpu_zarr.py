@@ -1,0 +1,66 @@
+"""Zarr v2 sources and sinks on the MI355X path (``-m gpu``): from_zarr
+uploads decoded chunks into HBM, to_zarr / store write HBM chunks back
+(core/ops.py:88-182).  Byte moves: bit-exact; the reduction over a Zarr
+source uses the f64-accumulate tolerance of DESIGN.md (rtol 1e-6 for f32)."""
+
+import random
+
+import numpy as np
+import pytest
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.random as crandom
+from cubed_amd import zarr_io as Z
+from oracle import cubed_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spec(gpu_executor):
+    return cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=gpu_executor)
+
+
+@pytest.mark.parametrize("compressor", ["default", None, {"id": "zlib", "level": 1}])
+def test_from_zarr_bit_exact_and_mean(tmp_path, spec, compressor):
+    x = np.random.default_rng(5).random((50, 37, 41)).astype(np.float32)
+    a = Z.ZarrV2Array.create(str(tmp_path / "x.zarr"), x.shape, x.dtype, (10, 37, 16), compressor=compressor)
+    a[...] = x
+    y = cubed.from_zarr(str(tmp_path / "x.zarr"), spec=spec)
+    assert y.chunksize == (10, 37, 16)
+    assert np.array_equal(y.compute(), x)
+    got = xp.mean(y * y, axis=0).compute()
+    exp = R.mean(x * x, (10, 37, 16), 0, 2_000_000_000, 100_000_000)
+    assert np.allclose(got, exp, rtol=1e-6, atol=0)
+
+
+def test_from_zarr_missing_chunks_read_fill(tmp_path, spec):
+    a = Z.ZarrV2Array.create(str(tmp_path / "f.zarr"), (7, 9), np.int64, (3, 4), fill_value=-3)
+    a.write_chunk((1, 1), np.arange(12).reshape(3, 4))
+    exp = np.full((7, 9), -3)
+    exp[3:6, 4:8] = np.arange(12).reshape(3, 4)
+    assert np.array_equal(cubed.from_zarr(str(tmp_path / "f.zarr"), spec=spec).compute(), exp)
+
+
+def test_to_zarr_random_roundtrip(tmp_path, spec):
+    random.seed(11)
+    x = crandom.random((45, 30), chunks=(20, 7), spec=spec)
+    random.seed(11)
+    ref = R.random_array((45, 30), (20, 7), random.getrandbits(128))
+    t = cubed.to_zarr((x + 1) * 2, str(tmp_path / "o.zarr"))
+    back = Z.open_array(str(tmp_path / "o.zarr"))
+    assert back.chunks == (20, 7)
+    assert np.array_equal(back[...], (ref + 1) * 2)
+    # and it reads back through from_zarr unchanged
+    assert np.array_equal(cubed.from_zarr(t, spec=spec).compute(), (ref + 1) * 2)
+
+
+def test_store_rechunks_to_target(tmp_path, spec):
+    x = xp.asarray(np.arange(600, dtype=np.int32).reshape(20, 30), chunks=(20, 5), spec=spec)
+    t = Z.open_array(str(tmp_path / "s.zarr"), mode="w", shape=(20, 30), dtype=np.int32, chunks=(6, 30),
+                     compressor={"id": "gzip", "level": 1})
+    cubed.store(x, t)
+    assert np.array_equal(Z.open_array(str(tmp_path / "s.zarr"))[...], np.arange(600).reshape(20, 30))
+    with pytest.raises(ValueError, match="Different number"):
+        cubed.store([x, x], [t])

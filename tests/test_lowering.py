@@ -237,3 +237,38 @@ def test_full_reduction_is_lifted_to_the_stream_kernel(built, dry):
     first = _fused(dry)[0]
     assert first.fold is not None and first.prog.mode & MODE_STREAM
     assert first.max_kept == 64 * 64 and first.max_red == 4 * 100  # inner dims lifted; chunks x rows reduced
+
+
+def test_concat_is_one_copy_launch(built, dry):
+    """A concat whose middle output chunk straddles three inputs is one box
+    copy launch (no scratch gather, no per-input launches)."""
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    a = xp.asarray(np.ones((4, 5)), chunks=(3, 2), spec=spec)
+    b = xp.asarray(np.ones((1, 5)), chunks=(3, 2), spec=spec)
+    c = xp.asarray(np.ones((3, 5)), chunks=(3, 2), spec=spec)
+    d = xp.concat([a, b, c], axis=0)
+    arrays_to_plan(a, b, c).execute(executor=dry, array_names=[a.name, b.name, c.name])
+    dry.launched.clear()
+    arrays_to_plan(d).execute(executor=dry, resume=True, array_names=[d.name])
+    copies = [l for l in dry.launched if isinstance(l, CopyLaunch)]
+    assert len(dry.launched) == 1 and len(copies) == 1
+    # middle row of output blocks: 3 column blocks x 3 source pieces
+    assert copies[0].nboxes == 3 * 1 + 3 * 3 + 3 * 1
+
+
+def test_stack_and_reshape_lower(built, dry):
+    from cubed_amd.array_api.manipulation_functions import reshape_rechunk
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    s = xp.stack([xp.ones((4, 6), chunks=(2, 3), spec=spec) for _ in range(3)], axis=1)
+    assert s.shape == (4, 3, 6) and s.chunks == ((2, 2), (1, 1, 1), (3, 3))
+    arrays_to_plan(s).execute(executor=dry, array_names=[s.name])
+    r = xp.reshape(xp.arange(12, chunks=4, spec=spec), (3, 4))
+    assert r.chunks == ((1, 1, 1), (4,))
+    # dask's reshape_rechunk examples (vendor/dask/array/reshape.py)
+    assert reshape_rechunk((6, 5, 4), (3, 2, 5, 4), ((3, 3), (5,), (2, 2))) == \
+        (((2, 4), (5,), (2, 2)), ((1, 2), (2,), (5,), (2, 2)))
+    assert reshape_rechunk((6, 5, 4), (30, 4), ((2, 2, 2), (2, 3), (4,))) == \
+        (((1,) * 6, (5,), (4,)), ((5,) * 6, (4,)))
+    with pytest.raises(NotImplementedError):
+        reshape_rechunk((6, 5, 4), (4, 5, 6), ((6,), (5,), (4,)))
