@@ -604,14 +604,26 @@ CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
                            const cubed_program_t& P, const CUBED_G V* (&p)[NL],
                            const int64_t (&rs)[NL], int64_t lo, int64_t hi) {
   int64_t r = lo;
+  // leaves with reduced stride 0 (broadcast operands) are loop-invariant:
+  // loaded once here instead of once per row
+  V inv[NL][4];
+  if (MIXED && lo < hi) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+      if (rs[l] == 0) ld4c<V>(inv[l], p[l]);
+  }
   for (; r + U <= hi; r += U) {
     V buf[U][NL][4];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int l = 0; l < NL; ++l) {
-        if (MIXED) ld4s<V>(buf[u][l], p[l] + u * rs[l], rs[l] != 0);
-        else ld4(buf[u][l], p[l] + u * rs[l]);
+        if (MIXED && rs[l] == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) buf[u][l][j] = inv[l][j];
+        } else {
+          ld4(buf[u][l], p[l] + u * rs[l]);
+        }
       }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -626,8 +638,12 @@ CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
     V buf[NL][4];
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-      if (MIXED) ld4s<V>(buf[l], p[l], rs[l] != 0);
-      else ld4(buf[l], p[l]);
+      if (MIXED && rs[l] == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) buf[l][j] = inv[l][j];
+      } else {
+        ld4(buf[l], p[l]);
+      }
     }
     set_leaves<NL, V>(regs, buf);
     CUBED_RUN_PROLOGUE(V, 4, regs);

@@ -1489,7 +1489,7 @@ def canonicalize(rows: List[TaskRow], n: int, red_axes, leaves, kinds, check_out
 
 
 LIFT_MIN_ELEMS = 4096  # inner elements per task for a lifted full reduction
-LIFT_MIN_ROWS = 64     # outer (reduced) rows per kept element: partials stay small
+LIFT_MIN_ROWS = 32     # outer (reduced) rows per kept element: partials stay small
 
 
 def _lift_dims(rows, n):

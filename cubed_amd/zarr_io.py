@@ -451,6 +451,10 @@ def store(sources, targets, executor=None, **kwargs):
     """Save arrays to Zarr arrays (core/ops.py:111-152): each source is
     computed into HBM (rechunked to its target's chunks if they differ) and
     its chunks written by the rank that owns them."""
+    return _store_arrays(sources, targets, executor, **kwargs)
+
+
+def _store_arrays(sources, targets, executor, **kwargs):
     from .core.array import CoreArray, compute
 
     if isinstance(sources, CoreArray):
@@ -486,7 +490,7 @@ def to_zarr(x, store, executor=None, **kwargs):
         dist.barrier()  # metadata exists before any rank writes chunks
         if rank != 0:
             target = open_array(store, mode="r+")
-    store(x, target, executor=executor, **kwargs)
+    _store_arrays(x, target, executor, **kwargs)
     if world > 1:
         dist.barrier()  # every rank's chunks are on disk when to_zarr returns
     return target
