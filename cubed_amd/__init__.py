@@ -12,13 +12,14 @@ __version__ = "0.1.0"
 
 from .array_api import Array
 from .core.array import compute, measure_reserved_mem, visualize
+from .core.gufunc import apply_gufunc
 from .core.ops import from_array, from_zarr, map_blocks, store, to_zarr
 from .nan_functions import nanmean, nansum
 from .runtime.types import Callback, TaskEndEvent
 from .spec import Spec
 
 __all__ = [
-    "__version__", "Callback", "Array", "Spec", "TaskEndEvent", "compute", "from_array",
+    "__version__", "Callback", "Array", "Spec", "TaskEndEvent", "apply_gufunc", "compute", "from_array",
     "from_zarr", "map_blocks", "measure_reserved_mem", "nanmean", "nansum", "store",
     "to_zarr", "visualize",
 ]
