@@ -170,6 +170,15 @@ template <typename V, int VEC>
 CUBED_DEV void stv(char* base, int64_t off, int dt, const V (&v)[VEC]) {
   if constexpr (VEC == 1) {
     st1<V>(base + off * dt_size(dt), dt, v[0]);
+  } else if constexpr (VEC == 2) {
+    if (dt == CUBED_F64) {
+      f64x2 a; a.x = (double)v[0]; a.y = (double)v[1];
+      *gstore_ptr<f64x2>(base + off * 8) = a;
+    } else {
+      const int sz = dt_size(dt);
+      st1<V>(base + off * sz, dt, v[0]);
+      st1<V>(base + (off + 1) * sz, dt, v[1]);
+    }
   } else {
     switch (dt) {
       case CUBED_F32: {

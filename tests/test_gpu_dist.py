@@ -28,7 +28,9 @@ def _seeds(seed, n):
     return [random.getrandbits(128) for _ in range(n)]
 
 
-def _cases(rank, world):
+def _cases(rank, world, zdir):
+    import os
+
     import torch
 
     torch.cuda.set_device(0)
@@ -109,13 +111,27 @@ def _cases(rank, world):
     out["rechunk_mean"] = xp.mean(zc.rechunk((60, 9)), axis=0).compute()
     out["rechunk_max"] = xp.max(zc.rechunk((60, 9)), axis=0).compute()
     note("rechunk_mean")
+
+    # concat / stack / reshape: sources on other ranks are fetched
+    c1 = cubed.from_array(np.arange(70.0).reshape(7, 10), chunks=(3, 4), spec=spec)
+    c2 = cubed.from_array(np.arange(100.0, 120.0).reshape(2, 10), chunks=(3, 4), spec=spec)
+    out["concat"] = xp.concat([c1, c2, c1], axis=0).compute()
+    out["stack"] = xp.stack([c1, c1 * 2], axis=1).compute()
+    out["reshape"] = xp.reshape(cubed.from_array(np.arange(24.0), chunks=4, spec=spec), (4, 6)).compute()
+    note("manipulation")
+
+    # Zarr sink written by every rank (its own chunks), read back as a source
+    zpath = os.path.join(zdir, "w.zarr")
+    cubed.to_zarr(zc * 3, zpath)
+    out["zarr"] = cubed.from_zarr(zpath, spec=spec).compute()
+    note("zarr")
     torch.cuda.synchronize()
     return out
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_executor_matches_oracle(world):
-    res = run_ranks(_cases, world, timeout=300)
+def test_distributed_executor_matches_oracle(world, tmp_path):
+    res = run_ranks(_cases, world, str(tmp_path), timeout=300)
     # every rank assembles the same results
     for r in range(1, world):
         for k in res[0]:
@@ -158,3 +174,9 @@ def test_distributed_executor_matches_oracle(world):
     z = np.random.default_rng(15).random((60, 50))
     assert np.allclose(got["rechunk_mean"], z.mean(axis=0), rtol=1e-12, atol=0)
     assert np.array_equal(got["rechunk_max"], z.max(axis=0))
+
+    a70 = np.arange(70.0).reshape(7, 10)
+    assert np.array_equal(got["concat"], np.concatenate([a70, np.arange(100.0, 120.0).reshape(2, 10), a70]))
+    assert np.array_equal(got["stack"], np.stack([a70, a70 * 2], axis=1))
+    assert np.array_equal(got["reshape"], np.arange(24.0).reshape(4, 6))
+    assert np.array_equal(got["zarr"], z * 3)
