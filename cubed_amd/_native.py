@@ -149,6 +149,9 @@ def lib():
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]
     L.cubed_combine_partials.restype = c_int
+    L.cubed_gemm_batched.argtypes = [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                                     c_int64, c_int64, c_int64, c_int64, c_int32, c_void_p]
+    L.cubed_gemm_batched.restype = c_int
     L.cubed_blosc_header.argtypes = [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64),
                                      POINTER(c_int), POINTER(c_int)]
     L.cubed_blosc_header.restype = c_int
@@ -179,7 +182,7 @@ EXPORTED_SYMBOLS = (
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups",
-    "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
+    "cubed_gemm_batched", "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress",
 )
 

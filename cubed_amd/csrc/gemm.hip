@@ -5,6 +5,11 @@
 // the blockwise contraction is one C_t = A_t @ B_t on a chunk pair.
 // f32: v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate), 128x128
 // output tiles (below).  f64 / int64: 64x64 tiles of vector FMAs.
+// f32 and f64 products run on rocBLAS by default (blas.hip: 125 TF vs this
+// kernel's 102 TF on 8 x 5000^3, tools/gemm_probe.py); these kernels serve
+// int64 and CUBED_AMD_GEMM=native.  A K-permuted variant reading b128 operand
+// fragments (4 MFMAs per LDS read) measured 72 TF -- the transposed B staging
+// stores conflict -- and was dropped.
 #include "common.h"
 #include <stdio.h>
 

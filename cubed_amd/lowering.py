@@ -680,21 +680,50 @@ class FusedLaunch:
                                        self.ws_bytes, stream), "cubed_fused_chunks")
 
 
+GEMM_PATH = __import__("os").environ.get("CUBED_AMD_GEMM", "blas")  # "blas" | "native"
+
+
 class GemmLaunch:
+    """The chunk products of one matmul/tensordot pipeline.  f32 / f64 go to
+    rocBLAS (cubed_gemm_batched: tasks of one shape per batched call); int64
+    (and CUBED_AMD_GEMM=native) to the hand-written kernels of gemm.hip."""
+
     def __init__(self, rows, dtype_code, max_m, max_n, device, zero_targets=()):
         import torch
 
         self.n = len(rows)
         self.dtype_code = dtype_code
         self.max_m, self.max_n = max_m, max_n
-        self.table = torch.from_numpy(rows.view(np.uint8).copy()).to(device) if self.n else None
+        self.blas = GEMM_PATH != "native" and dtype_code in (ir.dtype_code(np.float32),
+                                                             ir.dtype_code(np.float64))
+        self.table = None
+        self.groups = []
+        if not self.n:
+            return
+        if not self.blas:
+            self.table = torch.from_numpy(rows.view(np.uint8).copy()).to(device)
+            return
+        by_shape = {}
+        for r in rows:
+            key = tuple(int(r[f]) for f in ("m", "n", "k", "lda", "ldb", "ldc", "accumulate"))
+            by_shape.setdefault(key, []).append((int(r["a"]), int(r["b"]), int(r["c"])))
+        for key, ptrs in by_shape.items():
+            arr = torch.tensor(np.array(ptrs, dtype=np.int64).T.copy(), device=device)  # (3, batch)
+            self.groups.append((key, arr))
 
     def run(self, stream):
         if not self.n:
             return
         L = nat.lib()
-        nat.check(L.cubed_gemm_chunks(self.table.data_ptr(), self.n, self.dtype_code, self.max_m,
-                                      self.max_n, stream), "cubed_gemm_chunks")
+        if not self.blas:
+            nat.check(L.cubed_gemm_chunks(self.table.data_ptr(), self.n, self.dtype_code, self.max_m,
+                                          self.max_n, stream), "cubed_gemm_chunks")
+            return
+        for (m, n, k, lda, ldb, ldc, acc), arr in self.groups:
+            base = arr.data_ptr()
+            batch = arr.shape[1]
+            nat.check(L.cubed_gemm_batched(self.dtype_code, base, base + 8 * batch, base + 16 * batch, batch,
+                                           m, n, k, lda, ldb, ldc, acc, stream), "cubed_gemm_batched")
 
 
 class Lowerer:

@@ -315,6 +315,14 @@ int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntasks,
                       void* stream);
 
 /* library info */
+/* Plain chunk GEMMs through rocBLAS (cubed_amd/csrc/blas.hip): ``batch``
+ * row-major products C_i (+)= A_i @ B_i of one shape, device arrays of
+ * pointers; dtype CUBED_F32 or CUBED_F64.  Replaces the numpy BLAS call of
+ * _matmul (linear_algebra_functions.py:62-64) like cubed_gemm_chunks. */
+int cubed_gemm_batched(int32_t dtype, const void* d_a_ptrs, const void* d_b_ptrs, const void* d_c_ptrs,
+                       int64_t batch, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
+                       int64_t ldc, int32_t accumulate, void* stream);
+
 /* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
  * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and
  * writes (storage/zarr.py:8-103 LazyZarrArray.create/open; the chunk I/O of

@@ -304,6 +304,29 @@ def test_matmul_f32_tiles(ex, shape_a, shape_b, ca, cb):
     assert np.all(np.abs(got - exp) <= 1e-6 * scale + 1e-30)
 
 
+@pytest.mark.parametrize("path", ["blas", "native"])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_matmul_blas_and_native_paths(ex, monkeypatch, path, dtype):
+    """f32/f64 chunk products through rocBLAS (default) and the hand-written
+    kernels (CUBED_AMD_GEMM=native), ragged chunks (several shapes per
+    launch), against an f64 product; bound = the f32 (or f64) rounding of a
+    length-K dot product plus the k-chunk sums."""
+    import cubed_amd.lowering as L
+
+    monkeypatch.setattr(L, "GEMM_PATH", path)
+    r = np.random.default_rng(21)
+    x = (r.random((150, 130)) - 0.5).astype(dtype)
+    y = (r.random((130, 170)) - 0.5).astype(dtype)
+    spec = mkspec(ex)
+    got = xp.matmul(cubed.from_array(x, chunks=(64, 50), spec=spec),
+                    cubed.from_array(y, chunks=(50, 80), spec=spec)).compute()
+    exp = x.astype(np.float64) @ y.astype(np.float64)
+    scale = np.abs(x).astype(np.float64) @ np.abs(y).astype(np.float64)
+    eps = 1e-6 if dtype == np.float32 else 1e-14
+    assert got.dtype == dtype
+    assert np.all(np.abs(got - exp) <= eps * scale + 1e-300)
+
+
 def test_tensordot_golden(ex):
     c = json.load(open(os.path.join(GOLDEN, "reference_cases.json")))["tensordot_axes_1"]
     spec = mkspec(ex)

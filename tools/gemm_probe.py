@@ -22,12 +22,20 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     tab = torch.from_numpy(rows.view(np.uint8).copy()).cuda()
     L = nat.lib()
     st = torch.cuda.current_stream().cuda_stream
-    nat.check(L.cubed_gemm_chunks(tab.data_ptr(), T, 9, n, n, st), "gemm")
+    if os.environ.get("CUBED_GEMM_VARIANT") == "blas":
+        from cubed_amd.lowering import GemmLaunch
+
+        GL = GemmLaunch(rows, 9, n, n, torch.device("cuda"))
+        assert GL.blas
+        run = lambda: GL.run(st)  # noqa: E731
+    else:
+        run = lambda: nat.check(L.cubed_gemm_chunks(tab.data_ptr(), T, 9, n, n, st), "gemm")  # noqa: E731
+    run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(3):
-        nat.check(L.cubed_gemm_chunks(tab.data_ptr(), T, 9, n, n, st), "gemm")
+        run()
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
@@ -37,5 +45,5 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           f"{2 * T * n ** 3 / ms / 1e9:.1f} TF, max err {err:.2e}", flush=True)
 else:
     for v in sys.argv[1:] or ["0"]:
-        env = dict(os.environ, CUBED_GEMM_VARIANT=v)
+        env = dict(os.environ, CUBED_GEMM_VARIANT=v)  # "blas" = rocBLAS path, else the native kernel
         subprocess.run([sys.executable, __file__, "--child"], env=env, check=True, timeout=300)
