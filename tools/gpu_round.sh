@@ -3,7 +3,7 @@
 # Every GPU step has its own time limit; a crash/abort/timeout ends the session
 # (test *failures* -- pytest exit 1 -- do not, so the bench still runs).
 set -o pipefail
-mkdir -p gpurun_out
+cd "${GRAFT_REPO_ROOT:-.}" && mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() { echo "== $1 $(date +%T)" >> gpurun_out/steps.log; }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
