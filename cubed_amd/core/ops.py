@@ -125,6 +125,12 @@ def _lower_callable(func, arrays, inds, out_ind, dtype, kwargs):
     refuses the plan)."""
     if isinstance(func, ir.Program):
         return func
+    if isinstance(func, _BlockIdFunc):
+        # the last argument is the block-offsets array map_blocks appended
+        meta = tuple((np.dtype(a.dtype), a.ndim) for a in arrays[:-1])
+        return ir.PerBlockProgram(func=func.func, kwargs=dict(kwargs), args_meta=meta,
+                                  inds=tuple(inds[:-1]), out_ind=tuple(out_ind), dtype=dtype,
+                                  nargs=len(arrays))
     if isinstance(func, partial) and not func.args:
         base = func.func
         kwargs = {**func.keywords, **kwargs}
@@ -145,6 +151,19 @@ def _lower_callable(func, arrays, inds, out_ind, dtype, kwargs):
             return ir.OpaqueProgram(func=func, nargs=len(arrays))
         return ir.ExprProgram(ndim=space, nargs=len(args), outputs=e,
                               out_axes=tuple(range(space)), name=name)
+    # a numpy reduction applied per chunk with keepdims (map_blocks(np.max,
+    # x, axis=0, keepdims=True)): the per-chunk reduce program of reduction()
+    red = as_chunk_reduction(base)
+    if red is not None and len(arrays) == 1 and kwargs.get("keepdims") and \
+            set(kwargs) <= {"axis", "keepdims", "dtype"} and tuple(inds[0] or ()) == tuple(out_ind):
+        ax = kwargs.get("axis")
+        nd = arrays[0].ndim
+        ax = tuple(range(nd)) if ax is None else tuple(a % nd for a in (ax if isinstance(ax, tuple) else (ax,)))
+        extra = {"dtype": kwargs["dtype"]} if kwargs.get("dtype") is not None else {}
+        try:
+            return red.program(nd, arrays[0].dtype, ax, keepdims=True, **extra)
+        except (NotImplementedError, TypeError, ValueError):
+            pass
     from ..tracing import trace_callable
 
     traced = trace_callable(func, arrays, inds, out_ind, dtype, kwargs)
@@ -410,11 +429,18 @@ def map_blocks(func, *args: "Array", dtype=None, chunks=None, drop_axis=[], new_
         if isinstance(func, _BlockIdProgram):
             func = func.build(len(args))
         else:
-            func = ir.OpaqueProgram(func=func, nargs=len(new_args))
+            func = _BlockIdFunc(func)
         return _map_blocks(func, *new_args, dtype=dtype, chunks=chunks, drop_axis=drop_axis,
                            new_axis=new_axis, **kwargs)
     return _map_blocks(func, *args, dtype=dtype, chunks=chunks, drop_axis=drop_axis,
                        new_axis=new_axis, **kwargs)
+
+
+class _BlockIdFunc:
+    """A user function taking ``block_id``: lowered per block (PerBlockProgram)."""
+
+    def __init__(self, func):
+        self.func = func
 
 
 def _has_block_id(func) -> bool:

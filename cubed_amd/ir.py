@@ -384,6 +384,37 @@ class GemmThenProgram(Program):
 
 
 @dataclass(frozen=True, eq=False)
+class PerBlockProgram(Program):
+    """A user chunk function that takes ``block_id`` (map_blocks,
+    core/ops.py:520-643): traced once per output block with the block id
+    bound, so block-dependent constants (``int(sum(block_id))``) become IR
+    constants.  The executor groups blocks whose traced programs are equal
+    and launches each group (``trace(block_id)`` raises when untraceable)."""
+    func: Any = None
+    kwargs: Any = None
+    args_meta: Tuple[Tuple[Any, int], ...] = ()  # (dtype, ndim) of the array args (no offsets)
+    inds: Tuple[Any, ...] = ()
+    out_ind: Tuple[Any, ...] = ()
+    dtype: Any = None
+    nargs: int = 1
+    name: str = "per-block"
+
+    def trace(self, block_id):
+        import functools
+        from types import SimpleNamespace
+
+        from .tracing import trace_callable
+
+        arrays = [SimpleNamespace(dtype=np.dtype(dt), ndim=nd) for dt, nd in self.args_meta]
+        f = functools.partial(self.func, block_id=tuple(int(b) for b in block_id), **(self.kwargs or {}))
+        prog = trace_callable(f, arrays, list(self.inds), self.out_ind, self.dtype, {})
+        if prog is None:
+            raise FusionError(f"{getattr(self.func, '__name__', self.func)!r} is not traceable for block "
+                              f"{tuple(block_id)}")
+        return replace(prog, nargs=self.nargs, name=getattr(self.func, "__name__", "per-block"))
+
+
+@dataclass(frozen=True, eq=False)
 class OpaqueProgram(Program):
     """A user function the IR could not express.  Plans containing one can be
     built (like the reference) but the GPU executor refuses to run them."""

@@ -1295,8 +1295,9 @@ class Lowerer:
                 src = self.ctx.device_source(leaf.target)
                 if isinstance(src, _ConstSource):
                     raise LoweringError("copy from a constant")
-                # destination strides for the region's kept dims (space = out dims)
+                # destination strides for the region's kept (non-int) dims
                 dstr = _dst_strides_for(leaf.axes, program.out_axes, dst)
+                dstr = [st for st, r in zip(dstr, region) if not _is_int_sel(r)]
                 boxes += boxes_for_region(src, region, dst.base, dstr, leaf.field)
             else:
                 a = args[leaf.index]

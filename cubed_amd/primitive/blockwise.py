@@ -208,7 +208,8 @@ def fuse(op1: PrimitiveOperation, op2: PrimitiveOperation) -> PrimitiveOperation
                                      nargs=p1.config.function_nargs)
     else:
         program = _fuse_program(p2.config.function, [p1.config.function], [p1.config.function_nargs])
-        if isinstance(program, ir.OpaqueProgram) and isinstance(p1.config.function, ir.ExprProgram) \
+        if isinstance(program, ir.OpaqueProgram) and \
+                isinstance(p1.config.function, (ir.ExprProgram, ir.PerBlockProgram)) \
                 and isinstance(p2.config.function, ir.ExprProgram):
             # not expressible as one program (e.g. a consumer of a chunk
             # reshape): one task still runs both, through op1's chunk

@@ -323,7 +323,8 @@ class GpuDagExecutor(DagExecutor):
                 raise LoweringError(
                     f"op {name}: {program.func!r} cannot run on the MI355X executor "
                     "(not expressible as a fused chunk program)")
-            if isinstance(program, (ir.ExprProgram, ir.MatmulProgram, ir.TensordotProgram)):
+            if isinstance(program, (ir.ExprProgram, ir.MatmulProgram, ir.TensordotProgram,
+                                    ir.PerBlockProgram)):
                 return self._lower_part(program, cfg, target, keys)
             if isinstance(program, ir.GemmThenProgram):
                 from types import SimpleNamespace
@@ -349,6 +350,19 @@ class GpuDagExecutor(DagExecutor):
         """Launches of one blockwise program over the tasks this rank owns.
         With several GPUs, chunks the owned tasks read from other ranks are
         fetched first (FetchLaunch) and the task views point at the copies."""
+        if isinstance(program, ir.PerBlockProgram):
+            # traced per output block; blocks with equal programs share a launch
+            groups = {}
+            for key in keys:
+                try:
+                    p = program.trace(key)
+                except ir.FusionError as e:
+                    raise LoweringError(str(e)) from None
+                groups.setdefault(repr(p.outputs), (p, []))[1].append(key)
+            out = []
+            for p, ks in groups.values():
+                out += self._lower_part(p, cfg, target, ks)
+            return out
         if self.world == 1:
             return self._lower_local(program, cfg, target, keys)
         if isinstance(program, ir.ExprProgram) and program.reduce is not None and \

@@ -44,6 +44,15 @@ class _Proxy:
                       max(x.ndim for x in xs))
 
     def __array_function__(self, func, types, args, kwargs):
+        fill = {np.ones_like: 1, np.zeros_like: 0}.get(func)
+        if func is np.full_like and len(args) >= 2:
+            fill = args[1]
+        if fill is not None and set(kwargs) <= {"dtype"} and len(args) <= 2:
+            # a constant of the chunk's shape (the task's extents come from its
+            # output block, so the operand is not read at all)
+            x = _lift(args[0])
+            dt = np.dtype(kwargs["dtype"]) if kwargs.get("dtype") is not None else x.dtype
+            return _Proxy(ir.Const(np.array(fill).astype(dt).item(), dt), x.ndim)
         if func is np.where and not kwargs:
             c, a, b = (_lift(x) for x in args)
             dt = np.result_type(_np_like(args[1]), _np_like(args[2]))
@@ -80,6 +89,21 @@ class _Untraceable(Exception):
     pass
 
 
+class _Unusable:
+    """Stand-in for an argument the traced function must not touch."""
+
+    def __getattr__(self, name):
+        raise _Untraceable("argument without output dims")
+
+    def _fail(self, *a, **k):
+        raise _Untraceable("argument without output dims")
+
+    __array_ufunc__ = __array_function__ = None
+    __add__ = __radd__ = __sub__ = __rsub__ = __mul__ = __rmul__ = __truediv__ = _fail
+    __rtruediv__ = __pow__ = __neg__ = __abs__ = __lt__ = __le__ = __gt__ = __ge__ = _fail
+    __array__ = _fail
+
+
 def _np_like(x):
     if isinstance(x, _Proxy):
         return np.empty((), dtype=x.dtype)
@@ -107,9 +131,18 @@ def trace_callable(func, arrays, inds, out_ind, dtype, kwargs):
     pos = {idx: i for i, idx in enumerate(out_ind)}
     proxies = []
     for i, (a, ind) in enumerate(zip(arrays, inds)):
-        if ind is None or any(idx not in pos for idx in ind):
-            return None
-        proxies.append(_Proxy(ir.Arg(i, a.dtype, tuple(pos[idx] for idx in ind)), a.ndim))
+        axes = [pos.get(idx) for idx in ind] if ind is not None else None
+        if axes is not None and None in axes and len(axes) == space:
+            # map_blocks(drop_axis=d, new_axis=d) relabels an axis: a dropped
+            # dim of a full-rank argument lands on the output dim at its position
+            used = {x for x in axes if x is not None}
+            axes = [d if x is None and d not in used else x for d, x in enumerate(axes)]
+        if axes is None or None in axes:
+            # an argument whose dims are not output dims can only be passed
+            # through unused (e.g. ``lambda x, y: x`` with y's dim dropped)
+            proxies.append(_Unusable())
+            continue
+        proxies.append(_Proxy(ir.Arg(i, a.dtype, tuple(axes)), a.ndim))
     try:
         with np.errstate(all="ignore"):
             out = func(*proxies, **kwargs)

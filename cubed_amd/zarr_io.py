@@ -247,6 +247,10 @@ class ZarrV2Array:
             out[sl] = self.read_chunk(coords)
         return out[key]
 
+    def __array__(self, dtype=None, copy=None):
+        out = self[...]
+        return out if dtype is None else out.astype(dtype)
+
     def __setitem__(self, key, value):
         if key not in (Ellipsis, slice(None)) and key != ():
             raise NotImplementedError("only arr[...] = value writes are supported")
@@ -456,6 +460,7 @@ def store(sources, targets, executor=None, **kwargs):
 
 def _store_arrays(sources, targets, executor, **kwargs):
     from .core.array import CoreArray, compute
+    from .storage import DeviceArray
 
     if isinstance(sources, CoreArray):
         sources = [sources]
@@ -471,10 +476,24 @@ def _store_arrays(sources, targets, executor, **kwargs):
             raise ValueError(f"source shape {s.shape} does not match target shape {t.shape}")
         if s.ndim and tuple(s.chunksize) != tuple(t.chunks):
             s = s.rechunk(tuple(t.chunks))
+        if not isinstance(s.zarray_maybe_lazy, DeviceArray):
+            # a virtual source (asarray / full): the reference's blockwise
+            # identity (core/ops.py:140-150) materialises it chunk by chunk
+            s = _identity(s)
         arrays.append(s)
     compute(*arrays, executor=executor, _return_in_memory_array=False, **kwargs)
     for a, t in zip(arrays, targets):
         write_device_array(a.zarray_maybe_lazy, t)
+
+
+def _identity(x):
+    from . import ir
+    from .core.ops import map_blocks
+
+    n = x.ndim
+    prog = ir.ExprProgram(ndim=n, nargs=1, outputs=ir.Arg(0, x.dtype, tuple(range(n))),
+                          out_axes=tuple(range(n)), name="identity")
+    return map_blocks(prog, x, dtype=x.dtype)
 
 
 def to_zarr(x, store, executor=None, **kwargs):

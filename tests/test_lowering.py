@@ -272,3 +272,43 @@ def test_stack_and_reshape_lower(built, dry):
         (((1,) * 6, (5,), (4,)), ((5,) * 6, (4,)))
     with pytest.raises(NotImplementedError):
         reshape_rechunk((6, 5, 4), (4, 5, 6), ((6,), (5,), (4,)))
+
+
+def test_int_indexed_copy_box_strides(built, dry):
+    """a[1, 2:4]: the int-indexed leading dim has no destination dim; the
+    box's destination stride is the kept dim's (regression: it took the int
+    dim's 0 and wrote both elements to one place)."""
+    spec = cubed.Spec(None, allowed_mem=100000, executor=dry)
+    a = xp.asarray(np.arange(16).reshape(4, 4), chunks=(2, 2), spec=spec)
+    b = a[1, 2:4]
+    arrays_to_plan(b).execute(executor=dry, array_names=[b.name])
+    copies = [l for l in dry.launched if isinstance(l, CopyLaunch)]
+    assert copies and all(bx.dstride[-1] == 1 and bx.extent[-1] == 2 for bx in copies[-1].boxes)
+
+
+def test_block_id_functions_trace_per_block(built, dry):
+    """map_blocks with a ``block_id`` function (test_core.py:184-209):
+    traced once per output block, blocks with equal programs share a launch
+    (sum(block_id) = 0..4 over 5 blocks: 5 programs; with ``% 2``: 2)."""
+    spec = cubed.Spec(None, allowed_mem=100000, executor=dry)
+    a = xp.arange(10, dtype="int64", chunks=(2,), spec=spec)
+
+    def f(block, block_id=None, c=0):
+        return np.ones_like(block) * int(sum(block_id)) + c
+
+    def g(block, block_id=None):
+        return block * (block_id[0] % 2)
+
+    for func, n in ((f, 5), (g, 2)):
+        dry.launched.clear()
+        b = cubed.map_blocks(func, a, dtype="int64")
+        arrays_to_plan(b).execute(executor=dry, array_names=[b.name])
+        assert len(_fused(dry)) == n + 1  # + the arange launch
+
+
+def test_numpy_reduction_in_map_blocks_lowers(built, dry):
+    spec = cubed.Spec(None, allowed_mem=100000, executor=dry)
+    a = xp.asarray(np.arange(10), chunks=5, spec=spec)
+    b = cubed.map_blocks(np.max, a, axis=0, keepdims=True, dtype=a.dtype, chunks=(1,))
+    arrays_to_plan(b).execute(executor=dry, array_names=[b.name])
+    assert _fused(dry)[-1].prog.nfields == 1
