@@ -91,7 +91,7 @@ GEMM_DTYPE = np.dtype([
     ("accumulate", np.int64),
 ])
 
-COPY_ROWS, COPY_ELEMS, COPY_TILE = 0, 1, 2
+COPY_ROWS, COPY_ELEMS, COPY_TILE, COPY_FLAT = 0, 1, 2, 3
 
 
 class NativeError(RuntimeError):

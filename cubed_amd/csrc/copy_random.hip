@@ -130,6 +130,52 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restr
   }
 }
 
+// Flat-destination kernel for 2-d boxes whose destination is packed
+// (dst row stride == row length): the box is walked as one contiguous run of
+// W-byte destination words, so every wave writes kSeg aligned consecutive
+// words whatever the row length (rechunk pieces of 4000-B rows no longer end
+// in partial lines per wave); each lane finds its source row by one 32-bit
+// division (host guarantees < 2^31 words per box).
+template <int W, int UN>
+__global__ __launch_bounds__(kBlock) void k_copy_flat(const cubed_box_t* __restrict__ boxes,
+                                                      int64_t nboxes, int32_t isz, int64_t bpb,
+                                                      int64_t segs_per_block) {
+  using T = typename conditional<W == 16, u32x4,
+            typename conditional<W == 8, uint64_t,
+            typename conditional<W == 4, uint32_t, uint8_t>::type>::type>::type;
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int64_t bi = g / bpb, blk = g % bpb;
+  if (bi >= nboxes) return;
+  const cubed_box_t* __restrict__ B = boxes + bi;
+  const uint32_t nw = (uint32_t)(B->extent[1] * isz / W);
+  const int64_t total = B->extent[0] * (int64_t)nw;
+  const int64_t sstr = B->src_stride[0] * isz;
+  const char* __restrict__ sbase = (const char*)(uintptr_t)B->src_base;
+  CUBED_G T* __restrict__ dst = (CUBED_G T*)(uintptr_t)B->dst_base;
+  constexpr int kSeg = 64 * UN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t w_begin = blk * segs_per_block * kSeg;
+  int64_t w_end = w_begin + segs_per_block * kSeg;
+  if (w_end > total) w_end = total;
+  for (int64_t i0 = w_begin + (int64_t)wave * kSeg; i0 < w_end; i0 += (int64_t)(kBlock / 64) * kSeg) {
+    T v[UN];
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t i = i0 + k * 64 + lane;
+      if (i < w_end) {
+        const uint32_t r = (uint32_t)i / nw, c = (uint32_t)i - r * nw;
+        const CUBED_G T* __restrict__ src = (const CUBED_G T*)(uintptr_t)(sbase + (int64_t)r * sstr);
+        v[k] = __builtin_nontemporal_load(src + c);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int64_t i = i0 + k * 64 + lane;
+      if (i < w_end) __builtin_nontemporal_store(v[k], dst + i);
+    }
+  }
+}
+
 // 64x64 LDS tile transpose-copy for 2-d boxes whose contiguous axes differ:
 // src contiguous along dim 1, dst contiguous along dim 0 (host arranges).
 template <typename T>
@@ -222,6 +268,22 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
     if (bpb < 1) bpb = 1;
     if (bpb > 65536) bpb = 65536;
     hipLaunchKernelGGL(k_copy_elems, grid2(nboxes * bpb), dim3(kBlock), 0, st, d_boxes, nboxes, nd, isz, bpb);
+  } else if (path == 3) {
+    // flat: work = max destination words per box (< 2^31), 16 segments of
+    // 64*UN words per workgroup (64 KiB with 16-B lanes)
+    if (nd != 2) return fail("cubed_copy_boxes: flat path needs 2-d boxes");
+    if (max_box_elems <= 0 || max_box_elems >= ((int64_t)1 << 31)) return fail("cubed_copy_boxes: flat path box size");
+    constexpr int UN = 4;
+    const int64_t spb = 16;
+    const int64_t nseg = (max_box_elems + 64 * UN - 1) / (64 * UN);
+    const int64_t bpb = (nseg + spb - 1) / spb;
+    const dim3 grid = grid2(nboxes * bpb);
+    switch (width) {
+      case 16: hipLaunchKernelGGL((k_copy_flat<16, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
+      case 8: hipLaunchKernelGGL((k_copy_flat<8, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
+      case 4: hipLaunchKernelGGL((k_copy_flat<4, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
+      default: hipLaunchKernelGGL((k_copy_flat<1, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
+    }
   } else {
     // rows: max_box_elems = max rows per box, row_bytes = longest row; work
     // units are <= 4 KiB row segments; aim ~64 KB per workgroup

@@ -26,6 +26,7 @@ import ctypes
 import dataclasses
 import itertools
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -266,6 +267,13 @@ class CopyLaunch:
             self.lane = lane
             self.work = max(math.prod(b.extent[:-1]) for b in boxes)
             self.row_bytes = max(b.extent[-1] for b in boxes) * itemsize
+            words = max(b.extent[0] * b.extent[1] * itemsize // lane for b in boxes) if nd == 2 else 0
+            if (nd == 2 and 0 < words < 2 ** 31 and all(b.dstride[0] == b.extent[1] for b in boxes)
+                    and os.environ.get("CUBED_AMD_COPY_FLAT", "1") != "0"):
+                # packed destinations (rechunk pieces): walk each box as one
+                # run of destination words
+                self.path = nat.COPY_FLAT
+                self.work = words
         elif nd == 2 and all(b.sstride[1] == 1 and b.dstride[0] == 1 for b in boxes):
             self.path = nat.COPY_TILE
             self.lane = 0

@@ -291,10 +291,15 @@ typedef struct {
  *                            work = max rows per box, row_bytes = max row size
  *       CUBED_COPY_ELEMS  -- any strides, element at a time; work = max elems
  *       CUBED_COPY_TILE   -- 2-d boxes, src contiguous along dim 1 and dst
- *                            along dim 0 (64x64 LDS tile); work = tiles/box */
+ *                            along dim 0 (64x64 LDS tile); work = tiles/box
+ *       CUBED_COPY_FLAT   -- 2-d boxes, innermost dim contiguous on both sides
+ *                            and dst packed (dst_stride[0] == extent[1]): the
+ *                            box is written as one run of lane_bytes words;
+ *                            work = max words per box (< 2^31) */
 #define CUBED_COPY_ROWS 0
 #define CUBED_COPY_ELEMS 1
 #define CUBED_COPY_TILE 2
+#define CUBED_COPY_FLAT 3
 int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int32_t ndim,
                      int32_t itemsize, int32_t path, int32_t lane_bytes,
                      int64_t work, int64_t row_bytes, void* stream);
