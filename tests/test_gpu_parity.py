@@ -261,6 +261,25 @@ def test_rechunk_int_dtypes(ex):
     assert np.array_equal(b.compute(), x)
 
 
+@pytest.mark.parametrize("flat", ["1", "0"])
+@pytest.mark.parametrize("dtype, shape, source, target", [
+    (np.float64, (300, 4000), (30, 4000), (300, 250)),   # 2000-B rows: 16-B lanes
+    (np.int32, (512, 1000), (64, 1000), (512, 250)),     # 1000-B rows: 8-B lanes
+    (np.int16, (400, 1000), (50, 1000), (400, 250)),     # 500-B rows: 4-B lanes
+    (np.uint8, (1000, 999), (100, 999), (1000, 37)),     # 37-B rows: 1-B lanes
+])
+def test_rechunk_copy_paths_bit_exact(ex, monkeypatch, flat, dtype, shape, source, target):
+    # packed-destination pieces take k_copy_flat (CUBED_COPY_FLAT) unless
+    # CUBED_AMD_COPY_FLAT=0 selects the per-row kernel; boxes span several
+    # workgroups so segment and row boundaries fall mid-wave
+    monkeypatch.setenv("CUBED_AMD_COPY_FLAT", flat)
+    x = np.random.default_rng(5).integers(0, 2**31, size=shape).astype(dtype)
+    spec = cubed.Spec(allowed_mem=10**9, executor=ex)
+    b = cubed.from_array(x, chunks=source, spec=spec).rechunk(target)
+    assert b.chunksize == tuple(target)
+    assert np.array_equal(b.compute(), x)
+
+
 def test_merge_chunks_values(ex):
     x = np.arange(100, dtype=np.float64).reshape(10, 10)
     spec = cubed.Spec(allowed_mem=100000, executor=ex)

@@ -312,3 +312,18 @@ def test_numpy_reduction_in_map_blocks_lowers(built, dry):
     b = cubed.map_blocks(np.max, a, axis=0, keepdims=True, dtype=a.dtype, chunks=(1,))
     arrays_to_plan(b).execute(executor=dry, array_names=[b.name])
     assert _fused(dry)[-1].prog.nfields == 1
+
+
+def test_copy_launch_picks_flat_path_for_packed_destinations(monkeypatch):
+    # rechunk piece: 30 rows of 250 f64 out of 4000-wide source rows into a
+    # packed (., 250) destination chunk -> CUBED_COPY_FLAT, work = 16-B words
+    from cubed_amd.lowering import Box
+
+    packed = Box(1 << 20, 1 << 30, [30, 250], [4000, 1], [250, 1])
+    cl = CopyLaunch([packed], 8, "cpu")
+    assert (cl.path, cl.lane, cl.work) == (nat.COPY_FLAT, 16, 30 * 250 * 8 // 16)
+    # destination rows not packed (dst stride 400): per-row kernel
+    strided = Box(1 << 20, 1 << 30, [30, 250], [4000, 1], [400, 1])
+    assert CopyLaunch([strided], 8, "cpu").path == nat.COPY_ROWS
+    monkeypatch.setenv("CUBED_AMD_COPY_FLAT", "0")
+    assert CopyLaunch([packed], 8, "cpu").path == nat.COPY_ROWS
