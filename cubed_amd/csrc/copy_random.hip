@@ -13,6 +13,7 @@
 // with 16/8/4/1-byte lanes.  Boxes whose innermost runs differ (after the host
 // drops unit dims -- e.g. (1,N) chunks -> (N,1) chunks) go through a 64x64
 // LDS tile so both the read and the write stay coalesced.
+#include <cstdlib>
 #include "common.h"
 #include <stdio.h>
 
@@ -274,7 +275,13 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
     if (nd != 2) return fail("cubed_copy_boxes: flat path needs 2-d boxes");
     if (max_box_elems <= 0 || max_box_elems >= ((int64_t)1 << 31)) return fail("cubed_copy_boxes: flat path box size");
     constexpr int UN = 4;
-    const int64_t spb = 16;
+    // segments per workgroup (16 = 64 KiB with 16-B lanes); CUBED_AMD_COPY_SPB
+    // overrides for A/B runs
+    int64_t spb = 16;
+    if (const char* e = getenv("CUBED_AMD_COPY_SPB")) {
+      const long v = atol(e);
+      if (v >= 1 && v <= 1024) spb = v;
+    }
     const int64_t nseg = (max_box_elems + 64 * UN - 1) / (64 * UN);
     const int64_t bpb = (nseg + spb - 1) / spb;
     const dim3 grid = grid2(nboxes * bpb);
