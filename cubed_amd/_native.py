@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 5  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 6  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -91,6 +91,17 @@ GEMM_DTYPE = np.dtype([
     ("accumulate", np.int64),
 ])
 
+# cubed_gemm_chain_t / cubed_gemm_seg_t (chained chunk GEMMs)
+CHAIN_DTYPE = np.dtype([
+    ("c", np.int64), ("m", np.int64), ("n", np.int64), ("ldc", np.int64),
+    ("seg0", np.int64), ("nseg", np.int64), ("ktot", np.int64), ("accumulate", np.int64),
+])
+SEG_DTYPE = np.dtype([
+    ("a", np.int64), ("b", np.int64), ("k", np.int64), ("lda", np.int64), ("ldb", np.int64),
+    ("pad", np.int64),
+])
+GEMM_AUTO, GEMM_ANY, GEMM_MFMA = -1, 0, 1
+
 COPY_ROWS, COPY_ELEMS, COPY_TILE, COPY_FLAT = 0, 1, 2, 3
 
 
@@ -125,6 +136,11 @@ def lib():
     L.cubed_copy_boxes.restype = c_int
     L.cubed_gemm_chunks.argtypes = [c_void_p, c_int64, c_int32, c_int64, c_int64, c_void_p]
     L.cubed_gemm_chunks.restype = c_int
+    L.cubed_gemm_chain_path.argtypes = [c_void_p, c_int64, c_void_p, c_int32, c_int32]
+    L.cubed_gemm_chain_path.restype = c_int
+    L.cubed_gemm_chain.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                   c_void_p, c_int32, c_void_p]
+    L.cubed_gemm_chain.restype = c_int
     L.cubed_fused_compile.argtypes = [POINTER(Program), c_char_p, POINTER(c_void_p)]
     L.cubed_fused_compile.restype = c_int
     L.cubed_fused_chunks_compiled.argtypes = [c_void_p, POINTER(Program), c_void_p, c_void_p, c_int64,
@@ -183,7 +199,7 @@ EXPORTED_SYMBOLS = (
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups",
     "cubed_gemm_batched", "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
-    "cubed_blosc_compress",
+    "cubed_blosc_compress", "cubed_gemm_chain", "cubed_gemm_chain_path",
 )
 
 

@@ -23,6 +23,7 @@ from .creation_functions import (
 )
 from .data_type_functions import astype, can_cast, finfo, iinfo, isdtype, result_type
 from .dtypes import (
+    bfloat16,
     bool,
     complex64,
     complex128,

@@ -85,12 +85,13 @@ def _field_map(p: ir.ExprProgram) -> Dict[Optional[str], ir.ReduceField]:
     return out
 
 
-def find_chains(dag, array_names) -> Dict[str, Chain]:
-    """{first node name: Chain} for every fusable reduction chain."""
+def find_chains(dag, array_names, exclude=()) -> Dict[str, Chain]:
+    """{first node name: Chain} for every fusable reduction chain (nodes in
+    ``exclude`` -- already claimed by another fusion -- are left alone)."""
     nodes = dict(dag.nodes(data=True))
     requested = set(array_names or ())
     chains = {}
-    claimed = set()
+    claimed = set(exclude)
     for n in dag.nodes():
         d = nodes[n]
         if n in claimed or "pipeline" not in d or d["pipeline"].function is not apply_blockwise:
@@ -118,7 +119,7 @@ def find_chains(dag, array_names) -> Dict[str, Chain]:
                 break
             nxt = next(iter(dag.successors(arr)))
             nd = nodes[nxt]
-            if "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
+            if nxt in claimed or "pipeline" not in nd or nd["pipeline"].function is not apply_blockwise:
                 break
             p2 = nd["pipeline"].config.function
             if not isinstance(p2, ir.ExprProgram) or p2.reduce is None:

@@ -8,6 +8,7 @@ from typing import Optional, TypeVar
 
 import numpy as np
 
+from .. import ir
 from ..runtime.types import Callback, Executor
 from ..spec import Spec
 from ..utils import chunk_memory, gensym_factory, normalize_chunks
@@ -94,7 +95,10 @@ class CoreArray:
                 raise RuntimeError(f"array {self.name} has not been computed")
             from ..runtime.executors.gpu import gather_to_host
 
-            return gather_to_host(t)
+            out = gather_to_host(t)
+            if out.dtype == ir.bfloat16:  # numpy has no bfloat16: widen exactly to f32
+                out = ir.bf16_to_numpy(out)
+            return out
         if isinstance(t, VirtualInMemoryArray):
             return np.array(t.array)
         if isinstance(t, VirtualFullArray):

@@ -1,0 +1,590 @@
+// gemm_chain.hip -- blockwise matmul / tensordot as chained chunk GEMMs.
+//
+// The reference computes matmul(A, B) in (i, k, j) tasks, each one numpy BLAS
+// call on a chunk pair, writing a (m, 1, n) partial product that a sum
+// reduction over the k axis then reads back
+// (cubed/array_api/linear_algebra_functions.py:13-78, _matmul :62-64,
+// _sum_wo_cat :67-78).  Here one task is one OUTPUT chunk C_ij, and its
+// contraction walks the k chunks in order: C_ij = sum_k A_ik @ B_kj, each
+// (A_ik, B_kj) pair a "segment" of one continuous K loop.  The partial
+// products never exist in HBM (at 40000^2 in 5000^2 chunks they would be
+// 2 x 51.2 GB of f32 written and re-read), and a per-chunk product is simply
+// a chain of one segment.
+//
+// Kernels:
+//   k_gemm_bf16_chain  bf16 x bf16 -> f32 accumulate (-> f32 / bf16 out) on
+//                      v_mfma_f32_16x16x32_bf16.  256 x 256 output tile per
+//                      512-thread workgroup (8 waves, 2 (M) x 4 (N), each
+//                      128 x 64 = 8 x 4 accumulators), K staged 64 deep
+//                      straight from HBM into LDS with global_load_lds
+//                      (16 B per lane, double buffered: the next K tile is in
+//                      flight while the current one feeds the MFMAs).
+//                      A is staged k-contiguous [m][64] (XOR-swizzled 16-B
+//                      chunks, conflict-free ds_read_b128 fragments); B is
+//                      staged as it lies in HBM, [k][256] rows, and read
+//                      transposed by ds_read_b64_tr_b16 (no transpose pass).
+//                      A segment boundary inside a K tile is a per-lane
+//                      pointer select; rows/cols past the chunk edge are
+//                      clamped (results discarded), k past the chain's end
+//                      reads a zero page.
+//   k_gemm_f32_chain   f32 on v_mfma_f32_32x32x2_f32 (exact f32 products, f32
+//                      accumulate): 128 x 128 tile, K staged 32 deep through
+//                      registers (float4) into k-major LDS.
+//   k_gemm_any_chain   any dtype (f64 / int64 / ragged bf16 or f32 shapes):
+//                      64 x 64 tiles of scalar FMAs, every element bounds-
+//                      checked.  Correctness path, not a fast path.
+#include "common.h"
+#include <stdio.h>
+
+namespace cubed {
+extern thread_local char g_err[512];
+}
+using namespace cubed;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+#define CUBED_L __attribute__((address_space(3)))
+
+namespace {
+
+// XCD-aware block order: blocks b and b+8 share an XCD (round-robin
+// dispatch), so map each XCD's blocks onto one contiguous run of tiles
+// (bijective for any grid size; cdna_hip_programming.md T1).
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblk) {
+  if (nblk < 8) return b;
+  const int64_t xcd = b & 7, q = nblk >> 3, r = nblk & 7, i = b >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
+}
+
+// tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked
+// column by column, so the workgroups resident on one XCD share A row panels
+// and B column panels in its L2.
+template <int BM, int BN, int GM>
+__device__ __forceinline__ bool tile_of(int64_t g, int64_t tiles_m, int64_t tiles_n, int64_t& t,
+                                        int64_t& m0, int64_t& n0) {
+  const int64_t tpt = tiles_m * tiles_n;
+  t = g / tpt;
+  const int64_t tile = g - t * tpt;
+  const int64_t per_group = GM * tiles_n;
+  const int64_t grp = tile / per_group, first_m = grp * GM;
+  const int64_t gsz = (tiles_m - first_m) < GM ? (tiles_m - first_m) : GM;
+  const int64_t in_g = tile - grp * per_group;
+  m0 = (first_m + in_g % gsz) * BM;
+  n0 = (in_g / gsz) * BN;
+  return true;
+}
+
+// ------------------------------------------------------------------ bf16 MFMA
+constexpr int HB_BM = 256, HB_BN = 256, HB_BK = 64;
+constexpr int HB_A = HB_BM * HB_BK * 2;   // 32 KiB: [256 rows][128 B]
+constexpr int HB_B = HB_BK * HB_BN * 2;   // 32 KiB: [64 k-rows][512 B]
+constexpr int HB_STAGE = HB_A + HB_B;
+
+struct Seg {  // wave-uniform view of one segment
+  const char* a;
+  const char* b;
+  int64_t lda2, ldb2;  // row pitches in bytes
+};
+
+__device__ __forceinline__ Seg load_seg(const cubed_gemm_seg_t* __restrict__ segs, int64_t i) {
+  Seg s;
+  s.a = (const char*)(uintptr_t)segs[i].a;
+  s.b = (const char*)(uintptr_t)segs[i].b;
+  s.lda2 = segs[i].lda * 2;
+  s.ldb2 = segs[i].ldb * 2;
+  return s;
+}
+
+__device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
+  __builtin_amdgcn_global_load_lds((const CUBED_G void*)(uintptr_t)src, (CUBED_L void*)dst, 16, 0, 0);
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_chain_t* __restrict__ tasks,
+                                                         const cubed_gemm_seg_t* __restrict__ segs,
+                                                         int64_t tiles_m, int64_t tiles_n,
+                                                         const char* __restrict__ zero) {
+  __shared__ __attribute__((aligned(1024))) char lds_[2 * HB_STAGE];
+  CUBED_L char* lds = (CUBED_L char*)lds_;
+  int64_t t, m0, n0;
+  tile_of<HB_BM, HB_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  const cubed_gemm_chain_t* __restrict__ T = tasks + t;
+  const int64_t M = T->m, N = T->n, KT = T->ktot;
+  if (m0 >= M || n0 >= N) return;
+  const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+
+  // ---- per-lane staging geometry (constant over the K loop)
+  // A: wave w stages rows 8*(4w+i) + lane>>3 (i = 0..3), 16-B chunk lane&7 of
+  // the LDS row holds global chunk (lane&7) ^ ((row>>1)&7).
+  int64_t gmA[4];
+  int dA[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = 8 * (4 * w + i) + (lane >> 3);
+    gmA[i] = (m0 + r < M ? m0 + r : M - 1);
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) dA[p] = 8 * ((lane & 7) ^ (4 * p + (lane >> 4)));
+  // B: wave w stages k-rows 2*(4w+i) + lane>>5, 16-B chunk c = lane&31 of the
+  // LDS row holds global chunk c ^ swz(row), swz(r) = 2*((r&3) | ((r>>3)&1)<<2).
+  int rB[4];
+  int64_t gnB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 2 * (4 * w + i) + (lane >> 5);
+    rB[i] = r;
+    const int swz = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+    int64_t n = n0 + 8 * ((lane & 31) ^ swz);
+    gnB[i] = (n + 8 <= N ? n : N - 8);
+  }
+
+  // ---- wave-uniform segment state
+  int64_t s = seg0, ks = 0;
+  Seg cur = load_seg(segs, s);
+  int64_t ke = segs[s].k;
+
+  // issue the global->LDS loads of K tile starting at k0 into stage buffer
+  auto stage = [&](int64_t k0, CUBED_L char* buf) {
+    const bool inside = k0 + HB_BK <= ke;  // uniform: no boundary in this tile
+    Seg nxt;
+    bool has_next = false;
+    if (!inside) {
+      has_next = s + 1 < segN;
+      if (has_next) nxt = load_seg(segs, s + 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t kk = k0 + dA[i & 1];
+      const char* src;
+      if (inside || kk < ke) src = cur.a + gmA[i] * cur.lda2 + (kk - ks) * 2;
+      else if (has_next && kk < KT) src = nxt.a + gmA[i] * nxt.lda2 + (kk - ke) * 2;
+      else src = zero;
+      glds16(src, buf + (4 * w + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t kk = k0 + rB[i];
+      const char* src;
+      if (inside || kk < ke) src = cur.b + (kk - ks) * cur.ldb2 + gnB[i] * 2;
+      else if (has_next && kk < KT) src = nxt.b + (kk - ke) * nxt.ldb2 + gnB[i] * 2;
+      else src = zero;
+      glds16(src, buf + HB_A + (4 * w + i) * 1024);
+    }
+  };
+  // after staging tile k0: move to the next segment if the next tile starts in it
+  auto advance = [&](int64_t k0next) {
+    if (k0next >= ke && s + 1 < segN) {
+      ks = ke;
+      ++s;
+      cur = load_seg(segs, s);
+      ke = ks + segs[s].k;
+    }
+  };
+
+  // ---- per-lane LDS read offsets
+  // A fragment (mb, kstep): row wr*128 + mb*16 + (lane&15), chunk (4*kstep + lane>>4) ^ ((lane>>1)&7)
+  int offA[2];
+#pragma unroll
+  for (int k2 = 0; k2 < 2; ++k2)
+    offA[k2] = wr * 16384 + (lane & 15) * 128 + 16 * ((4 * k2 + (lane >> 4)) ^ ((lane >> 1) & 7));
+  // B fragment (nb, kstep, half): row 32*kstep + 8g + 4*half + q, chunk (8wc + 2nb + (p>>1)) ^ swz
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int swzq = 2 * (q | ((g & 1) << 2));
+  int offB[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+    offB[nb] = HB_A + (8 * g + q) * 512 + 16 * ((8 * wc + 2 * nb + (pp >> 1)) ^ swzq) + 8 * (pp & 1);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nkt = (KT + HB_BK - 1) / HB_BK;
+  stage(0, lds);
+  advance(HB_BK);
+  __syncthreads();
+  for (int64_t kt = 0; kt < nkt; ++kt) {
+    CUBED_L char* bufc = lds + (kt & 1) * HB_STAGE;
+    if (kt + 1 < nkt) {
+      stage((kt + 1) * HB_BK, lds + ((kt + 1) & 1) * HB_STAGE);
+      advance((kt + 2) * HB_BK);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 bf[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const CUBED_L char* p = bufc + offB[nb] + k2 * 32 * 512;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CUBED_L bf16x4*)p);
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CUBED_L bf16x4*)(p + 4 * 512));
+        bf[nb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) {
+        const bf16x8 af = *(const CUBED_L bf16x8*)(bufc + offA[k2] + mb * 2048);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+  char* C = (char*)(uintptr_t)T->c;
+  const int64_t ldc = T->ldc;
+  const bool accum = T->accumulate != 0;
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + wr * 128 + mb * 16 + (lane >> 4) * 4 + r;
+        const int64_t gn = n0 + wc * 64 + nb * 16 + (lane & 15);
+        if (gm < M && gn < N) {
+          float v = acc[mb][nb][r];
+          if constexpr (OUT_BF16) {
+            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (gm * ldc + gn) * 2);
+            if (accum) v += bf16_to_f32(*c);
+            *c = f32_to_bf16(v);
+          } else {
+            CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (gm * ldc + gn) * 4);
+            if (accum) v += *c;
+            *c = v;
+          }
+        }
+      }
+}
+
+// ------------------------------------------------------------------ f32 MFMA
+// 128x128 tile per 256-thread workgroup: 2x2 waves, each a 64x64 sub-tile of
+// 2x2 v_mfma_f32_32x32x2_f32 accumulators; K staged 32 deep through
+// registers (float4) into k-major LDS; next tile's loads in flight during the
+// current tile's MFMAs.  Segments as in the bf16 kernel (k % 4 == 0 per
+// segment, so a float4 never straddles two).
+constexpr int HF_BM = 128, HF_BN = 128, HF_BK = 32;
+
+struct F4 { float x, y, z, w; };
+
+template <int LDA_S, int LDB_S>
+__global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
+                                                        const cubed_gemm_seg_t* __restrict__ segs,
+                                                        int64_t tiles_m, int64_t tiles_n) {
+  __shared__ float As[HF_BK][LDA_S];
+  __shared__ float Bs[HF_BK][LDB_S];
+  int64_t t, m0, n0;
+  tile_of<HF_BM, HF_BN, 8>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  const cubed_gemm_chain_t* __restrict__ T = tasks + t;
+  const int64_t M = T->m, N = T->n, KT = T->ktot;
+  if (m0 >= M || n0 >= N) return;
+  const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  int64_t s = seg0, ks = 0, ke = segs[seg0].k;
+  const float* a_cur = (const float*)(uintptr_t)segs[s].a;
+  const float* b_cur = (const float*)(uintptr_t)segs[s].b;
+  int64_t lda = segs[s].lda, ldb = segs[s].ldb;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  F4 ra[4], rb[4];
+  auto load = [&](int64_t k0) {
+    const bool inside = k0 + HF_BK <= ke;
+    const float* a_n = nullptr;
+    const float* b_n = nullptr;
+    int64_t lda_n = 0, ldb_n = 0;
+    if (!inside && s + 1 < segN) {
+      a_n = (const float*)(uintptr_t)segs[s + 1].a;
+      b_n = (const float*)(uintptr_t)segs[s + 1].b;
+      lda_n = segs[s + 1].lda;
+      ldb_n = segs[s + 1].ldb;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 256 * i;
+      // A tile: 128 rows x 8 float4 along k
+      const int row = f >> 3, kq = (f & 7) * 4;
+      const int64_t gm = m0 + row, kk = k0 + kq;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (gm < M && kk < KT) {
+        const float* p = (inside || kk < ke) ? a_cur + gm * lda + (kk - ks) : a_n + gm * lda_n + (kk - ke);
+        v = *(const CUBED_G f32x4*)(uintptr_t)p;
+      }
+      ra[i] = F4{v.x, v.y, v.z, v.w};
+      // B tile: 32 k-rows x 32 float4 along n
+      const int kr = f >> 5, nq = (f & 31) * 4;
+      const int64_t kk2 = k0 + kr, gn = n0 + nq;
+      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (kk2 < KT && gn < N) {
+        const float* p = (inside || kk2 < ke) ? b_cur + (kk2 - ks) * ldb + gn : b_n + (kk2 - ke) * ldb_n + gn;
+        u = *(const CUBED_G f32x4*)(uintptr_t)p;
+      }
+      rb[i] = F4{u.x, u.y, u.z, u.w};
+    }
+  };
+  auto advance = [&](int64_t k0next) {
+    if (k0next >= ke && s + 1 < segN) {
+      ks = ke;
+      ++s;
+      a_cur = (const float*)(uintptr_t)segs[s].a;
+      b_cur = (const float*)(uintptr_t)segs[s].b;
+      lda = segs[s].lda;
+      ldb = segs[s].ldb;
+      ke = ks + segs[s].k;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = tid + 256 * i;
+      const int row = f >> 3, kq = (f & 7) * 4;
+      As[kq + 0][row] = ra[i].x;
+      As[kq + 1][row] = ra[i].y;
+      As[kq + 2][row] = ra[i].z;
+      As[kq + 3][row] = ra[i].w;
+      const int kr = f >> 5, nq = (f & 31) * 4;
+      f32x4 v;
+      v.x = rb[i].x; v.y = rb[i].y; v.z = rb[i].z; v.w = rb[i].w;
+      *(f32x4*)&Bs[kr][nq] = v;
+    }
+  };
+
+  load(0);
+  advance(HF_BK);
+  store();
+  __syncthreads();
+  const int hi = lane >> 5, lo = lane & 31;
+  for (int64_t k0 = 0; k0 < KT; k0 += HF_BK) {
+    const bool more = k0 + HF_BK < KT;
+    if (more) {
+      load(k0 + HF_BK);  // in flight during this tile's MFMAs
+      advance(k0 + 2 * HF_BK);
+    }
+#pragma unroll 4
+    for (int kk = 0; kk < HF_BK; kk += 2) {
+      const float a0 = As[kk + hi][wm + lo], a1 = As[kk + hi][wm + 32 + lo];
+      const float b0 = Bs[kk + hi][wn + lo], b1 = Bs[kk + hi][wn + 32 + lo];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  // C/D map of a 32x32 accumulator: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  CUBED_G float* __restrict__ C = (CUBED_G float*)(uintptr_t)T->c;
+  const bool accum = T->accumulate != 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * hi;
+        const int64_t gm = m0 + wm + 32 * i + row, gn = n0 + wn + 32 * j + lo;
+        if (gm < M && gn < N) {
+          CUBED_G float* c = C + gm * T->ldc + gn;
+          *c = accum ? (*c + acc[i][j][r]) : acc[i][j][r];
+        }
+      }
+}
+
+// ------------------------------------------------------------------ any dtype
+// c + a*b: fused for floats (BLAS-style FMA accumulation), wrapping for int64
+CUBED_DEV float mul_add(float a, float b, float c) { return fmaf(a, b, c); }
+CUBED_DEV double mul_add(double a, double b, double c) { return fma(a, b, c); }
+CUBED_DEV int64_t mul_add(int64_t a, int64_t b, int64_t c) {
+  return (int64_t)((uint64_t)c + (uint64_t)a * (uint64_t)b);
+}
+
+static constexpr int TM = 64, TN = 64, TK = 16;
+
+// IN: storage dtype of A and B (cubed_dtype); V: accumulator type
+template <int IN, typename V>
+__global__ __launch_bounds__(256) void k_gemm_any_chain(const cubed_gemm_chain_t* __restrict__ tasks,
+                                                     const cubed_gemm_seg_t* __restrict__ segs,
+                                                     int64_t tiles_m, int64_t tiles_n, int32_t out_dt) {
+  __shared__ V As[TK][TM + 1];
+  __shared__ V Bs[TK][TN + 1];
+  int64_t t, m0, n0;
+  tile_of<TM, TN, 8>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  const cubed_gemm_chain_t* __restrict__ TT = tasks + t;
+  const int64_t M = TT->m, N = TT->n;
+  if (m0 >= M || n0 >= N) return;
+  const int isz = dt_size(IN);
+  const int tid = threadIdx.x;
+  const int tr = (tid >> 4) * 4, tc = (tid & 15) * 4;  // 4x4 per thread
+  V acc[4][4] = {};
+  for (int64_t si = TT->seg0; si < TT->seg0 + TT->nseg; ++si) {
+    const char* A = (const char*)(uintptr_t)segs[si].a;
+    const char* B = (const char*)(uintptr_t)segs[si].b;
+    const int64_t K = segs[si].k, lda = segs[si].lda, ldb = segs[si].ldb;
+    for (int64_t k0 = 0; k0 < K; k0 += TK) {
+      for (int i = tid; i < TM * TK; i += 256) {
+        const int mm = i / TK, kk = i % TK;
+        const int64_t gm = m0 + mm, gk = k0 + kk;
+        As[kk][mm] = (gm < M && gk < K) ? ld1<V>(A + (gm * lda + gk) * isz, IN) : (V)0;
+      }
+      for (int i = tid; i < TN * TK; i += 256) {
+        const int kk = i / TN, nn = i % TN;
+        const int64_t gk = k0 + kk, gn = n0 + nn;
+        Bs[kk][nn] = (gk < K && gn < N) ? ld1<V>(B + (gk * ldb + gn) * isz, IN) : (V)0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < TK; ++kk) {
+        V a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { a[i] = As[kk][tr + i]; b[i] = Bs[kk][tc + i]; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mul_add(a[i], b[j], acc[i][j]);
+      }
+      __syncthreads();
+    }
+  }
+  const int osz = dt_size(out_dt);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gm = m0 + tr + i, gn = n0 + tc + j;
+      if (gm < M && gn < N) {
+        char* c = (char*)(uintptr_t)TT->c + (gm * TT->ldc + gn) * osz;
+        V v = acc[i][j];
+        if (TT->accumulate) v = v + ld1<V>(c, out_dt);
+        st1<V>(c, out_dt, v);
+      }
+    }
+}
+
+int fail(const char* m) {
+  snprintf(g_err, sizeof(g_err), "cubed_gemm_chain: %s", m);
+  return CUBED_E_ARG;
+}
+
+bool aligned16(int64_t x) { return (x & 15) == 0; }
+
+}  // namespace
+
+// Which kernel serves a chain set (host tables): the MFMA fast paths need
+// every segment's k a multiple of 8 (bf16) / 4 (f32) and >= the K tile
+// (64 / 32), 16-B aligned operand rows, and (bf16) n a multiple of 8.
+extern "C" int cubed_gemm_chain_path(const cubed_gemm_chain_t* tasks, int64_t ntasks,
+                                     const cubed_gemm_seg_t* segs, int32_t in_dtype,
+                                     int32_t out_dtype) {
+  if (in_dtype == CUBED_BF16 && (out_dtype == CUBED_F32 || out_dtype == CUBED_BF16)) {
+    for (int64_t t = 0; t < ntasks; ++t) {
+      const cubed_gemm_chain_t& T = tasks[t];
+      if (T.n < 8 || T.n % 8 || T.m < 1) return CUBED_GEMM_ANY;
+      for (int64_t i = T.seg0; i < T.seg0 + T.nseg; ++i) {
+        const cubed_gemm_seg_t& s = segs[i];
+        if (s.k < 64 || s.k % 8 || s.lda % 8 || s.ldb % 8 || !aligned16(s.a) || !aligned16(s.b))
+          return CUBED_GEMM_ANY;
+      }
+    }
+    return CUBED_GEMM_MFMA;
+  }
+  if (in_dtype == CUBED_F32 && out_dtype == CUBED_F32) {
+    for (int64_t t = 0; t < ntasks; ++t) {
+      const cubed_gemm_chain_t& T = tasks[t];
+      if (T.n % 4 || T.m < 1) return CUBED_GEMM_ANY;
+      for (int64_t i = T.seg0; i < T.seg0 + T.nseg; ++i) {
+        const cubed_gemm_seg_t& s = segs[i];
+        if (s.k < 32 || s.k % 4 || s.lda % 4 || s.ldb % 4 || !aligned16(s.a) || !aligned16(s.b))
+          return CUBED_GEMM_ANY;
+      }
+    }
+    return CUBED_GEMM_MFMA;
+  }
+  return CUBED_GEMM_ANY;
+}
+
+extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
+                                int64_t ntasks, const cubed_gemm_seg_t* segs,
+                                const cubed_gemm_seg_t* d_segs, int64_t nsegs, int32_t in_dtype,
+                                int32_t out_dtype, const void* d_zero, int32_t path, void* stream) {
+  if (ntasks == 0) return 0;
+  if (!tasks || !d_tasks || !segs || !d_segs || ntasks < 0 || nsegs <= 0) return fail("bad argument");
+  int64_t max_m = 1, max_n = 1;
+  for (int64_t t = 0; t < ntasks; ++t) {
+    const cubed_gemm_chain_t& T = tasks[t];
+    if (T.m < 0 || T.n < 0 || T.nseg < 1 || T.seg0 < 0 || T.seg0 + T.nseg > nsegs || T.c == 0)
+      return fail("task out of range");
+    int64_t kt = 0;
+    for (int64_t i = T.seg0; i < T.seg0 + T.nseg; ++i) {
+      if (segs[i].k < 0 || !segs[i].a || !segs[i].b) return fail("bad segment");
+      kt += segs[i].k;
+    }
+    if (kt != T.ktot) return fail("ktot is not the sum of the task's segments");
+    max_m = T.m > max_m ? T.m : max_m;
+    max_n = T.n > max_n ? T.n : max_n;
+  }
+  const int auto_path = cubed_gemm_chain_path(tasks, ntasks, segs, in_dtype, out_dtype);
+  if (path == CUBED_GEMM_AUTO) path = auto_path;
+  if (path == CUBED_GEMM_MFMA && auto_path != CUBED_GEMM_MFMA) return fail("shapes do not fit the MFMA path");
+  hipStream_t st = (hipStream_t)stream;
+  if (path == CUBED_GEMM_MFMA && in_dtype == CUBED_BF16) {
+    if (!d_zero) return fail("the bf16 path needs a zero page");
+    const int64_t tm = (max_m + HB_BM - 1) / HB_BM, tn = (max_n + HB_BN - 1) / HB_BN;
+    const int64_t blocks = ntasks * tm * tn;
+    if (blocks > 0x7fffffff) return fail("grid too large");
+    if (out_dtype == CUBED_BF16)
+      hipLaunchKernelGGL(k_gemm_bf16_chain<true>, dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm,
+                         tn, (const char*)d_zero);
+    else
+      hipLaunchKernelGGL(k_gemm_bf16_chain<false>, dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm,
+                         tn, (const char*)d_zero);
+  } else if (path == CUBED_GEMM_MFMA && in_dtype == CUBED_F32) {
+    const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
+    const int64_t blocks = ntasks * tm * tn;
+    if (blocks > 0x7fffffff) return fail("grid too large");
+    hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       d_tasks, d_segs, tm, tn);
+  } else {
+    const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
+    const int64_t blocks = ntasks * tm * tn;
+    if (blocks > 0x7fffffff) return fail("grid too large");
+    dim3 grid((unsigned)blocks), blk(256);
+    switch (in_dtype) {
+      case CUBED_BF16:
+        hipLaunchKernelGGL((k_gemm_any_chain<CUBED_BF16, float>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, out_dtype);
+        break;
+      case CUBED_F32:
+        hipLaunchKernelGGL((k_gemm_any_chain<CUBED_F32, float>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, out_dtype);
+        break;
+      case CUBED_F64:
+        hipLaunchKernelGGL((k_gemm_any_chain<CUBED_F64, double>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, out_dtype);
+        break;
+      case CUBED_I64:
+        hipLaunchKernelGGL((k_gemm_any_chain<CUBED_I64, int64_t>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, out_dtype);
+        break;
+      default:
+        snprintf(g_err, sizeof(g_err), "cubed_gemm_chain: input dtype %d not supported", in_dtype);
+        return CUBED_E_DTYPE;
+    }
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}

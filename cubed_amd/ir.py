@@ -28,7 +28,13 @@ import numpy as np
 
 # ----------------------------------------------------------------- dtypes
 
+# numpy has no bfloat16: it is carried as a distinct 2-byte void dtype (its
+# bit pattern = the top half of an IEEE f32).  The kernels load/store it as
+# CUBED_BF16; host readback widens it exactly to float32 (bf16_to_numpy).
+bfloat16 = np.dtype("V2")
+
 DTYPE_CODES = {
+    bfloat16: 12,
     np.dtype("bool"): 0, np.dtype("int8"): 1, np.dtype("int16"): 2,
     np.dtype("int32"): 3, np.dtype("int64"): 4, np.dtype("uint8"): 5,
     np.dtype("uint16"): 6, np.dtype("uint32"): 7, np.dtype("uint64"): 8,
@@ -45,7 +51,27 @@ def dtype_code(dt) -> int:
 
 
 def is_float(dt) -> bool:
-    return np.dtype(dt).kind == "f"
+    dt = np.dtype(dt)
+    return dt.kind == "f" or dt == bfloat16
+
+
+def is_bf16(dt) -> bool:
+    return np.dtype(dt) == bfloat16
+
+
+def bf16_to_numpy(a: np.ndarray) -> np.ndarray:
+    """bfloat16 bits (the V2 carrier dtype) -> the same values as float32."""
+    return (np.ascontiguousarray(a).view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+
+
+def numpy_to_bf16(a: np.ndarray) -> np.ndarray:
+    """float values -> bfloat16 bits (round to nearest even through f32, NaN
+    kept quiet), as the V2 carrier dtype."""
+    u = np.ascontiguousarray(np.asarray(a, dtype=np.float32)).view(np.uint32).astype(np.uint64)
+    nan = (u & 0x7FFFFFFF) > 0x7F800000
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    r = np.where(nan, ((u >> 16) | 0x40).astype(np.uint16), r)
+    return r.view(bfloat16)
 
 
 def is_int(dt) -> bool:

@@ -377,7 +377,7 @@ class Codegen:
         else:
             v = float(np.array(value).astype(np.float64))
             if self.vtype == V_F32 or dtype == np.float32:
-                v = float(np.float32(v)) if dtype.kind == "f" and dtype.itemsize <= 4 else v
+                v = float(np.float32(v)) if ir.is_float(dtype) and dtype.itemsize <= 4 else v
             item = ("f", v)
         for i, c in enumerate(self.consts):
             if c == item and not (isinstance(c[1], float) and math.isnan(c[1])):
@@ -487,7 +487,7 @@ def choose_vtype(exprs, leaves) -> int:
     dts = [np.dtype(n.dtype) for n in nodes if not isinstance(n, ir.Field)]
     if all(d.kind in "biu" for d in dts):
         return V_I64
-    small = {np.dtype(np.float32), np.dtype(np.float16), np.dtype(np.bool_), np.dtype(np.int8),
+    small = {np.dtype(np.float32), np.dtype(np.float16), ir.bfloat16, np.dtype(np.bool_), np.dtype(np.int8),
              np.dtype(np.uint8), np.dtype(np.int16), np.dtype(np.uint16)}
     ok = True
     for n in nodes:
@@ -688,50 +688,70 @@ class FusedLaunch:
                                        self.ws_bytes, stream), "cubed_fused_chunks")
 
 
-GEMM_PATH = __import__("os").environ.get("CUBED_AMD_GEMM", "blas")  # "blas" | "native"
+GEMM_PATH = __import__("os").environ.get("CUBED_AMD_GEMM", "native")  # "native" | "blas"
 
 
 class GemmLaunch:
-    """The chunk products of one matmul/tensordot pipeline.  f32 / f64 go to
-    rocBLAS (cubed_gemm_batched: tasks of one shape per batched call); int64
-    (and CUBED_AMD_GEMM=native) to the hand-written kernels of gemm.hip."""
+    """Chained chunk GEMMs of one matmul / tensordot (``cubed_gemm_chain``):
+    one task per output chunk, each summing its segment products in one K
+    loop (a per-chunk product is a chain of one segment).  The hand-written
+    MFMA kernels (csrc/gemm_chain.hip) run every dtype; CUBED_AMD_GEMM=blas
+    sends single-segment f32 / f64 products to rocBLAS instead, kept only
+    as the library comparator of bench.py / tools/gemm_probe.py."""
 
-    def __init__(self, rows, dtype_code, max_m, max_n, device, zero_targets=()):
+    def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None):
         import torch
 
-        self.n = len(rows)
-        self.dtype_code = dtype_code
-        self.max_m, self.max_n = max_m, max_n
-        self.blas = GEMM_PATH != "native" and dtype_code in (ir.dtype_code(np.float32),
-                                                             ir.dtype_code(np.float64))
-        self.table = None
+        self.n = len(tasks)
+        self.in_code, self.out_code = in_code, out_code
+        self.tasks = np.ascontiguousarray(tasks)
+        self.segs = np.ascontiguousarray(segs) if len(segs) else np.zeros(1, dtype=nat.SEG_DTYPE)
+        self.zero = zero_ptr
+        self.path = nat.GEMM_AUTO if path is None else path
+        self.flops = 2.0 * float(sum(int(t["m"]) * int(t["n"]) * int(t["ktot"]) for t in self.tasks))
+        self.blas = (GEMM_PATH == "blas" and in_code == out_code and
+                     in_code in (ir.dtype_code(np.float32), ir.dtype_code(np.float64)) and
+                     self.n and all(int(t["nseg"]) == 1 for t in self.tasks))
         self.groups = []
         if not self.n:
             return
-        if not self.blas:
-            self.table = torch.from_numpy(rows.view(np.uint8).copy()).to(device)
+        if self.blas:
+            by_shape = {}
+            for t in self.tasks:
+                sg = self.segs[int(t["seg0"])]
+                key = (int(t["m"]), int(t["n"]), int(sg["k"]), int(sg["lda"]), int(sg["ldb"]),
+                       int(t["ldc"]), int(t["accumulate"]))
+                by_shape.setdefault(key, []).append((int(sg["a"]), int(sg["b"]), int(t["c"])))
+            for key, ptrs in by_shape.items():
+                arr = torch.tensor(np.array(ptrs, dtype=np.int64).T.copy(), device=device)  # (3, batch)
+                self.groups.append((key, arr))
             return
-        by_shape = {}
-        for r in rows:
-            key = tuple(int(r[f]) for f in ("m", "n", "k", "lda", "ldb", "ldc", "accumulate"))
-            by_shape.setdefault(key, []).append((int(r["a"]), int(r["b"]), int(r["c"])))
-        for key, ptrs in by_shape.items():
-            arr = torch.tensor(np.array(ptrs, dtype=np.int64).T.copy(), device=device)  # (3, batch)
-            self.groups.append((key, arr))
+        self.d_tasks = torch.from_numpy(self.tasks.view(np.uint8).copy()).to(device)
+        self.d_segs = torch.from_numpy(self.segs.view(np.uint8).copy()).to(device)
+
+    def kernel_path(self) -> int:
+        """CUBED_GEMM_MFMA or CUBED_GEMM_ANY (host-side decision)."""
+        if self.path != nat.GEMM_AUTO:
+            return self.path
+        return nat.lib().cubed_gemm_chain_path(self.tasks.ctypes.data, self.n, self.segs.ctypes.data,
+                                               self.in_code, self.out_code)
 
     def run(self, stream):
         if not self.n:
             return
         L = nat.lib()
-        if not self.blas:
-            nat.check(L.cubed_gemm_chunks(self.table.data_ptr(), self.n, self.dtype_code, self.max_m,
-                                          self.max_n, stream), "cubed_gemm_chunks")
+        if self.blas:
+            for (m, n, k, lda, ldb, ldc, acc), arr in self.groups:
+                base = arr.data_ptr()
+                batch = arr.shape[1]
+                nat.check(L.cubed_gemm_batched(self.in_code, base, base + 8 * batch, base + 16 * batch,
+                                               batch, m, n, k, lda, ldb, ldc, acc, stream),
+                          "cubed_gemm_batched")
             return
-        for (m, n, k, lda, ldb, ldc, acc), arr in self.groups:
-            base = arr.data_ptr()
-            batch = arr.shape[1]
-            nat.check(L.cubed_gemm_batched(self.dtype_code, base, base + 8 * batch, base + 16 * batch, batch,
-                                           m, n, k, lda, ldb, ldc, acc, stream), "cubed_gemm_batched")
+        nat.check(L.cubed_gemm_chain(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.n,
+                                     self.segs.ctypes.data, self.d_segs.data_ptr(), len(self.segs),
+                                     self.in_code, self.out_code, self.zero, self.path, stream),
+                  "cubed_gemm_chain")
 
 
 class Lowerer:

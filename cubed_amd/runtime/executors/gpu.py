@@ -162,6 +162,7 @@ class GpuDagExecutor(DagExecutor):
         self.rank, self.world = 0, 1
         self.timing: Optional[LaunchTimer] = None
         self.fuse_reductions = True
+        self.fuse_gemm_sums = True
         self._chains: Dict = {}
         self._exec_dags: Dict = {}
         self.fuse_producers = True
@@ -567,9 +568,11 @@ class GpuDagExecutor(DagExecutor):
         return CopyLaunch(boxes, dst.dtype.itemsize, self.device)
 
     def _lower_gemm(self, program, cfg, target, keys):
-        rows = np.zeros(len(keys), dtype=nat.GEMM_DTYPE)
-        max_m = max_n = 1
-        f32 = (program.out_dtype == np.float32)
+        """Per-chunk products (each task a chain of one segment): the matmul
+        blockwise op when its k-sum is not fused (gemm_chains.py)."""
+        tasks = np.zeros(len(keys), dtype=nat.CHAIN_DTYPE)
+        segs = np.zeros(len(keys), dtype=nat.SEG_DTYPE)
+        in_dt = None
         for i, key in enumerate(keys):
             args = cfg.block_function(("out",) + tuple(key))
             a_key, b_key = args[0], args[1]
@@ -577,21 +580,33 @@ class GpuDagExecutor(DagExecutor):
             B = self.device_source(cfg.reads_map[b_key[0]].array)
             if A.ndim != 2 or B.ndim != 2:
                 raise LoweringError("batched matmul chunks are not lowered yet")
-            if f32 and not (A.dtype == np.float32 and B.dtype == np.float32):
-                raise LoweringError("f32 matmul with non-f32 inputs")
-            if not f32 and not (A.dtype == B.dtype == target.dtype and
-                                A.dtype in (np.float64, np.int64)):
+            if A.dtype != B.dtype or (in_dt is not None and A.dtype != in_dt):
                 raise LoweringError(f"matmul of {A.dtype} x {B.dtype} -> {target.dtype} is not lowered "
-                                    "(f32, f64 and int64 only)")
+                                    "(operands of one dtype only)")
+            in_dt = A.dtype
+            if A.dtype not in (np.float32, np.float64, np.int64, ir.bfloat16):
+                raise LoweringError(f"matmul of {A.dtype} is not lowered (f32, bf16, f64, int64)")
             am, ak = A.chunk_extent(a_key[1:])
             bk, bn = B.chunk_extent(b_key[1:])
             if ak != bk:
                 raise LoweringError("contracted chunk extents differ")
-            rows[i] = (A.chunk_addr(a_key[1:]), B.chunk_addr(b_key[1:]), target.chunk_addr(key),
-                       am, bn, ak, ak, bn, bn, 0)
-            max_m, max_n = max(max_m, am), max(max_n, bn)
-        code = ir.dtype_code(np.float32 if f32 else target.dtype)
-        return GemmLaunch(rows, code, max_m, max_n, self.device)
+            segs[i] = (A.chunk_addr(a_key[1:]), B.chunk_addr(b_key[1:]), ak, ak, bn, 0)
+            tasks[i] = (target.chunk_addr(key), am, bn, bn, i, 1, ak, 0)
+        return GemmLaunch(tasks, segs, ir.dtype_code(in_dt or target.dtype), ir.dtype_code(target.dtype),
+                          self.device, self.zero_page())
+
+    def zero_page(self) -> int:
+        """Device address of 4 KiB of zeros (k past a GEMM chain's end)."""
+        import torch
+
+        from ...storage import _GEOMETRY_ONLY
+
+        if _GEOMETRY_ONLY[0]:
+            return 0
+        z = getattr(self, "_zero", None)
+        if z is None:
+            z = self._zero = torch.zeros(4096, dtype=torch.uint8, device=self.device)
+        return (z.data_ptr() + 255) // 256 * 256
 
     # -- execution -------------------------------------------------------------
     def compiled(self, name, node):
@@ -620,8 +635,12 @@ class GpuDagExecutor(DagExecutor):
         if entry is not None and entry[0]() is dag:
             return entry[1]
         from ...chains import find_chains
+        from ...gemm_chains import find_gemm_chains
 
-        chains = find_chains(dag, array_names) if self.fuse_reductions else {}
+        chains = find_gemm_chains(dag, array_names) if self.fuse_gemm_sums else {}
+        taken = {m for ch in chains.values() for m in ch.nodes}
+        if self.fuse_reductions:
+            chains.update(find_chains(dag, array_names, exclude=taken))
         members = {}
         nodes = dict(dag.nodes(data=True))
         for first, ch in chains.items():
@@ -633,10 +652,17 @@ class GpuDagExecutor(DagExecutor):
                     t = nodes[out].get("target")
                     if isinstance(t, DeviceArray):
                         self.elided.add(id(t))
+            for t in getattr(ch, "extra_targets", ()):
+                if t is not ch.final_target:
+                    self.elided.add(id(t))
         self._chains[key] = (weakref.ref(dag), (chains, members))
         return chains, members
 
     def compiled_chain(self, chain):
+        from ...gemm_chains import GemmChain
+
+        if isinstance(chain, GemmChain):
+            return self.compiled_gemm_chain(chain)
         entry = self._cache.get(("chain", id(chain.first_spec)))
         if entry is not None and entry[0]() is chain.first_spec:
             return entry[1]
@@ -656,6 +682,48 @@ class GpuDagExecutor(DagExecutor):
         launches = _with_gathers(launch, self.device)
         self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
         return launches
+
+    def compiled_gemm_chain(self, chain):
+        """matmul's chunk products + k-sum as ONE cubed_gemm_chain launch
+        (gemm_chains.py); with several GPUs each rank computes the output
+        chunks it owns, after fetching the A row / B column chunks it lacks."""
+        from ...gemm_chains import K_AXIS, chain_tables
+
+        key = ("gemm", id(chain.first_spec))
+        entry = self._cache.get(key)
+        if entry is not None and entry[0]() is chain.first_spec:
+            return entry[1]
+        F = chain.final_target
+        self.allocate(F)
+        keys = self._task_keys(F)
+        out = []
+        if self.world > 1:
+            def reads(k):
+                G = chain.gemm_target
+                res = []
+                for kk in range(G.numblocks[K_AXIS]):
+                    args = chain.gemm_spec.block_function(("out", k[0], kk, k[-1]))
+                    for a in args[:2]:
+                        src = self.device_source(chain.gemm_spec.reads_map[a[0]].array)
+                        if isinstance(src, DeviceArray) and src.world > 1:
+                            res.append((src, tuple(a[1:]), None))
+                return res
+
+            fetch, arrays = self._plan_fetch({k: F.owner(k) for k in keys}, reads)
+            owned = [k for k in keys if F.owner(k) == self.rank]
+            if fetch is not None:
+                out.append(fetch)
+            with _remote_chunks(fetch, arrays):
+                tasks, segs, in_dt, out_dt = chain_tables(self, chain, owned)
+        else:
+            tasks, segs, in_dt, out_dt = chain_tables(self, chain, keys)
+        in_dt = in_dt if in_dt is not None else out_dt
+        if in_dt not in (np.float32, np.float64, np.int64, ir.bfloat16):
+            raise LoweringError(f"matmul of {in_dt} is not lowered (f32, bf16, f64, int64)")
+        out.append(GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
+                              self.zero_page()))
+        self._cache[key] = (weakref.ref(chain.first_spec), out)
+        return out
 
     def _compiled_chain_dist(self, chain, target, keys):
         """A reduction chain over chunks spread across the ranks: each rank
@@ -725,10 +793,10 @@ class GpuDagExecutor(DagExecutor):
         stream = self.stream
         dag = self.exec_dag(dag, array_names)
         nodes = dict(dag.nodes(data=True))
+        chains, members = self.chains_of(dag, array_names)
         if self.check_memory:
             self._check_hbm(dag)
         timing = self.timing
-        chains, members = self.chains_of(dag, array_names)
         for name, node in visit_nodes(dag, resume=resume):
             t0 = time.time()
             if name in members:
@@ -749,6 +817,7 @@ class GpuDagExecutor(DagExecutor):
                         self._agreed.add((name, id(ch)))
                         if not ok:
                             self._cache.pop(("chain", id(ch.first_spec)), None)
+                        self._cache.pop(("gemm", id(ch.first_spec)), None)
                     if not ok:
                         # not fusable after all: run the chain's pipelines one by one
                         chains.pop(name)
@@ -760,6 +829,8 @@ class GpuDagExecutor(DagExecutor):
                                 if isinstance(t, DeviceArray):
                                     self.elided.discard(id(t))
                                     self.allocate(t)
+                        for t in getattr(ch, "extra_targets", ()):
+                            self.elided.discard(id(t))
                         launches = self.compiled(name, node)
             else:
                 launches = self.compiled(name, node)

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 5
+#define CUBED_ABI_VERSION 6
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -318,6 +318,46 @@ typedef struct {
 int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntasks,
                       int32_t dtype, int64_t max_m, int64_t max_n,
                       void* stream);
+
+/* Chained chunk GEMMs (blockwise matmul / tensordot with the k-sum fused):
+ * task t computes C_t (=|+=) sum over its segments s of A_s @ B_s, row-major
+ * views, every A_s m x k_s, every B_s k_s x n, accumulated in one continuous
+ * K loop (f32 for f32/bf16 inputs, f64 / wrapping int64 otherwise) and
+ * rounded to out_dtype once.  Replaces, per OUTPUT chunk, the (i, k, j)
+ * tasks of _matmul (cubed/array_api/linear_algebra_functions.py:35-52,62-64:
+ * one numpy BLAS call per chunk pair) together with the _sum_wo_cat
+ * reduction over k (:52,67-78) that reads their partial products back; a
+ * per-chunk product is a chain of one segment.  Host copies of both tables
+ * (tasks, segs) are validated and pick the kernel; the device copies are
+ * what the kernels read.  d_zero: >= 64 zero bytes of device memory (the
+ * bf16 path reads k past the chain's end from it).  path: CUBED_GEMM_AUTO,
+ * or CUBED_GEMM_ANY to force the element-wise kernel (tests). */
+typedef struct {
+  int64_t c;            /* output chunk base (device byte address)           */
+  int64_t m, n, ldc;    /* output extents and row pitch (elements)           */
+  int64_t seg0, nseg;   /* segments [seg0, seg0 + nseg) of the segment table  */
+  int64_t ktot;         /* sum of the segments' k                            */
+  int64_t accumulate;   /* 1: C += ..., 0: C = ...                           */
+} cubed_gemm_chain_t;
+
+typedef struct {
+  int64_t a, b;         /* device byte addresses of A_s (m x k) and B_s (k x n) */
+  int64_t k;            /* contracted extent of this pair                      */
+  int64_t lda, ldb;     /* row pitches in elements                             */
+  int64_t pad;
+} cubed_gemm_seg_t;
+
+#define CUBED_GEMM_AUTO (-1)
+#define CUBED_GEMM_ANY 0   /* element-wise tiles, any dtype and shape          */
+#define CUBED_GEMM_MFMA 1  /* bf16 (16x16x32) / f32 (32x32x2) MFMA tiles       */
+
+/* Kernel the chain set would run on (CUBED_GEMM_MFMA or CUBED_GEMM_ANY). */
+int cubed_gemm_chain_path(const cubed_gemm_chain_t* tasks, int64_t ntasks,
+                          const cubed_gemm_seg_t* segs, int32_t in_dtype, int32_t out_dtype);
+int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
+                     int64_t ntasks, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
+                     int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
+                     int32_t path, void* stream);
 
 /* library info */
 /* Plain chunk GEMMs through rocBLAS (cubed_amd/csrc/blas.hip): ``batch``

@@ -1,0 +1,216 @@
+"""Chained chunk GEMMs (matmul / tensordot, BASELINE config 5) on the MI355X.
+
+``xp.matmul`` keeps the reference's plan -- (i, k, j) chunk products then a
+sum over k (cubed/array_api/linear_algebra_functions.py:13-78) -- and the
+executor runs it as ONE ``cubed_gemm_chain`` launch per matmul (the k-sum
+fused into the K loop, cubed_amd/gemm_chains.py).  These tests check that
+launch, its kernels (the bf16 16x16x32 and f32 32x32x2 MFMA tiles, the
+element-wise fallback) and the unfused per-chunk form against an f64 product
+of the SAME (dtype-rounded) inputs.
+
+Parity: numpy's f32 matmul (BLAS) and the reference's k-chunk f32 sums have
+their own summation order, so f32 results are compared with an error bound,
+not bit for bit.  bf16 has no reference dtype (cubed/array_api/dtypes.py
+:14-37): "parity unpinned" -- the check is the bound alone.
+
+Bounds (written per test): an f32 accumulation of K products of magnitude
+sum |a||b| = S has error <= K * 2^-24 * S (gamma_K); in practice the error
+grows like sqrt(K), so the tests use the tighter 8 * sqrt(K) * 2^-24 * S
+(checked to hold with a wide margin at K = 40000) plus, for bf16 outputs, the
+final rounding of the result to bf16 (2^-9 relative).
+"""
+
+import numpy as np
+import pytest
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.lowering as L
+from cubed_amd import _native as nat
+from cubed_amd import ir
+
+pytestmark = pytest.mark.gpu
+
+U = 2.0 ** -24
+
+
+@pytest.fixture()
+def ex(gpu_executor):
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor, LaunchTimer
+
+    e = GpuDagExecutor("cuda:0")
+    e.timing = LaunchTimer()
+    return e
+
+
+def _launches(ex, cls=L.GemmLaunch):
+    out = []
+    for lst in ex._cache.values():
+        for l in lst[1]:
+            if isinstance(l, cls):
+                out.append(l)
+    return out
+
+
+def _bf16_round(x):
+    return ir.bf16_to_numpy(ir.numpy_to_bf16(x))
+
+
+def _operands(shape_a, shape_b, seed, signed=True):
+    r = np.random.default_rng(seed)
+    x = r.random(shape_a, dtype=np.float64)
+    y = r.random(shape_b, dtype=np.float64)
+    if signed:
+        x, y = x - 0.5, y - 0.5
+    return x.astype(np.float32), y.astype(np.float32)
+
+
+def _check_bound(got, x64, y64, K, out_bf16=False, factor=8.0):
+    exp = x64 @ y64
+    scale = np.abs(x64) @ np.abs(y64)
+    bound = factor * np.sqrt(K) * U * scale
+    if out_bf16:
+        bound = bound + 2.0 ** -8 * np.abs(exp)
+    err = np.abs(got.astype(np.float64) - exp)
+    worst = float(np.max(err / np.maximum(bound, 1e-300)))
+    assert np.all(err <= bound), f"max err / bound = {worst}"
+    return worst
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_chained_matmul_k40000(ex, dt):
+    """K = 40000 in 8 chunks of 5000 (config 5's K and chunking; 5000 is not
+    a multiple of the 64-deep K tile, so segment boundaries fall inside
+    tiles), ragged M/N edge chunks and tiles; one launch, MFMA path."""
+    x, y = _operands((296, 40000), (40000, 264), 7)
+    spec = cubed.Spec(allowed_mem="20GB", executor=ex)
+    a = cubed.from_array(x, chunks=(150, 5000), spec=spec)
+    b = cubed.from_array(y, chunks=(5000, 136), spec=spec)
+    if dt == "bf16":
+        a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
+        x64, y64 = _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64)
+    else:
+        x64, y64 = x.astype(np.float64), y.astype(np.float64)
+    m = xp.matmul(a, b)
+    assert m.dtype == (ir.bfloat16 if dt == "bf16" else np.float32)
+    got = m.compute()
+    assert got.dtype == np.float32  # bf16 results come back widened exactly to f32
+    gl = _launches(ex)
+    assert len(gl) == 1 and gl[0].kernel_path() == nat.GEMM_MFMA
+    assert all(int(t["nseg"]) == 8 and int(t["ktot"]) == 40000 for t in gl[0].tasks)
+    _check_bound(got, x64, y64, 40000, out_bf16=(dt == "bf16"))
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_mfma_path_equals_element_path_bound(ex, dt, monkeypatch):
+    """The same chain through the element-wise kernel (forced): both within
+    the bound; for bf16 inputs every product is exact in f32, so the two
+    kernels differ only by summation order."""
+    x, y = _operands((200, 640), (640, 136), 3)
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    res = {}
+    for path in (nat.GEMM_MFMA, nat.GEMM_ANY):
+        monkeypatch.setattr(L.GemmLaunch, "__init__", _forced_path_init(path))
+        from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+        e = GpuDagExecutor("cuda:0")
+        spec = cubed.Spec(allowed_mem="2GB", executor=e)
+        a = cubed.from_array(x, chunks=(100, 128), spec=spec)
+        b = cubed.from_array(y, chunks=(128, 136), spec=spec)
+        if dt == "bf16":
+            a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
+        res[path] = xp.matmul(a, b).compute()
+        assert _launches(e)[0].kernel_path() == path
+    rnd = _bf16_round if dt == "bf16" else (lambda v: v)
+    for got in res.values():
+        _check_bound(got, rnd(x).astype(np.float64), rnd(y).astype(np.float64), 640,
+                     out_bf16=(dt == "bf16"))
+
+
+_orig_init = L.GemmLaunch.__init__
+
+
+def _forced_path_init(path):
+    def init(self, tasks, segs, in_code, out_code, device, zero_ptr, path_=None):
+        _orig_init(self, tasks, segs, in_code, out_code, device, zero_ptr, path=path)
+    return init
+
+
+def test_ragged_k_takes_element_path(ex):
+    """A last k chunk shorter than the 64-deep K tile: the element kernel
+    (auto-selected), still exact to the bound."""
+    x, y = _operands((130, 300), (300, 72), 5)
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    a = xp.astype(cubed.from_array(x, chunks=(64, 130), spec=spec), xp.bfloat16)
+    b = xp.astype(cubed.from_array(y, chunks=(130, 72), spec=spec), xp.bfloat16)
+    got = xp.matmul(a, b).compute()
+    assert _launches(ex)[0].kernel_path() == nat.GEMM_ANY
+    _check_bound(got, _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64), 300,
+                 out_bf16=True)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_unfused_per_chunk_products(ex, dt):
+    """With the k-sum fusion off, every (i, k, j) task is a one-segment chain
+    writing its partial product, then the reference's sum reduction runs:
+    the reference's own plan, same bound (+ the bf16 rounding of each
+    partial for bf16)."""
+    ex.fuse_gemm_sums = False
+    x, y = _operands((256, 512), (512, 128), 9)
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    a = cubed.from_array(x, chunks=(128, 128), spec=spec)
+    b = cubed.from_array(y, chunks=(128, 128), spec=spec)
+    if dt == "bf16":
+        a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
+        x64, y64 = _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64)
+    else:
+        x64, y64 = x.astype(np.float64), y.astype(np.float64)
+    got = xp.matmul(a, b).compute()
+    gl = _launches(ex)
+    assert len(gl) == 1 and all(int(t["nseg"]) == 1 for t in gl[0].tasks) and gl[0].n == 2 * 4 * 1
+    if dt == "bf16":
+        exp = x64 @ y64
+        scale = np.abs(x64) @ np.abs(y64)
+        # 4 partials each rounded to bf16 (2^-9 relative of the partial's scale) + the final rounding
+        assert np.all(np.abs(got - exp) <= 5 * 2.0 ** -8 * scale)
+    else:
+        _check_bound(got, x64, y64, 512)
+
+
+def test_matmul_int64_exact(ex):
+    r = np.random.default_rng(4)
+    x = r.integers(-50, 50, (90, 130)).astype(np.int64)
+    y = r.integers(-50, 50, (130, 70)).astype(np.int64)
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    got = xp.matmul(cubed.from_array(x, chunks=(40, 60), spec=spec),
+                    cubed.from_array(y, chunks=(60, 30), spec=spec)).compute()
+    assert got.dtype == np.int64 and np.array_equal(got, x @ y)
+
+
+def test_matmul_f64_bound(ex):
+    r = np.random.default_rng(6)
+    x = r.random((100, 700)) - 0.5
+    y = r.random((700, 90)) - 0.5
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    got = xp.matmul(cubed.from_array(x, chunks=(64, 200), spec=spec),
+                    cubed.from_array(y, chunks=(200, 64), spec=spec)).compute()
+    exp = x @ y
+    scale = np.abs(x) @ np.abs(y)
+    assert got.dtype == np.float64
+    assert np.all(np.abs(got - exp) <= 700 * 2.0 ** -53 * scale)
+
+
+def test_bf16_astype_round_trip(ex):
+    """astype to bf16 rounds to nearest even (ties, inf, overflow, subnormals
+    as torch does; NaN stays NaN); back to f32 it is exact."""
+    import torch
+
+    v = np.array([1.0, 1.00390625, 1.01171875, -3.14159, 2.5e-3, np.nan, np.inf, -np.inf, 3.4e38,
+                  1e-40, 0.0, -0.0] * 11, dtype=np.float32)
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    a = cubed.from_array(v, chunks=(50,), spec=spec)
+    got = xp.astype(xp.astype(a, xp.bfloat16), xp.float32).compute()
+    exp = torch.from_numpy(v).to(torch.bfloat16).float().numpy()
+    nan = np.isnan(exp)
+    assert np.array_equal(np.isnan(got), nan)  # NaN payloads differ (torch: 0xFFFF), NaN-ness not
+    assert np.array_equal(got[~nan].view(np.uint32), exp[~nan].view(np.uint32))

@@ -327,3 +327,52 @@ def test_copy_launch_picks_flat_path_for_packed_destinations(monkeypatch):
     assert CopyLaunch([strided], 8, "cpu").path == nat.COPY_ROWS
     monkeypatch.setenv("CUBED_AMD_COPY_FLAT", "0")
     assert CopyLaunch([packed], 8, "cpu").path == nat.COPY_ROWS
+
+
+def test_matmul_and_k_sum_are_one_chained_gemm(built, dry):
+    """xp.matmul's (i, k, j) chunk products and its sum over k lower to ONE
+    cubed_gemm_chain launch: a task per output chunk whose segments are the
+    (A_ik, B_kj) pairs in k order; the (M, nk, N) partials are never
+    allocated (gemm_chains.py)."""
+    from cubed_amd.lowering import GemmLaunch
+
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(3)
+    A = xp.astype(crandom.random((400, 1024), chunks=(100, 256), spec=spec), xp.bfloat16)
+    B = xp.astype(crandom.random((1024, 312), chunks=(256, 104), spec=spec), xp.bfloat16)
+    arrays_to_plan(A, B).execute(executor=dry, array_names=[A.name, B.name])
+    dry.launched.clear()
+    m = xp.matmul(A, B)
+    assert m.dtype == xp.bfloat16
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    assert [type(l).__name__ for l in dry.launched] == ["GemmLaunch"]
+    g = dry.launched[0]
+    assert g.n == 4 * 3 and all(int(t["nseg"]) == 4 and int(t["ktot"]) == 1024 for t in g.tasks)
+    assert (g.in_code, g.out_code) == (12, 12)
+    assert g.kernel_path() == nat.GEMM_MFMA
+    # segments of task (i, j) walk k in order over A's row i and B's column j
+    t0 = g.tasks[0]
+    seg = g.segs[int(t0["seg0"]):int(t0["seg0"]) + 4]
+    assert [int(s["k"]) for s in seg] == [256] * 4
+    assert len({int(s["a"]) for s in seg}) == 4 and len({int(s["b"]) for s in seg}) == 4
+
+
+def test_matmul_without_k_sum_fusion_is_per_chunk(built, dry):
+    dry.fuse_gemm_sums = False
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    a = cubed.from_array(np.ones((64, 96), np.float32), chunks=(32, 32), spec=spec)
+    b = cubed.from_array(np.ones((96, 64), np.float32), chunks=(32, 32), spec=spec)
+    m = xp.matmul(a, b)
+    arrays_to_plan(m).execute(executor=dry, array_names=[m.name])
+    kinds = [type(l).__name__ for l in dry.launched]
+    assert kinds[0] == "GemmLaunch" and "FusedLaunch" in kinds
+    g = dry.launched[0]
+    assert g.n == 2 * 3 * 2 and all(int(t["nseg"]) == 1 for t in g.tasks)
+
+
+def test_bfloat16_promotion():
+    assert xp.result_type(xp.bfloat16, xp.bfloat16) == xp.bfloat16
+    assert xp.result_type(xp.bfloat16, xp.float32) == xp.float32
+    assert xp.result_type(xp.float64, xp.bfloat16) == xp.float64
+    with pytest.raises(TypeError):
+        xp.result_type(xp.bfloat16, xp.int32)

@@ -71,6 +71,9 @@ int main(void) {
   P(cubed_task_t, out_stride); P(cubed_task_t, key_lo); P(cubed_task_t, block_offset);
   P(cubed_box_t, src_stride); P(cubed_box_t, dst_stride);
   P(cubed_gemm_task_t, ldc); P(cubed_gemm_task_t, accumulate);
+  S(cubed_gemm_chain_t); S(cubed_gemm_seg_t);
+  P(cubed_gemm_chain_t, seg0); P(cubed_gemm_chain_t, ktot); P(cubed_gemm_chain_t, accumulate);
+  P(cubed_gemm_seg_t, k); P(cubed_gemm_seg_t, ldb);
   return 0;
 }
 """
@@ -108,6 +111,46 @@ def test_struct_layouts_match_binding(c_layout):
     assert nat.GEMM_DTYPE.itemsize == c_layout["cubed_gemm_task_t"]
     for f in ("ldc", "accumulate"):
         assert nat.GEMM_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_task_t.{f}"], f
+    assert nat.CHAIN_DTYPE.itemsize == c_layout["cubed_gemm_chain_t"]
+    for f in ("seg0", "ktot", "accumulate"):
+        assert nat.CHAIN_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_chain_t.{f}"], f
+    assert nat.SEG_DTYPE.itemsize == c_layout["cubed_gemm_seg_t"]
+    for f in ("k", "ldb"):
+        assert nat.SEG_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_seg_t.{f}"], f
+
+
+def _chain(m, n, ks, lda=None, ldb=None, align=0):
+    from cubed_amd import _native as nat
+
+    segs = np.zeros(len(ks), dtype=nat.SEG_DTYPE)
+    for i, k in enumerate(ks):
+        segs[i] = (4096 * (i + 1) + align, 1 << 20, k, lda or k, ldb or n, 0)
+    tasks = np.zeros(1, dtype=nat.CHAIN_DTYPE)
+    tasks[0] = (1 << 24, m, n, n, 0, len(ks), sum(ks), 0)
+    return tasks, segs
+
+
+@pytest.mark.parametrize("case,in_dt,out_dt,expect", [
+    (dict(m=5000, n=5000, ks=[5000] * 8), "bf16", "bf16", 1),    # config 5, bf16
+    (dict(m=5000, n=5000, ks=[5000] * 8), "bf16", "f32", 1),
+    (dict(m=5000, n=5000, ks=[5000] * 8), "f32", "f32", 1),      # config 5, f32
+    (dict(m=100, n=100, ks=[100, 60]), "bf16", "bf16", 0),       # a segment shorter than BK=64
+    (dict(m=100, n=100, ks=[100, 100]), "f32", "f32", 1),         # f32: BK = 32
+    (dict(m=100, n=101, ks=[104]), "bf16", "bf16", 0),           # ragged n: no 16-B rows
+    (dict(m=100, n=96, ks=[100]), "bf16", "bf16", 0),            # k % 8 != 0
+    (dict(m=100, n=96, ks=[104], align=8), "bf16", "bf16", 0),   # operand not 16-B aligned
+    (dict(m=64, n=64, ks=[64]), "f64", "f64", 0),                # f64 / int64: element kernel
+])
+def test_gemm_chain_path_selection(built, case, in_dt, out_dt, expect):
+    """cubed_gemm_chain_path is pure host logic: which kernel a chain set
+    would take (the MFMA tiles' alignment / segment-length preconditions)."""
+    from cubed_amd import _native as nat
+
+    codes = {"bf16": 12, "f32": 9, "f64": 10}
+    tasks, segs = _chain(case["m"], case["n"], case["ks"], align=case.get("align", 0))
+    got = nat.lib().cubed_gemm_chain_path(tasks.ctypes.data, len(tasks), segs.ctypes.data,
+                                          codes[in_dt], codes[out_dt])
+    assert got == expect
 
 
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
