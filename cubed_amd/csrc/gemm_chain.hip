@@ -15,10 +15,10 @@
 //   k_gemm_bf16_chain  bf16 x bf16 -> f32 accumulate (-> f32 / bf16 out) on
 //                      v_mfma_f32_16x16x32_bf16.  256 x 256 output tile per
 //                      512-thread workgroup (8 waves, 2 (M) x 4 (N), each
-//                      128 x 64 = 8 x 4 accumulators), K staged 64 deep
+//                      128 x 64 = 8 x 4 accumulators), K staged 32 deep
 //                      straight from HBM into LDS with global_load_lds
-//                      (16 B per lane, double buffered: the next K tile is in
-//                      flight while the current one feeds the MFMAs).
+//                      (16 B per lane) through a 4-slot ring: three K steps
+//                      in flight while the fourth feeds the MFMAs.
 //                      A is staged k-contiguous [m][64] (XOR-swizzled 16-B
 //                      chunks, conflict-free ds_read_b128 fragments); B is
 //                      staged as it lies in HBM, [k][256] rows, and read
@@ -43,6 +43,7 @@ using namespace cubed;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 #define CUBED_L __attribute__((address_space(3)))
 
@@ -76,9 +77,16 @@ __device__ __forceinline__ bool tile_of(int64_t g, int64_t tiles_m, int64_t tile
 }
 
 // ------------------------------------------------------------------ bf16 MFMA
-constexpr int HB_BM = 256, HB_BN = 256, HB_BK = 64;
-constexpr int HB_A = HB_BM * HB_BK * 2;   // 32 KiB: [256 rows][128 B]
-constexpr int HB_B = HB_BK * HB_BN * 2;   // 32 KiB: [64 k-rows][512 B]
+// LDS is a ring of HB_NS slots, each one 32-deep K step of the 256x256 tile:
+// A [256 rows][32 k] (64-B rows) + B [32 k-rows][256 n] (512-B rows).  The
+// loads of step p+3 are issued right after the barrier of step p, so three
+// steps (96 KiB per CU) are always in flight; the wait for a step is a
+// counted vmcnt (4 global_load_lds per wave per step), never vmcnt(0) in the
+// steady state, and the barrier is a raw s_barrier (a __syncthreads() would
+// drain every LDS-DMA in flight).
+constexpr int HB_BM = 256, HB_BN = 256, HB_BK = 32, HB_NS = 4;
+constexpr int HB_A = HB_BM * HB_BK * 2;   // 16 KiB
+constexpr int HB_B = HB_BK * HB_BN * 2;   // 16 KiB
 constexpr int HB_STAGE = HB_A + HB_B;
 
 struct Seg {  // wave-uniform view of one segment
@@ -105,7 +113,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
                                                          const cubed_gemm_seg_t* __restrict__ segs,
                                                          int64_t tiles_m, int64_t tiles_n,
                                                          const char* __restrict__ zero) {
-  __shared__ __attribute__((aligned(1024))) char lds_[2 * HB_STAGE];
+  __shared__ __attribute__((aligned(1024))) char lds_[HB_NS * HB_STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
   tile_of<HB_BM, HB_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
@@ -119,80 +127,88 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   const int wr = w >> 2, wc = w & 3;
 
   // ---- per-lane staging geometry (constant over the K loop)
-  // A: wave w stages rows 8*(4w+i) + lane>>3 (i = 0..3), 16-B chunk lane&7 of
-  // the LDS row holds global chunk (lane&7) ^ ((row>>1)&7).
-  int64_t gmA[4];
-  int dA[2];
+  // A: wave w stages rows 16*(2w+i) + lane>>2 (i = 0, 1); 16-B chunk lane&3 of
+  // the 64-B LDS row holds global chunk (lane&3) ^ 2*((row>>3)&1)
+  // [(row>>3)&1 = (lane>>5)&1], which makes the fragment reads conflict-free.
+  int64_t gmA[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t r = 8 * (4 * w + i) + (lane >> 3);
+  for (int i = 0; i < 2; ++i) {
+    const int64_t r = 16 * (2 * w + i) + (lane >> 2);
     gmA[i] = (m0 + r < M ? m0 + r : M - 1);
   }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) dA[p] = 8 * ((lane & 7) ^ (4 * p + (lane >> 4)));
-  // B: wave w stages k-rows 2*(4w+i) + lane>>5, 16-B chunk c = lane&31 of the
+  const int dA = 8 * ((lane & 3) ^ (2 * ((lane >> 5) & 1)));
+  // B: wave w stages k-rows 2*(2w+i) + lane>>5; 16-B chunk c = lane&31 of the
   // LDS row holds global chunk c ^ swz(row), swz(r) = 2*((r&3) | ((r>>3)&1)<<2).
-  int rB[4];
-  int64_t gnB[4];
+  int rB[2];
+  int64_t gnB[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = 2 * (4 * w + i) + (lane >> 5);
+  for (int i = 0; i < 2; ++i) {
+    const int r = 2 * (2 * w + i) + (lane >> 5);
     rB[i] = r;
     const int swz = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
     int64_t n = n0 + 8 * ((lane & 31) ^ swz);
     gnB[i] = (n + 8 <= N ? n : N - 8);
   }
 
-  // ---- wave-uniform segment state
+  // ---- wave-uniform segment state (the segment containing the next step to stage)
   int64_t s = seg0, ks = 0;
   Seg cur = load_seg(segs, s);
   int64_t ke = segs[s].k;
 
-  // issue the global->LDS loads of K tile starting at k0 into stage buffer
-  auto stage = [&](int64_t k0, CUBED_L char* buf) {
-    const bool inside = k0 + HB_BK <= ke;  // uniform: no boundary in this tile
-    Seg nxt;
-    bool has_next = false;
-    if (!inside) {
-      has_next = s + 1 < segN;
-      if (has_next) nxt = load_seg(segs, s + 1);
-    }
+  // per-lane byte offsets of this lane's 4 pieces inside the current segment
+  // (recomputed only when the segment changes)
+  int64_t offSA[2], offSB[2];
+  auto seg_offsets = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t kk = k0 + dA[i & 1];
-      const char* src;
-      if (inside || kk < ke) src = cur.a + gmA[i] * cur.lda2 + (kk - ks) * 2;
-      else if (has_next && kk < KT) src = nxt.a + gmA[i] * nxt.lda2 + (kk - ke) * 2;
-      else src = zero;
-      glds16(src, buf + (4 * w + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t kk = k0 + rB[i];
-      const char* src;
-      if (inside || kk < ke) src = cur.b + (kk - ks) * cur.ldb2 + gnB[i] * 2;
-      else if (has_next && kk < KT) src = nxt.b + (kk - ke) * nxt.ldb2 + gnB[i] * 2;
-      else src = zero;
-      glds16(src, buf + HB_A + (4 * w + i) * 1024);
+    for (int i = 0; i < 2; ++i) {
+      offSA[i] = gmA[i] * cur.lda2 + dA * 2;
+      offSB[i] = rB[i] * cur.ldb2 + gnB[i] * 2;
     }
   };
-  // after staging tile k0: move to the next segment if the next tile starts in it
-  auto advance = [&](int64_t k0next) {
-    if (k0next >= ke && s + 1 < segN) {
+  seg_offsets();
+
+  // issue the 4 global->LDS loads of the K step starting at k0 into slot buf
+  auto stage = [&](int64_t k0, CUBED_L char* buf) {
+    const char* a0 = cur.a + (k0 - ks) * 2;        // uniform
+    const char* b0 = cur.b + (k0 - ks) * cur.ldb2;  // uniform
+    const char* sa[2];
+    const char* sb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      sa[i] = a0 + offSA[i];
+      sb[i] = b0 + offSB[i];
+    }
+    if (k0 + HB_BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
+      const bool has_next = s + 1 < segN;
+      const Seg nxt = load_seg(segs, has_next ? s + 1 : s);
+      const int64_t ka = k0 + dA;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* na = nxt.a + gmA[i] * nxt.lda2 + (ka - ke) * 2;
+        sa[i] = ka < ke ? sa[i] : ((has_next && ka < KT) ? na : zero);
+        const int64_t kb = k0 + rB[i];
+        const char* nbp = nxt.b + (kb - ke) * nxt.ldb2 + gnB[i] * 2;
+        sb[i] = kb < ke ? sb[i] : ((has_next && kb < KT) ? nbp : zero);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(sa[i], buf + (2 * w + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(sb[i], buf + HB_A + (2 * w + i) * 1024);
+    // the next step to stage starts at k0 + HB_BK: move on if it is in the next segment
+    if (k0 + HB_BK >= ke && s + 1 < segN) {
       ks = ke;
       ++s;
       cur = load_seg(segs, s);
       ke = ks + segs[s].k;
+      seg_offsets();
     }
   };
 
-  // ---- per-lane LDS read offsets
-  // A fragment (mb, kstep): row wr*128 + mb*16 + (lane&15), chunk (4*kstep + lane>>4) ^ ((lane>>1)&7)
-  int offA[2];
-#pragma unroll
-  for (int k2 = 0; k2 < 2; ++k2)
-    offA[k2] = wr * 16384 + (lane & 15) * 128 + 16 * ((4 * k2 + (lane >> 4)) ^ ((lane >> 1) & 7));
-  // B fragment (nb, kstep, half): row 32*kstep + 8g + 4*half + q, chunk (8wc + 2nb + (p>>1)) ^ swz
+  // ---- per-lane LDS read offsets (within a slot)
+  // A fragment mb: row wr*128 + mb*16 + (lane&15), chunk (lane>>4) ^ 2*((lane>>3)&1)
+  const int offA = wr * 8192 + (lane & 15) * 64 + 16 * ((lane >> 4) ^ (2 * ((lane >> 3) & 1)));
+  // B fragment (nb, half): row 8g + 4*half + q, chunk (8wc + 2nb + (p>>1)) ^ swz
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int swzq = 2 * (q | ((g & 1) << 2));
   int offB[4];
@@ -206,35 +222,44 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int64_t nkt = (KT + HB_BK - 1) / HB_BK;
-  stage(0, lds);
-  advance(HB_BK);
-  __syncthreads();
-  for (int64_t kt = 0; kt < nkt; ++kt) {
-    CUBED_L char* bufc = lds + (kt & 1) * HB_STAGE;
-    if (kt + 1 < nkt) {
-      stage((kt + 1) * HB_BK, lds + ((kt + 1) & 1) * HB_STAGE);
-      advance((kt + 2) * HB_BK);
+  const int64_t nst = (KT + HB_BK - 1) / HB_BK;
+  // prologue: steps 0, 1, 2 in flight
+  for (int64_t p = 0; p < 3 && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
+  for (int64_t p = 0; p < nst; ++p) {
+    // this wave's loads of step p have landed once at most the younger
+    // steps' loads (4 per step) are outstanding
+    const int64_t younger = nst - 1 - p;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every wave's step p landed; every wave finished reading step p-1's slot
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
+    const CUBED_L char* bufc = lds + (p & (HB_NS - 1)) * HB_STAGE;
+    // B fragments by transposed reads.  Inline asm: the builtin has no memory
+    // operand, so hipcc would put an s_waitcnt vmcnt(0) in front of it --
+    // draining the three K steps in flight -- and the reads only touch slot
+    // p, which the vmcnt + barrier above already made visible.
+    bf16x8 bf[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
+      s16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(pb));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(pb));
+      bf[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      bf16x8 bf[4];
+    for (int mb = 0; mb < 8; ++mb) {
+      const bf16x8 af = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const CUBED_L char* p = bufc + offB[nb] + k2 * 32 * 512;
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CUBED_L bf16x4*)p);
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((CUBED_L bf16x4*)(p + 4 * 512));
-        bf[nb] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-        const bf16x8 af = *(const CUBED_L bf16x8*)(bufc + offA[k2] + mb * 2048);
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);
-      }
+      for (int nb = 0; nb < 4; ++nb)
+        acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);
     }
-    __syncthreads();
   }
 
   // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
@@ -488,8 +513,8 @@ bool aligned16(int64_t x) { return (x & 15) == 0; }
 }  // namespace
 
 // Which kernel serves a chain set (host tables): the MFMA fast paths need
-// every segment's k a multiple of 8 (bf16) / 4 (f32) and >= the K tile
-// (64 / 32), 16-B aligned operand rows, and (bf16) n a multiple of 8.
+// every segment's k a multiple of 8 (bf16) / 4 (f32) and >= the K step
+// (32), 16-B aligned operand rows, and (bf16) n a multiple of 8.
 extern "C" int cubed_gemm_chain_path(const cubed_gemm_chain_t* tasks, int64_t ntasks,
                                      const cubed_gemm_seg_t* segs, int32_t in_dtype,
                                      int32_t out_dtype) {
@@ -499,7 +524,7 @@ extern "C" int cubed_gemm_chain_path(const cubed_gemm_chain_t* tasks, int64_t nt
       if (T.n < 8 || T.n % 8 || T.m < 1) return CUBED_GEMM_ANY;
       for (int64_t i = T.seg0; i < T.seg0 + T.nseg; ++i) {
         const cubed_gemm_seg_t& s = segs[i];
-        if (s.k < 64 || s.k % 8 || s.lda % 8 || s.ldb % 8 || !aligned16(s.a) || !aligned16(s.b))
+        if (s.k < 32 || s.k % 8 || s.lda % 8 || s.ldb % 8 || !aligned16(s.a) || !aligned16(s.b))
           return CUBED_GEMM_ANY;
       }
     }
