@@ -1,37 +1,54 @@
 """Benchmark: effective input GB/s of Cubed's hot path on MI355X.
 
-Default workload = BASELINE.json configs[1], "quad-means": u, v float32
+Headline (``value``) = BASELINE.json configs[1], "quad-means": u, v float32
 (1000, 720, 1440) per GPU, chunks (10, 720, 1440), ``xp.mean(u * v, axis=0)``
 (fused elementwise + mean), Spec(allowed_mem="2GB", reserved_mem="100MB") as
 in the reference's own quad-means test (cubed/tests/test_core.py:527-538).
-Inputs are generated on the GPU (bit-exact numpy Philox) and are resident in
-HBM before timing; a step is one ``plan.execute(executor, resume=True)`` of
-the mean's plan (every kernel and collective of the reduction), bracketed by
+Inputs are generated on the GPU (bit-exact numpy Philox) and resident in HBM
+before timing; a step is one ``plan.execute(executor, resume=True)`` of the
+mean's plan (every kernel and collective of the reduction), bracketed by
 barrier + synchronize.  value = input bytes of all ranks / time.
 
-Also reported in the same JSON line (``extra``): rechunk 50000x50000 f32
-row-chunks -> column-chunks (configs[2]) and config 1 ((a+1)*2 -> mean).
+``extra`` (same JSON line; each with its own ``roofline`` where one kernel
+dominates):
+* ``rechunk`` -- configs[2]: 50000^2 f32 row chunks (1000, 50000) -> column
+  chunks (50000, 1000), materialised, under the reference-shaped plan
+  (``allowed_mem=2GB``: read -> intermediate -> write, 625 + 25 tasks,
+  primitive/rechunk.py:23-98) and the 288 GB plan (one copy op); bit-exact
+  spot check of target chunks; its own CPU baseline (oracle restatement of
+  copy_read_to_write over the same plan);
+* ``rechunk_mean`` -- mean(x.rechunk(cols), axis=0) twice: "rechunk elided"
+  (the executor reads the rechunk through) and "materialised" (the copy runs,
+  then the mean);
+* ``config1`` -- (a+1)*2 -> mean(axis=0) on random((20000,20000), (5000,5000));
+* ``vorticity`` -- configs[3]: mean(a[1:]*x + b[1:]*y), (1000,900,800) f64;
+* ``matmul_f32`` / ``matmul_bf16`` -- configs[4]: xp.matmul of two
+  40000^2 arrays in (5000, 5000) chunks (the chunk products and the k-sum as
+  one chained-GEMM launch), TFLOP/s against the dense MFMA peak.
 
-Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- the arrays
-grow to (1000 * N, 720, 1440) and their chunks are spread block-cyclically
-over the N GPUs by the distributed GpuDagExecutor (chunk offset mod N), so
-every GPU holds 100 time chunks of u and v.  Each GPU reduces its own chunks
-to (n, total) partials in one streaming launch, one RCCL reduce per field
-combines them on the output block's owner, which runs the aggregate
-(cubed_fused_finish).  No other data-path collective runs.
+Multi-GPU: ``python bench.py --gpus N`` (no torchrun around it) re-launches
+itself as N ranks under torch.distributed.run before touching the GPU; under
+torchrun, WORLD_SIZE must equal --gpus.  Quad-means weak-scales (each GPU
+holds 100 time chunks of u and v: one streaming launch + one RCCL reduce per
+field); the rechunk extras strong-scale (50000^2 total: pack -> one
+all_to_all over xGMI -> unpack; rechunk+mean reduces before the exchange).
 
-CPU baseline (rank 0, N=1 only): the oracle's restatement of the
-reference's numpy executor (oracle/cubed_ref.py quad_means_cpu), 1 thread,
-on a bounded sample (300 of the 1000 time steps), Zarr/Blosc I/O excluded.
+CPU baseline (rank 0, N=1 only): the oracle's restatement of the reference's
+executors (oracle/cubed_ref.py) on the SAME inputs copied back from HBM --
+sequential (PythonDagExecutor, runtime/executors/python.py:14-32) and
+threaded (AsyncPythonDagExecutor's ThreadPoolExecutor, min(32, ncpu + 4)
+workers, python_async.py:91,121-142), warm-up excluded, BLAS pinned to one
+thread; Zarr/Blosc I/O is not modelled (optimistic for the reference).
 """
 
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,25 +57,60 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
+EXTRAS = ("rechunk", "rechunk_mean", "config1", "vorticity", "matmul_f32", "matmul_bf16")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--t-length", type=int, default=1000, help="time steps per GPU (quad-means)")
-    p.add_argument("--no-extra", action="store_true", help="skip the rechunk/config-1 extras")
+    p.add_argument("--no-extra", action="store_true", help="headline only")
+    p.add_argument("--only", default="", help="comma list of extras to run (default: all)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-matmul", action="store_true", help="skip the matmul extra")
-    p.add_argument("--cpu-sample", type=int, default=300)
+    p.add_argument("--no-matmul", action="store_true", help="skip the matmul extras")
+    p.add_argument("--matmul-n", type=int, default=40000)
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
-                        "several ranks on one GPU)")
+                        "several ranks on one GPU or on CPU)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC (see profiles/README.md)")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+# --------------------------------------------------------------------------- launch
+
+
+def launcher_command(args_list, gpus, port):
+    """The child command that runs this script as ``gpus`` ranks (one process
+    per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(args_list)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def maybe_relaunch(args, argv):
+    """--gpus N > 1 outside torchrun: run N ranks as a child (before any GPU
+    call) and exit with its status.  Under torchrun WORLD_SIZE must agree."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is None:
+        if args.gpus > 1:
+            rc = subprocess.call(launcher_command(argv, args.gpus, free_port()))
+            sys.exit(rc)
+        return
+    if int(world) != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}\n")
+        sys.exit(2)
 
 
 def setup_dist(args):
@@ -94,83 +146,7 @@ def sync():
     torch.cuda.synchronize()
 
 
-def run_plan(plan, ex, names, resume):
-    plan.execute(executor=ex, resume=resume, array_names=names)
-
-
-def quad_means(args, rank, world, ex):
-    import cubed_amd as cubed
-    import cubed_amd.array_api as xp
-    import cubed_amd.random as crandom
-    from cubed_amd.core.plan import arrays_to_plan
-    from cubed_amd.runtime.executors.gpu import LaunchTimer
-
-    T = args.t_length * world  # weak scaling: 1000 time steps per GPU
-    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex)
-    random.seed(1000)  # same plan (and root seeds) on every rank
-    u = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
-    v = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
-    # materialise the inputs in HBM (untimed)
-    arrays_to_plan(u, v).execute(executor=ex, array_names=[u.name, v.name])
-    sync()
-    m = xp.mean(u * v, axis=0)
-    plan = arrays_to_plan(m)
-    in_bytes = u.nbytes + v.nbytes
-
-    keep = (u, v)
-
-    def step():
-        # every op of the mean's plan runs each step; only u, v stay resident
-        _reset_targets(plan, keep)
-        run_plan(plan, ex, [m.name], resume=True)
-
-    for _ in range(args.warmup):
-        step()
-    sync()
-    barrier(world)
-    ex.timing = LaunchTimer()
-    sync()
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    barrier(world)
-    t1 = time.perf_counter()
-    timer, ex.timing = ex.timing, None
-    dt = t1 - t0
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return dict(in_bytes=in_bytes, dt=dt, timer=timer, m=m, u=u, v=v)
-
-
-def timed_launches(ex, fn, steps, world):
-    """(seconds per call, {launch: mean ms}) -- the executor's per-launch HIP
-    events recorded during the timed calls."""
-    from cubed_amd.runtime.executors.gpu import LaunchTimer
-
-    ex.timing = LaunchTimer()
-    dt = timed(fn, steps, world)
-    timer, ex.timing = ex.timing, None
-    return dt, {f"{k[0]}#{k[1]}:{k[2]}": round(v[1], 4) for k, v in timer.summary().items()}
-
-
-def timed(fn, steps, world):
-    """Mean seconds per call of fn over `steps` calls, barrier + synchronize
-    on both sides, max over ranks."""
-    sync()
-    barrier(world)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fn()
-    sync()
-    barrier(world)
-    dt = (time.perf_counter() - t0) / steps
+def max_over_ranks(dt, world):
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -181,81 +157,213 @@ def timed(fn, steps, world):
     return dt
 
 
-def dominant(timer, algo_bytes_by_key):
-    """The kernel launch with the largest total time (collectives excluded:
-    the roofline is the fused kernel's)."""
-    summ = timer.summary()
-    kern = [k for k in summ if k[2] == "FusedLaunch"] or list(summ)
-    key = max(kern, key=lambda k: summ[k][0] * summ[k][1])
-    count, ms = summ[key]
-    return key, ms, summ
-
-
-def rechunk_extra(ex, rank):
-    import cubed_amd as cubed
-    import cubed_amd.array_api as xp
-    import cubed_amd.random as crandom
-    from cubed_amd.core.plan import arrays_to_plan
-
-    N = 50000
-    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
-    random.seed(2000)
-    x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
-    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+def timed(fn, steps, world):
+    """Mean seconds per call over ``steps`` calls, barrier + synchronize on
+    both sides, max over ranks."""
     sync()
-    y = x.rechunk((N, 1000))
-    plan = arrays_to_plan(y)
-    for _ in range(2):
-        _exec_only(plan, ex, y, x)
-    dt, launches = timed_launches(ex, lambda: _exec_only(plan, ex, y, x), 5, ex.world)
-    nops = sum(1 for _, d in plan._finalize_dag().nodes(data=True)
-               if d.get("op_name") == "rechunk")
-    # correctness spot check: a few columns
-    return dict(metric="rechunk effective input GB/s", value=x.nbytes / dt / 1e9,
-                ms=dt * 1e3, ops=nops, bytes_moved_per_op=2 * x.nbytes, launches_ms=launches)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    barrier(world)
+    return max_over_ranks((time.perf_counter() - t0) / steps, world)
 
 
-def rechunk_mean_extra(ex, rank):
-    """configs[2] "rechunk+reduce": mean(x.rechunk(columns), axis=0) with x
-    50000^2 f32 in row chunks.  The rechunk feeds only the mean, so the
-    executor reads it through (rewrites.elide_rechunks): each GPU reduces the
-    row-chunk pieces it holds; with N GPUs the partials are combined over
-    RCCL.  value = x bytes / time."""
-    import cubed_amd as cubed
-    import cubed_amd.array_api as xp
-    import cubed_amd.random as crandom
-    from cubed_amd.core.plan import arrays_to_plan
+def timed_launches(ex, fn, steps, world):
+    """(seconds per call, {launch key: (count, mean ms)}) with the executor's
+    per-launch HIP events over the timed calls."""
+    from cubed_amd.runtime.executors.gpu import LaunchTimer
 
-    N = 50000
-    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
-    random.seed(2000)
-    x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
-    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
-    m = xp.mean(x.rechunk((N, 1000)), axis=0)
-    plan = arrays_to_plan(m)
-
-    def step():
-        _reset_targets(plan, x)
-        plan.execute(executor=ex, resume=True, array_names=[m.name])
-
-    step()
-    dt, launches = timed_launches(ex, step, 5, ex.world)
-    return dict(metric="rechunk+mean effective input GB/s", value=x.nbytes / dt / 1e9,
-                ms=dt * 1e3, launches_ms=launches)
+    ex.timing = LaunchTimer()
+    dt = timed(fn, steps, world)
+    timer, ex.timing = ex.timing, None
+    return dt, timer.summary()
 
 
-def _exec_only(plan, ex, y, x):
-    # re-run every rechunk op (x stays resident)
+def fmt_launches(summ):
+    return {f"{k[0]}#{k[1]}:{k[2]}": round(v[1], 4) for k, v in summ.items()}
+
+
+def reset_targets(plan, keep):
+    """Mark every array of the plan except ``keep`` unwritten, so the next
+    ``execute(resume=True)`` re-runs every op (inputs stay resident)."""
     from cubed_amd.storage import DeviceArray
 
+    keep = keep if isinstance(keep, (tuple, list)) else (keep,)
+    kept = {id(a.zarray) for a in keep}
     for _, d in plan._finalize_dag().nodes(data=True):
         t = d.get("target")
-        if isinstance(t, DeviceArray) and t is not x.zarray:
+        if isinstance(t, DeviceArray) and id(t) not in kept:
             t.written = False
-    plan.execute(executor=ex, resume=True, array_names=[y.name])
 
 
-def config1_extra(ex, rank):
+def step_fn(plan, ex, outs, keep):
+    names = [o.name for o in outs]
+
+    def step():
+        reset_targets(plan, keep)
+        plan.execute(executor=ex, resume=True, array_names=names)
+    return step
+
+
+def load_traffic(path, key):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    v = d.get(key)
+    if isinstance(v, dict):
+        return v.get("bytes")
+    return v
+
+
+def roofline_hbm(algo_bytes, ms, traffic_key, args, kernel):
+    achieved = algo_bytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.traffic_json, traffic_key),
+            "algo_bytes": algo_bytes, "kernel": kernel}
+
+
+def free_gpu():
+    import gc
+
+    import torch
+
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+# --------------------------------------------------------------------------- workloads
+
+
+def quad_means(args, rank, world, ex):
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    T = args.t_length * world  # weak scaling: 1000 time steps per GPU
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex)
+    random.seed(1000)  # same plan (and root seeds) on every rank
+    u = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=ex, array_names=[u.name, v.name])  # inputs in HBM (untimed)
+    sync()
+    m = xp.mean(u * v, axis=0)
+    plan = arrays_to_plan(m)
+    step = step_fn(plan, ex, [m], (u, v))
+    for _ in range(args.warmup):
+        step()
+    dt, summ = timed_launches(ex, step, args.steps, world)
+    return dict(in_bytes=u.nbytes + v.nbytes, dt=dt, summ=summ, m=m, u=u, v=v)
+
+
+def dominant(summ, kind):
+    keys = [k for k in summ if k[2] == kind] or list(summ)
+    key = max(keys, key=lambda k: summ[k][0] * summ[k][1])
+    return key, summ[key][1]
+
+
+def rechunk_extra(args, ex, rank, world):
+    """configs[2]: rechunk 50000^2 f32 rows -> columns, materialised.  The
+    2 GB plan is the reference's own (read (2000, 50000) -> int (2000, 2000)
+    -> write (50000, 2000): two copy ops); the 288 GB plan is one op."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    N = 50000
+    res = {}
+    for mem in ("2GB", "288GB"):
+        # x carries its Spec: rechunk plans with x.spec.allowed_mem
+        spec = cubed.Spec(allowed_mem=mem, executor=ex)
+        random.seed(2000)
+        x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        sync()
+        y = x.rechunk((N, 1000))
+        plan = arrays_to_plan(y)
+        dag = plan._finalize_dag()
+        ops = [d for _, d in dag.nodes(data=True) if d.get("op_name") == "rechunk"]
+        ntasks = [d["primitive_op"].num_tasks for d in ops]
+        step = step_fn(plan, ex, [y], x)
+        step()
+        dt, summ = timed_launches(ex, step, 5, world)
+        copies = {k: v for k, v in summ.items() if k[2] in ("CopyLaunch", "RechunkLaunch")}
+        per_op_ms = [v[1] for v in copies.values()]
+        r = dict(metric="rechunk effective input GB/s", value=round(x.nbytes / dt / 1e9, 1),
+                 ms=round(dt * 1e3, 4), allowed_mem=mem, ops=len(ops), tasks=ntasks,
+                 launches_ms=fmt_launches(summ))
+        if world == 1 and copies:
+            key, ms = max(copies.items(), key=lambda kv: kv[1][1])[0], max(per_op_ms)
+            # algorithmic bytes of one copy launch: every element read once + written once
+            r["roofline"] = roofline_hbm(2 * x.nbytes, ms, "rechunk_copy", args,
+                                         f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+        r["check"] = _rechunk_spot_check(x, y, ex, rank, world)
+        res[f"plan_{mem}"] = r
+        if mem == "288GB" and rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_rechunk_baseline(x, ex)
+        del x, y, plan
+        free_gpu()
+    return res
+
+
+def _rechunk_spot_check(x, y, ex, rank, world):
+    """Bit-exact check of the first and last target column chunks (and one
+    in the middle) against the source slices they must hold."""
+    if world > 1:
+        return "skipped (distributed: covered by tests/test_gpu_dist.py)"
+    X, Y = x.zarray, y.zarray
+    nb = Y.numblocks[1]
+    ok = True
+    for j in sorted({0, nb // 2, nb - 1}):
+        got = Y.read_chunk((0, j))
+        c0 = Y.chunk_start((0, j))[1]
+        w = got.shape[1]
+        for i in (0, X.numblocks[0] // 2, X.numblocks[0] - 1):
+            src = X.read_chunk((i, 0))[:, c0:c0 + w]
+            r0 = X.chunk_start((i, 0))[0]
+            ok &= bool(np.array_equal(got[r0:r0 + src.shape[0]].view(np.uint32), src.view(np.uint32)))
+    return "bit-exact" if ok else "MISMATCH"
+
+
+def rechunk_mean_extra(args, ex, rank, world):
+    """configs[2] "rechunk+reduce": mean(x.rechunk(columns), axis=0).
+    elided: the rechunk feeds only the mean, so the executor reads it
+    through (rewrites.elide_rechunks) -- no byte moves, row-chunk pieces
+    reduce in place (with N GPUs only partials cross xGMI).  materialised:
+    the rechunk copy runs (all_to_all with N GPUs), then the mean."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    N = 50000
+    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+    random.seed(2000)
+    x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+    out = {}
+    for mode in ("rechunk elided", "materialised"):
+        ex.elide_rechunks = mode == "rechunk elided"
+        m = xp.mean(x.rechunk((N, 1000)), axis=0)
+        plan = arrays_to_plan(m)
+        step = step_fn(plan, ex, [m], x)
+        step()
+        dt, summ = timed_launches(ex, step, 5, world)
+        out["elided" if mode.startswith("rechunk") else "materialised"] = dict(
+            metric=f"rechunk+mean effective input GB/s ({mode})", value=round(x.nbytes / dt / 1e9, 1),
+            ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+        del m, plan
+        ex._exec_dags.clear()
+    ex.elide_rechunks = True
+    return out
+
+
+def config1_extra(args, ex, rank, world):
     import cubed_amd as cubed
     import cubed_amd.array_api as xp
     import cubed_amd.random as crandom
@@ -268,57 +376,20 @@ def config1_extra(ex, rank):
     sync()
     m = xp.mean((a + 1) * 2, axis=0)
     plan = arrays_to_plan(m)
-    def step():
-        _reset_targets(plan, a)
-        plan.execute(executor=ex, resume=True, array_names=[m.name])
-
+    step = step_fn(plan, ex, [m], a)
     for _ in range(2):
         step()
-    dt, launches = timed_launches(ex, step, 5, ex.world)
-    return dict(metric="config1 (a+1)*2 -> mean(axis=0) effective input GB/s",
-                value=a.nbytes / dt / 1e9, ms=dt * 1e3, launches_ms=launches)
+    dt, summ = timed_launches(ex, step, 5, world)
+    r = dict(metric="config1 (a+1)*2 -> mean(axis=0) effective input GB/s",
+             value=round(a.nbytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+    if world == 1:
+        key, ms = dominant(summ, "FusedLaunch")
+        r["roofline"] = roofline_hbm(a.nbytes, ms, "config1_stream", args,
+                                     f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+    return r
 
 
-def matmul_extra(ex, rank, n=20000, c=5000):
-    """configs[4] shape of work, scaled to one GPU: xp.matmul of two f32
-    (n, n) arrays in (c, c) chunks -- (n/c)^3 chunk GEMMs on MFMA, then the
-    k-sum reduction.  Reports the whole plan's TFLOP/s and the GEMM launch's
-    own rate (HIP events on the executor stream)."""
-    import cubed_amd as cubed
-    import cubed_amd.array_api as xp
-    import cubed_amd.random as crandom
-    from cubed_amd.core.plan import arrays_to_plan
-    from cubed_amd.runtime.executors.gpu import LaunchTimer
-
-    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
-    random.seed(4000)
-    A = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xp.float32)
-    B = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xp.float32)
-    arrays_to_plan(A, B).execute(executor=ex, array_names=[A.name, B.name])
-    m = xp.matmul(A, B)
-    plan = arrays_to_plan(m)
-
-    def step():
-        _reset_targets(plan, (A, B))
-        plan.execute(executor=ex, resume=True, array_names=[m.name])
-
-    step()
-    ex.timing = LaunchTimer()
-    dt = timed(step, 2, ex.world)
-    timer, ex.timing = ex.timing, None
-    summ = timer.summary()
-    gemm = [v for k, v in summ.items() if k[2] == "GemmLaunch"]
-    flop = 2.0 * n ** 3
-    out = dict(metric="matmul f32 TFLOP/s (whole plan)", value=flop / dt / 1e12, ms=dt * 1e3,
-               n=n, chunk=c)
-    if gemm:
-        out["gemm_launch_ms"] = gemm[0][1]
-        out["gemm_tflops"] = flop / (gemm[0][1] * 1e-3) / 1e12 / ex.world
-        out["mfma_util_vs_157TF"] = out["gemm_tflops"] / 157.3
-    return out
-
-
-def vorticity_extra(ex, rank, T=1000):
+def vorticity_extra(args, ex, rank, world, T=1000):
     """configs[3]: the pangeo-vorticity expression of the reference example
     (examples/pangeo-vorticity.ipynb cell 2) -- mean(a[1:] * x + b[1:] * y)
     with a, b (1000, 900, 800) f64 and x, y (900, 800) f64, chunks 100."""
@@ -336,61 +407,154 @@ def vorticity_extra(ex, rank, T=1000):
     arrays_to_plan(a, b, x, y).execute(executor=ex, array_names=[a.name, b.name, x.name, y.name])
     m = xp.mean(a[1:] * x + b[1:] * y)
     plan = arrays_to_plan(m)
-
-    def step():
-        _reset_targets(plan, (a, b, x, y))
-        plan.execute(executor=ex, resume=True, array_names=[m.name])
-
+    step = step_fn(plan, ex, [m], (a, b, x, y))
     step()
-    dt, launches = timed_launches(ex, step, 3, ex.world)
+    dt, summ = timed_launches(ex, step, 3, world)
     in_bytes = a.nbytes + b.nbytes + x.nbytes + y.nbytes
-    return dict(metric="vorticity mean(a[1:]*x + b[1:]*y) effective input GB/s",
-                value=in_bytes / dt / 1e9, ms=dt * 1e3, launches_ms=launches)
+    r = dict(metric="vorticity mean(a[1:]*x + b[1:]*y) effective input GB/s",
+             value=round(in_bytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+    if world == 1:
+        key, ms = dominant(summ, "FusedLaunch")
+        # the dominant launch reads a[1:] and b[1:] (x, y broadcast: L2-resident)
+        algo = 2 * (T - 1) * 900 * 800 * 8 + 2 * 900 * 800 * 8
+        r["roofline"] = roofline_hbm(algo, ms, "vorticity_pieces", args,
+                                     f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+    return r
 
 
-def _reset_targets(plan, keep):
-    from cubed_amd.storage import DeviceArray
+def matmul_extra(args, ex, rank, world, dt_name):
+    """configs[4]: xp.matmul of two (n, n) arrays in (5000, 5000) chunks,
+    f32 or bf16 (inputs Philox f64 -> astype), one chained-GEMM launch."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
 
-    keep = keep if isinstance(keep, tuple) else (keep,)
-    kept = {id(a.zarray) for a in keep}
-    for _, d in plan._finalize_dag().nodes(data=True):
-        t = d.get("target")
-        if isinstance(t, DeviceArray) and id(t) not in kept:
-            t.written = False
+    n, c = args.matmul_n, 5000
+    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+    random.seed(4000)
+    xdt = xp.bfloat16 if dt_name == "bf16" else xp.float32
+    A = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xdt)
+    B = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xdt)
+    arrays_to_plan(A, B).execute(executor=ex, array_names=[A.name, B.name])
+    m = xp.matmul(A, B)
+    plan = arrays_to_plan(m)
+    step = step_fn(plan, ex, [m], (A, B))
+    step()
+    dt, summ = timed_launches(ex, step, 2, world)
+    flop = 2.0 * n ** 3
+    gemm = [v for k, v in summ.items() if k[2] == "GemmLaunch"]
+    r = dict(metric=f"matmul {dt_name} TFLOP/s (whole plan)", value=round(flop / dt / 1e12, 1),
+             ms=round(dt * 1e3, 3), n=n, chunk=c, launches_ms=fmt_launches(summ))
+    if gemm and world == 1:
+        gms = gemm[0][1]
+        tf = flop / (gms * 1e-3) / 1e12
+        r["roofline"] = {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_PEAK_TFS[dt_name],
+                         "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TFS[dt_name], 4),
+                         "traffic": load_traffic(args.traffic_json, f"matmul_{dt_name}"),
+                         "algo_flops": flop, "kernel": f"GemmLaunch, mean {gms:.3f} ms/launch"}
+    return r
 
 
-def cpu_baseline(args):
+# --------------------------------------------------------------------------- CPU baselines
+
+
+def _cpu_info(threads):
+    return (f"numpy {np.__version__}, host cpus {os.cpu_count()}, affinity "
+            f"{len(os.sched_getaffinity(0))}, worker threads {threads}, BLAS threads 1")
+
+
+def cpu_baseline(res, ex):
+    """The oracle's restatement of the reference's executors on config 2's
+    full inputs (copied back from HBM: the same bytes the GPU read),
+    sequential and threaded, warm-up excluded; also checks the GPU mean
+    against the oracle's at full size (rtol 1e-6, f32 output)."""
+    from threadpoolctl import threadpool_limits
+
     from oracle import cubed_ref as R
 
-    T = args.cpu_sample
-    rs1, rs2 = R.root_seed_after(11), R.root_seed_after(12)
-    u = R.random_array((T, 720, 1440), (10, 720, 1440), rs1).astype(np.float32)
-    v = R.random_array((T, 720, 1440), (10, 720, 1440), rs2).astype(np.float32)
-    times = []
-    for _ in range(5):
+    u = res["u"].zarray.to_numpy()
+    v = res["v"].zarray.to_numpy()
+    threads = min(32, (os.cpu_count() or 1) + 4)
+    out = {}
+    with threadpool_limits(1):
+        for name, th, reps in (("sequential", 1, 2), ("threads", threads, 3)):
+            R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=th)  # warm-up
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                exp = R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=th)
+                ts.append(time.perf_counter() - t0)
+            out[name] = (float(np.median(ts)), th)
+    got = res["m"].compute()
+    parity = bool(np.allclose(got, exp, rtol=1e-6, atol=0))
+    nbytes = u.nbytes + v.nbytes
+    dt, th = out["threads"]
+    return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": th, "kind": "port",
+            "sample": f"full config 2: quad-means ({u.shape[0]},720,1440) f32 u,v, chunks (10,720,1440), "
+                      f"oracle restatement of the reference threads executor (AsyncPythonDagExecutor "
+                      f"ThreadPoolExecutor), median of 3 after a warm-up; {_cpu_info(th)}; excludes "
+                      f"Zarr/Blosc I/O (optimistic)",
+            "sequential": {"value": round(nbytes / out["sequential"][0] / 1e9, 3), "cores": 1,
+                           "sample": "same inputs, PythonDagExecutor restatement, median of 2"},
+            "gpu_matches_oracle_full_size": parity}
+
+
+def cpu_rechunk_baseline(x, ex):
+    """copy_read_to_write (primitive/rechunk.py:187-192) over the reference's
+    2 GB plan (read -> intermediate -> write chunks) restated on numpy
+    arrays in memory, on the same 50000^2 f32 input; sequential and threaded
+    (one task per target chunk, as the threads executor maps them)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import cubed_ref as R
+
+    X = x.zarray.to_numpy()
+    N = X.shape[0]
+    read, inter, write = R.rechunking_plan(X.shape, (1000, N), (N, 1000), 4, (2_000_000_000 - 100_000_000) // 4)
+    threads = min(32, (os.cpu_count() or 1) + 4)
+
+    def copy_op(src, dst, chunks, pool):
+        keys = [(i, j) for i in range(-(-N // chunks[0])) for j in range(-(-N // chunks[1]))]
+
+        def task(k):
+            sl = tuple(slice(k[d] * chunks[d], min(N, (k[d] + 1) * chunks[d])) for d in range(2))
+            dst[sl] = src[sl]
+        if pool is None:
+            for k in keys:
+                task(k)
+        else:
+            list(pool.map(task, keys))
+
+    I = np.empty_like(X)
+    Y = np.empty_like(X)
+    out = {}
+    for name, th in (("sequential", 1), ("threads", threads)):
+        pool = ThreadPoolExecutor(th) if th > 1 else None
+        copy_op(X, I, inter, pool)  # warm-up (page faults of I, Y)
+        copy_op(I, Y, write, pool)
         t0 = time.perf_counter()
-        R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=1)
-        times.append(time.perf_counter() - t0)
-    dt = float(np.median(times))
-    return {"value": round((u.nbytes + v.nbytes) / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"quad-means ({T},720,1440) f32 u,v, chunks (10,720,1440), oracle "
-                      f"restatement of the reference python executor, median of 5, numpy "
-                      f"{np.__version__}, host cpus {os.cpu_count()}, affinity "
-                      f"{len(os.sched_getaffinity(0))}; excludes Zarr/Blosc I/O (optimistic)"}
+        copy_op(X, I, inter, pool)
+        copy_op(I, Y, write, pool)
+        out[name] = time.perf_counter() - t0
+        if pool:
+            pool.shutdown()
+    ok = bool(np.array_equal(Y.view(np.uint32), X.view(np.uint32)))
+    return {"value": round(X.nbytes / out["threads"] / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"full config 3: 50000^2 f32, reference 2 GB plan read {read} -> int {inter} -> "
+                      f"write {write}, in-memory numpy region copies (no Zarr/Blosc: optimistic), one "
+                      f"timed pass after a warm-up; {_cpu_info(threads)}",
+            "sequential": {"value": round(X.nbytes / out["sequential"] / 1e9, 3), "cores": 1},
+            "values_unchanged": ok}
 
 
-def load_traffic(path, key_name):
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(key_name)
-    except (OSError, ValueError):
-        return None
+# --------------------------------------------------------------------------- main
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    maybe_relaunch(args, argv)
     rank, world, local = setup_dist(args)
     from cubed_amd.runtime.executors.gpu import GpuDagExecutor
 
@@ -398,36 +562,37 @@ def main():
     res = quad_means(args, rank, world, ex)
     dt = res["dt"]
     in_bytes = res["in_bytes"]
-    value = in_bytes / (dt / args.steps) / 1e9  # global input bytes: all ranks
-    key, ms, summ = dominant(res["timer"], {})
+    value = in_bytes / dt / 1e9  # global input bytes: all ranks
+    key, ms = dominant(res["summ"], "FusedLaunch")
     # algorithmic bytes of the dominant launch: the fused u*v -> mean kernel
-    # reads u and v once (8.294e9 B at T=1000) and writes the (n, total)
-    # partials / final mean (2 x 4.147e9 B read)
-    algo = in_bytes // world  # this rank's share of u and v, read once by the fused launch
-    achieved = algo / (ms * 1e-3) / 1e9
-    extra = {"launches_ms": {f"{k[0]}#{k[1]}:{k[2]}": round(v[1], 4) for k, v in summ.items()}}
-    if not args.no_extra:
+    # reads this rank's u and v once (2 x 4.147e9 B at T=1000)
+    algo = in_bytes // world
+    extra = {"launches_ms": fmt_launches(res["summ"])}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(res, ex)
+    del res
+    free_gpu()
+    wanted = [e for e in EXTRAS if not args.only or e in args.only.split(",")]
+    if args.no_extra:
+        wanted = []
+    if args.no_matmul:
+        wanted = [e for e in wanted if not e.startswith("matmul")]
+    for name in wanted:
         try:
-            extra["rechunk"] = rechunk_extra(ex, rank)
+            if name == "rechunk":
+                extra[name] = rechunk_extra(args, ex, rank, world)
+            elif name == "rechunk_mean":
+                extra[name] = rechunk_mean_extra(args, ex, rank, world)
+            elif name == "config1":
+                extra[name] = config1_extra(args, ex, rank, world)
+            elif name == "vorticity":
+                extra[name] = vorticity_extra(args, ex, rank, world)
+            elif name.startswith("matmul"):
+                extra[name] = matmul_extra(args, ex, rank, world, name.split("_")[1])
         except Exception as e:  # pragma: no cover - reported, not fatal
-            extra["rechunk"] = {"error": repr(e)}
-        try:
-            extra["rechunk_mean"] = rechunk_mean_extra(ex, rank)
-        except Exception as e:  # pragma: no cover
-            extra["rechunk_mean"] = {"error": repr(e)}
-        try:
-            extra["config1"] = config1_extra(ex, rank)
-        except Exception as e:  # pragma: no cover
-            extra["config1"] = {"error": repr(e)}
-        try:
-            extra["vorticity"] = vorticity_extra(ex, rank)
-        except Exception as e:  # pragma: no cover
-            extra["vorticity"] = {"error": repr(e)}
-        if not args.no_matmul:
-            try:
-                extra["matmul"] = matmul_extra(ex, rank)
-            except Exception as e:  # pragma: no cover
-                extra["matmul"] = {"error": repr(e)}
+            extra[name] = {"error": repr(e)}
+        free_gpu()
     line = {
         "metric": "effective input GB/s (node) for fused elementwise+mean (quad-means)",
         "value": round(value, 2),
@@ -435,7 +600,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "ms_per_step": round(dt * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -444,15 +609,14 @@ def main():
         "backend": args.backend if world > 1 else None,
         "config": {"workload": "quad-means: mean(u*v, axis=0), u,v (1000,720,1440) f32 per GPU, "
                                "chunks (10,720,1440), Spec(allowed_mem=2GB, reserved_mem=100MB)",
-                   "t_length_per_gpu": args.t_length, "parallelism": f"block-partition dp{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic(args.traffic_json, "quad_means_fused"),
-                     "kernel": f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch"},
+                   "t_length_per_gpu": args.t_length, "parallelism": f"block-cyclic dp{world}",
+                   "extras_scaling": "strong (rechunk 50000^2 total), weak (others per GPU)"},
+        "roofline": roofline_hbm(algo, ms, "quad_means_fused", args,
+                                 f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch"),
         "extra": extra,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args)
+    if cpu is not None:
+        line["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

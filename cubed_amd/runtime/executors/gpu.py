@@ -790,6 +790,19 @@ class GpuDagExecutor(DagExecutor):
         return new
 
     def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
+        if self.world > 1 and self._stream is not None and self.device.type == "cuda":
+            # collectives are issued on torch's current stream: make it the
+            # executor's, so the pack / exchange / unpack sequence of a
+            # RechunkLaunch or FetchLaunch stays stream-ordered
+            import torch
+
+            st = self._stream if isinstance(self._stream, torch.cuda.Stream) else \
+                torch.cuda.ExternalStream(int(self._stream), device=self.device)
+            with torch.cuda.stream(st):
+                return self._execute_dag(dag, callbacks, array_names, resume)
+        return self._execute_dag(dag, callbacks, array_names, resume)
+
+    def _execute_dag(self, dag, callbacks, array_names, resume):
         stream = self.stream
         dag = self.exec_dag(dag, array_names)
         nodes = dict(dag.nodes(data=True))
