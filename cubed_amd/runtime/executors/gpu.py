@@ -473,7 +473,18 @@ class GpuDagExecutor(DagExecutor):
 
     def _lower_local(self, program, cfg, target, keys):
         if isinstance(program, ir.ExprProgram):
-            return _with_gathers(self.lowerer.lower_expr_pipeline(program, cfg, target, keys), self.device)
+            try:
+                return _with_gathers(self.lowerer.lower_expr_pipeline(program, cfg, target, keys), self.device)
+            except LoweringError:
+                from ...lowering import program_fits
+
+                if program_fits(program):
+                    raise
+                # more inputs / instructions than one fused program holds:
+                # factor parts out into HBM temporaries (cubed_amd/split.py)
+                from ...split import split_launches
+
+                return split_launches(self, program, cfg, target, keys)
         return [self._lower_gemm(program, cfg, target, keys)]
 
     def _task_reads(self, program, cfg, key, regions=True):

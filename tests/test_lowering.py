@@ -376,3 +376,36 @@ def test_bfloat16_promotion():
     assert xp.result_type(xp.float64, xp.bfloat16) == xp.float64
     with pytest.raises(TypeError):
         xp.result_type(xp.bfloat16, xp.int32)
+
+
+def test_five_input_map_splits_into_two_fused_launches(built, dry):
+    """A chunk function reading 5 arrays (more than one fused program's 4
+    leaves) runs as a part program into an HBM temporary + the remainder,
+    instead of raising (cubed_amd/split.py)."""
+    spec = cubed.Spec(allowed_mem=10**8, executor=dry)
+    arrs = [cubed.from_array(np.full((64, 48), i + 1.0), chunks=(32, 24), spec=spec) for i in range(5)]
+    m = cubed.map_blocks(lambda a, b, c, d, e: a * b + c * d + e, *arrs, dtype=np.float64)
+    arrays_to_plan(m).execute(executor=dry, array_names=[m.name])
+    fused = _fused(dry)
+    assert len(fused) == 2
+    assert fused[0].prog.nleaves <= 4 and fused[1].prog.nleaves <= 4
+    assert fused[0].ntasks == fused[1].ntasks == 4
+
+
+def test_split_program_keeps_every_input():
+    from cubed_amd import ir
+    from cubed_amd.lowering import collect_leaves, program_fits
+    from cubed_amd.split import split_program
+
+    f8 = np.dtype(np.float64)
+    a = [ir.Arg(i, f8, (0, 1)) for i in range(6)]
+    e = ir.apply_op("add", [ir.apply_op("multiply", [a[0], a[1]], f8),
+                            ir.apply_op("multiply", [a[2], a[3]], f8)], f8)
+    e = ir.apply_op("add", [e, ir.apply_op("subtract", [a[4], a[5]], f8)], f8)
+    p = ir.ExprProgram(ndim=2, nargs=6, outputs=e, out_axes=(0, 1), name="six")
+    assert not program_fits(p)
+    parts, rest = split_program(p)
+    assert parts and program_fits(rest) and all(program_fits(s) for s, _ in parts)
+    used = {l.index for s, _ in parts for l in collect_leaves([s.outputs])}
+    used |= {l.index for l in collect_leaves([rest.outputs]) if l.index < 6}
+    assert used == set(range(6))
