@@ -65,6 +65,8 @@ class Chain:
     final_spec: object
     final_target: DeviceArray
     levels: List[Tuple[object, object]]  # (spec, program) of each combine node
+    # the first node reads index/merge regions (lowered as pieces, chain_piece_rows)
+    regions: bool = False
 
 
 def _reduce_leaf(f: ir.ReduceField):
@@ -99,8 +101,7 @@ def find_chains(dag, array_names, exclude=()) -> Dict[str, Chain]:
         p1 = d["pipeline"].config.function
         if not isinstance(p1, ir.ExprProgram) or p1.reduce is None:
             continue
-        if any(isinstance(l, ir.Region) for f in p1.reduce.fields for l in ir.leaves(f.expr)):
-            continue
+        has_regions = any(isinstance(l, ir.Region) for f in p1.reduce.fields for l in ir.leaves(f.expr))
         fmap = _field_map(p1)
         if fmap is None:
             continue
@@ -172,6 +173,7 @@ def find_chains(dag, array_names, exclude=()) -> Dict[str, Chain]:
         chains[n] = Chain(members, program, first_cfg, first_cfg.write.array,
                           final_node["pipeline"].config, final_node["pipeline"].config.write.array,
                           levels)
+        chains[n].regions = has_regions
         claimed.update(members)
     return chains
 
@@ -309,6 +311,114 @@ def chain_rows(lowerer, chain: Chain, leaves, kinds, final_keys, select=None, ou
             obases, ostr = _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard)
             rows[i] = TaskRow(extent, [0] * len(leaves), lstrides, obases, ostr, 0, 0, 0)
     return rows, red
+
+
+def chain_piece_rows(lowerer, chain: Chain, leaves, kinds, final_keys):
+    """Task rows of a chain whose first node reads regions that straddle
+    source chunks (``a[1:]`` of index, core/ops.py:374-486): every
+    contributing task is cut into single-chunk pieces (Lowerer.task_pieces)
+    and the pieces of one output block that continue each other along a
+    reduced dim -- the tail of task j and the head of task j+1 read the same
+    source chunk -- are merged back into one row, so the pass walks SOURCE
+    chunks (one row each) instead of output tasks (two rows each, one of them
+    a single plane).  The chain sums every contributing task of a block, so
+    regrouping rows between tasks changes only the association of the
+    (associative) field reductions.  Returns (rows, reduced dims, group keys,
+    gathers): one group per final block, partials combined before the
+    chain's epilogue."""
+    p1 = chain.first_spec.function
+    axes = tuple(chain.program.reduce.axes)
+    na = len(axes)
+    n = chain.program.ndim
+    red = set(range(na)) | {na + a for a in axes}
+    isz = [np.dtype(leaves[l].dtype).itemsize if k == LEAF_ARRAY else 1 for l, k in enumerate(kinds)]
+    rows, groups, gathers = [], [], []
+    for K in final_keys:
+        tkeys = contributing_keys(chain, K)
+        if not tkeys:
+            raise LoweringError("a chain output block has no contributing tasks")
+        pieces = []
+        for t in tkeys:
+            reads = []
+            prow, pgroups = lowerer.task_pieces(p1, chain.first_spec, chain.first_target, t, leaves, [],
+                                                p1.structured, gathers, reads_out=reads)
+            if any(g[1] != pgroups[0][1] for g in pgroups):
+                raise LoweringError("region pieces cut a kept dim of a chain")
+            for r, rd in zip(prow, reads):
+                pieces.append((tuple((id(a), c, f) for a, c, f in rd), r))
+        merged = _merge_pieces(pieces, [a for a in axes], isz)
+        for r in merged:
+            extent = [1] * na + list(r.extent)
+            obases, ostr = _chain_outputs(chain, K, extent, axes, na, n, None, 0)
+            rows.append(TaskRow(extent, list(r.bases), [[0] * na + list(st) for st in r.lstrides],
+                                obases, ostr, r.key_lo, r.key_hi, r.block_offset))
+            groups.append(tuple(K))
+    return rows, red, groups, gathers
+
+
+def _merge_pieces(pieces, red_dims, isz):
+    """Merge rows that continue each other along one reduced dim (same source
+    chunks, equal extents elsewhere, every leaf's base advancing by extent x
+    stride).  ``pieces``: (source-chunk signature, TaskRow) in task order."""
+    buckets: Dict[tuple, List[TaskRow]] = {}
+    order = []
+    for sig, r in pieces:
+        key = (sig, r.key_lo, r.key_hi, r.block_offset)
+        if key not in buckets:
+            buckets[key] = []
+            order.append(key)
+        buckets[key].append(r)
+    out = []
+    for key in order:
+        rs = buckets[key]
+        acc: List[TaskRow] = []
+        for r in rs:
+            for i, q in enumerate(acc):
+                m = _try_merge(q, r, red_dims, isz)
+                if m is None:
+                    m = _try_merge(r, q, red_dims, isz)
+                if m is not None:
+                    acc[i] = m
+                    break
+            else:
+                acc.append(r)
+        out += acc
+    return out
+
+
+def _try_merge(q: TaskRow, r: TaskRow, red_dims, isz) -> Optional[TaskRow]:
+    """q followed by r along one reduced dim, as one row (None if they do not
+    continue each other)."""
+    nd = len(q.extent)
+    for d in red_dims:
+        if any(q.extent[e] != r.extent[e] for e in range(nd) if e != d):
+            continue
+        strides = []
+        ok = True
+        for l in range(len(q.bases)):
+            diff = r.bases[l] - q.bases[l]
+            step = q.extent[d] * isz[l]
+            if diff % step:
+                ok = False
+                break
+            s = diff // step
+            if (q.extent[d] > 1 and q.lstrides[l][d] != s) or (r.extent[d] > 1 and r.lstrides[l][d] != s):
+                ok = False
+                break
+            if any(q.lstrides[l][e] != r.lstrides[l][e] for e in range(nd) if e != d and q.extent[e] > 1):
+                ok = False
+                break
+            strides.append(s)
+        if not ok:
+            continue
+        ext = list(q.extent)
+        ext[d] += r.extent[d]
+        lstr = [list(st) for st in q.lstrides]
+        for l, s in enumerate(strides):
+            lstr[l][d] = s
+        return TaskRow(ext, list(q.bases), lstr, list(q.obases), [list(o) for o in q.ostrides],
+                       q.key_lo, q.key_hi, q.block_offset)
+    return None
 
 
 def _chain_outputs(chain, K, extent, axes, na, n, out_owned, discard):

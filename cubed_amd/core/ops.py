@@ -830,6 +830,7 @@ def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
     from ..array_api import manipulation_functions as mf
     from ..array_api import searching_functions as sf
     from ..array_api import statistical_functions as stf
+    from ..array_api.data_type_functions import astype
 
     def index_along(d):
         """The index along dim d, broadcastable against x."""
@@ -839,25 +840,56 @@ def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
                 idx = mf.expand_dims(idx, axis=e)
         return idx
 
-    reduce_max = stf.max if arg_func == "argmax" else stf.min
-    if axis is None and x.ndim > 1:
-        # the reference flattens with reshape (argmax(x) on an n-d array);
-        # here the flat C-order index is built from the per-dim indexes
-        m = reduce_max(x, keepdims=True)
+    def flat_index():
         flat = None
         for d in range(x.ndim):
             stride = int(np.prod(x.shape[d + 1:], dtype=np.int64))
             term = ef.multiply(index_along(d), cf.asarray(np.int64(stride), spec=x.spec))
             flat = term if flat is None else ef.add(flat, term)
-        target_axis, idx = None, flat
-    else:
-        if axis is None:
-            axis = 0
+        return flat
+
+    if axis is not None:
         axis = validate_axis(axis, x.ndim)
         if isinstance(axis, tuple):
             if len(axis) != 1:
                 raise ValueError("argmax/argmin take a single axis")
             axis = axis[0]
+    vbits = _packed_key_bits(x.dtype)
+    n_index = x.size if axis is None else x.shape[axis]
+    if vbits is not None and x.ndim > 0 and n_index <= (1 << (53 - vbits)):
+        # one pass over x: max of (value key << ibits | reversed index), exact
+        # in f64 / int64 (< 2^53); ties keep the smallest index, NaN wins
+        ibits = 53 - vbits
+        if axis is None and x.ndim > 1:
+            target_axis, idx = None, flat_index()
+        else:
+            target_axis, idx = (0 if axis is None else axis), index_along(0 if axis is None else axis)
+        if x.dtype.kind == "f" or x.dtype == ir.bfloat16:
+            key = elemwise("ordkey_max" if arg_func == "argmax" else "ordkey_min", x, dtype=np.float64)
+            low = cf.asarray(np.float64((1 << ibits) - 1), spec=x.spec)
+            scale = cf.asarray(np.float64(1 << ibits), spec=x.spec)
+            idx = astype(idx, np.float64)  # exact: < 2^53
+        else:
+            key = astype(x, np.int64)
+            if x.dtype.kind == "i":
+                key = ef.add(key, cf.asarray(np.int64(1 << (vbits - 1)), spec=x.spec))
+            if arg_func == "argmin":
+                key = ef.subtract(cf.asarray(np.int64((1 << vbits) - 1), spec=x.spec), key)
+            low = cf.asarray(np.int64((1 << ibits) - 1), spec=x.spec)
+            scale = cf.asarray(np.int64(1 << ibits), spec=x.spec)
+        packed = ef.add(ef.multiply(key, scale), ef.subtract(low, idx))
+        m = stf.max(packed, axis=target_axis, keepdims=keepdims)
+        return astype(ef.subtract(low, ef.remainder(m, scale)), np.int64)
+
+    reduce_max = stf.max if arg_func == "argmax" else stf.min
+    if axis is None and x.ndim > 1:
+        # the reference flattens with reshape (argmax(x) on an n-d array);
+        # here the flat C-order index is built from the per-dim indexes
+        m = reduce_max(x, keepdims=True)
+        target_axis, idx = None, flat_index()
+    else:
+        if axis is None:
+            axis = 0
         m = reduce_max(x, axis=axis, keepdims=True)
         target_axis, idx = axis, index_along(axis)
     eq = ef.equal(x, m)
@@ -866,6 +898,19 @@ def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
     big = cf.asarray(np.int64(np.iinfo(np.int64).max), spec=x.spec)
     cand = sf.where(eq, idx, big)
     return stf.min(cand, axis=target_axis, keepdims=keepdims)
+
+
+def _packed_key_bits(dtype):
+    """Bits of the order-preserving value key of ``dtype`` for the one-pass
+    argmax/argmin (None: no packed form; 64-bit values take two passes)."""
+    dt = np.dtype(dtype)
+    if dt.kind == "b":
+        return 1
+    if dt.kind in "iu" and dt.itemsize <= 4:
+        return 8 * dt.itemsize
+    if dt in (np.dtype(np.float32), np.dtype(np.float16), ir.bfloat16):
+        return 32  # keyed through the value's f32 bit pattern
+    return None
 
 
 def unify_chunks(*args: "Array", **kwargs):

@@ -77,6 +77,18 @@ CUBED_DEV V cast_val(V x, int t, int s) {
   }
 }
 
+// Order-preserving key of an f32 value in [0, 2^32 - 1]: larger value ->
+// larger key (reversed when `rev`), -0 and +0 equal, every NaN the largest
+// key in both orders (numpy's argmax/argmin return the first NaN).
+CUBED_DEV uint32_t ordkey32(float f, bool rev) {
+  if (f != f) return 0xffffffffu;
+  if (f == 0.f) f = 0.f;
+  uint32_t b = __float_as_uint(f);
+  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  // non-NaN keys are <= 0xff800000 (+inf), so the reversed order stays below NaN's
+  return rev ? 0xfffffffeu - b : b;
+}
+
 template <typename V, int VEC>
 CUBED_DEV void unary(int op, V (&X)[VEC]) {
   if constexpr (is_same_v<V, int64_t>) {
@@ -128,6 +140,8 @@ CUBED_DEV void unary(int op, V (&X)[VEC]) {
       case CUBED_OP_ATANH: CUBED_EACH(atanh(x)); break;
       case CUBED_OP_EXP2: CUBED_EACH(exp2(x)); break;
       case CUBED_OP_SIGNBIT: CUBED_EACH((V)(signbit(x) ? 1 : 0)); break;
+      case CUBED_OP_ORDKEY_MAX: CUBED_EACH((V)ordkey32((float)x, false)); break;
+      case CUBED_OP_ORDKEY_MIN: CUBED_EACH((V)ordkey32((float)x, true)); break;
       default: break;
     }
   }

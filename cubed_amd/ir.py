@@ -92,6 +92,8 @@ UNARY_OPS = {
     "log1p": 37, "expm1": 38, "log2": 39, "log10": 40, "sinh": 41, "cosh": 42,
     "asin": 43, "acos": 44, "atan": 45, "asinh": 46, "acosh": 47, "atanh": 48,
     "exp2": 49, "signbit": 50, "positive": None,
+    # internal (argmax/argmin packed keys): f64 result, float inputs only
+    "ordkey_max": 51, "ordkey_min": 52,
 }
 BINARY_OPS = {
     "add": 64, "subtract": 65, "multiply": 66, "divide": 67, "floor_divide": 68,

@@ -916,8 +916,16 @@ class Lowerer:
         gathers = []
         group_start = None
         if rows_fn is not None:
-            rows, red_axes = rows_fn(leaves, kinds)
+            res = rows_fn(leaves, kinds)
+            rows, red_axes = res[0], res[1]
             n = len(rows[0].extent)
+            if len(res) > 2:
+                # rows of several groups (chain_piece_rows): partials + grouped finish
+                group_keys = res[2]
+                gathers += res[3]
+                starts = [i for i in range(len(group_keys)) if i == 0 or group_keys[i] != group_keys[i - 1]]
+                group_start = np.array(starts + [len(group_keys)], dtype=np.int64)
+                partials = partials or len(starts) < len(group_keys)
         else:
             red_axes = set(program.reduce.axes) if program.reduce is not None else set()
             n = program.ndim

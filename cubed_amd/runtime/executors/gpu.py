@@ -205,8 +205,9 @@ class GpuDagExecutor(DagExecutor):
                     d.from_numpy(np.asarray(arr.array))
                 d.written = True
                 self._uploads[key] = d
-                self._keepalive = getattr(self, "_keepalive", [])
-                self._keepalive.append(arr)
+                # the cache entry (and its HBM) lives as long as the source
+                # array: id() may be reused once the array is collected
+                weakref.finalize(arr, _drop_upload, weakref.ref(self), key)
             return d
         if isinstance(arr, VirtualEmptyArray):
             raise LoweringError("a chunk function reads an empty (template) array")
@@ -682,6 +683,19 @@ class GpuDagExecutor(DagExecutor):
         target = chain.final_target
         self.allocate(target)
         keys = self._task_keys(target)
+        if chain.regions:
+            if self.world > 1:
+                # the distributed pieces path (DistPiecesLaunch) runs these per op
+                raise LoweringError("region chains run op by op on several GPUs")
+            from ...chains import chain_piece_rows
+
+            launch = self.lowerer.lower_expr_pipeline(
+                chain.program, chain.first_spec, target, keys,
+                rows_fn=lambda leaves, kinds: chain_piece_rows(self.lowerer, chain, leaves, kinds, keys),
+                sample_key=contributing_keys(chain, keys[0])[0])
+            launches = _with_gathers(launch, self.device)
+            self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
+            return launches
         if self.world > 1:
             launches = self._compiled_chain_dist(chain, target, keys)
             self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
@@ -895,9 +909,17 @@ class GpuDagExecutor(DagExecutor):
                     total += t.device_bytes()
                 else:  # this rank's block-cyclic share, at most
                     total += -(-t.nchunks // self.world) * sum(t.slot_bytes(f) for f in t.fields)
+        # uploaded host / in-memory sources are replicated on every rank
+        total += sum(d.device_bytes() for d in self._uploads.values() if d.allocated)
         if total > HBM_BYTES_PER_GPU:
             raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")
+
+
+def _drop_upload(ex_ref, key):
+    ex = ex_ref()
+    if ex is not None:
+        ex._uploads.pop(key, None)
 
 
 class _remote_chunks:

@@ -26,6 +26,7 @@ import itertools
 import json
 import math
 import os
+import shutil
 import zlib
 from concurrent.futures import ThreadPoolExecutor
 import numpy as np
@@ -123,10 +124,15 @@ class ZarrV2Array:
             if mode == "w-":
                 raise FileExistsError(f"a Zarr array already exists at {path!r}")
             if mode == "w":
+                # every entry but the metadata goes, nested chunk directories
+                # ("/" separator) included: a stale chunk the new write never
+                # touches would otherwise read back instead of fill_value
                 for f in os.listdir(path):
                     if f != ".zarray":
                         p = os.path.join(path, f)
-                        if os.path.isfile(p):
+                        if os.path.isdir(p) and not os.path.islink(p):
+                            shutil.rmtree(p)
+                        else:
                             os.remove(p)
         os.makedirs(path, exist_ok=True)
         tmp = mpath + f".tmp{os.getpid()}"

@@ -110,6 +110,10 @@ enum cubed_op {
   CUBED_OP_LOG2, CUBED_OP_LOG10, CUBED_OP_SINH, CUBED_OP_COSH, CUBED_OP_ASIN,
   CUBED_OP_ACOS, CUBED_OP_ATAN, CUBED_OP_ASINH, CUBED_OP_ACOSH,
   CUBED_OP_ATANH, CUBED_OP_EXP2, CUBED_OP_SIGNBIT,
+  /* order-preserving 32-bit key of the value rounded to f32 (argmax/argmin
+     packed keys, core/ops.py:1093-1153): NaN above +inf, -0 == +0; the
+     _MIN form reverses the order of non-NaN values */
+  CUBED_OP_ORDKEY_MAX, CUBED_OP_ORDKEY_MIN,
   /* binary */
   CUBED_OP_ADD = 64, CUBED_OP_SUB, CUBED_OP_MUL, CUBED_OP_DIV,
   CUBED_OP_FLOORDIV, CUBED_OP_MOD, CUBED_OP_POW, CUBED_OP_MAX, CUBED_OP_MIN,

@@ -374,6 +374,35 @@ def test_index_slice_and_mean(ex):
     assert np.isclose(got, exp, rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("expr", ["mean0", "nanmean_all", "max_all", "argmax0_f32", "sum02"])
+def test_region_chains_walk_source_chunks(ex, expr):
+    """Reductions over straddling index regions as one chain launch over
+    merged source-chunk pieces (chains.chain_piece_rows): the straddled axis
+    is reduced, kept dims are whole blocks."""
+    rng = np.random.default_rng(29)
+    A = rng.random((47, 10, 12))
+    A[5, 3, 4] = np.nan
+    spec = mkspec(ex)
+    a = cubed.from_array(A, chunks=(10, 4, 5), spec=spec)
+    sa, SA = a[1:], A[1:]
+    if expr == "mean0":
+        got, exp = xp.mean(sa * 2, axis=0).compute(), np.mean(SA * 2, axis=0)
+    elif expr == "nanmean_all":
+        got, exp = cubed.nanmean(sa).compute(), np.nanmean(SA)
+    elif expr == "max_all":
+        got, exp = xp.max(a[3:]).compute(), np.max(A[3:])
+        assert np.isnan(got) and np.isnan(exp)
+        return
+    elif expr == "argmax0_f32":
+        s32 = xp.astype(a, xp.float32)[2:]
+        got, exp = xp.argmax(s32, axis=0).compute(), np.argmax(A.astype(np.float32)[2:], axis=0)
+        assert np.array_equal(got, exp)
+        return
+    else:
+        got, exp = xp.sum(sa, axis=(0, 2)).compute(), np.sum(SA, axis=(0, 2))
+    assert np.allclose(got, exp, rtol=1e-12, atol=0, equal_nan=True)
+
+
 @pytest.mark.parametrize("expr", ["map", "sum0", "sum1", "mean_all", "max0"])
 def test_straddling_regions_as_pieces(ex, expr):
     """index regions that straddle source chunks run as per-chunk pieces
@@ -453,6 +482,41 @@ def test_arg_reductions_ties_and_nans(ex, fn):
     for axis in (0, 1, None):
         got = getattr(xp, fn)(a, axis=axis).compute()
         assert np.array_equal(got, getattr(x, fn)(axis=axis)), axis
+
+
+@pytest.mark.parametrize("dtype", ["float32", "float16", "int32", "int16", "uint32", "uint8", "bool"])
+@pytest.mark.parametrize("fn", ["argmax", "argmin"])
+def test_arg_reductions_packed_keys(ex, fn, dtype):
+    """One-pass argmax/argmin over packed (value key, reversed index) keys for
+    <= 32-bit dtypes: bit-exact indexes vs numpy, ties -> first index, NaN ->
+    first NaN, -0 == +0, +-inf and the dtype's extreme values, over axis 0, 1,
+    None and keepdims."""
+    rng = np.random.default_rng(23)
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        x = (np.round(rng.standard_normal((45, 39)) * 2) / 2).astype(dt)  # ties
+        x[3, 4] = -0.0
+        x[9, 4] = 0.0
+        x[2, 10], x[30, 10] = np.inf, -np.inf
+        x[11, 20], x[12, 21] = np.finfo(dt).max, np.finfo(dt).min
+        x[40, 5] = x[17, 5] = np.nan
+        x[:, 33] = np.nan
+    elif dt.kind == "b":
+        x = rng.random((45, 39)) < 0.5
+        x[:, 7] = False
+        x[:, 8] = True
+    else:
+        info = np.iinfo(dt)
+        x = rng.integers(max(info.min, -5), min(info.max, 5) + 1, (45, 39)).astype(dt)
+        x[1, 2], x[44, 2] = info.max, info.min
+        x[6, 9] = x[8, 9] = info.max
+    spec = mkspec(ex)
+    a = cubed.from_array(x, chunks=(7, 10), spec=spec)
+    for axis in (0, 1, None):
+        for keepdims in (False, True):
+            got = np.asarray(getattr(xp, fn)(a, axis=axis, keepdims=keepdims).compute())
+            exp = getattr(np, fn)(x, axis=axis, keepdims=keepdims)
+            assert got.dtype == np.int64 and np.array_equal(got, exp), (axis, keepdims)
 
 
 # ----------------------------------------------------------- callbacks / resume

@@ -197,6 +197,28 @@ def test_vorticity_regions_are_pieces_not_gathers(built, dry):
     assert first.ntasks > first.ngroups
 
 
+def test_vorticity_chain_walks_source_chunks(built, dry):
+    """The whole reduction (per-chunk mean + merge/combine rounds + aggregate)
+    is ONE launch whose rows are the source chunks: the tail plane of task j
+    and the head of task j+1 (both in source chunk j+1) are merged, so no
+    single-plane pieces remain and there is one group (the scalar)."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(1)
+    a = crandom.random((40, 18, 16), chunks=(10, 9, 8), spec=spec)
+    b = crandom.random((40, 18, 16), chunks=(10, 9, 8), spec=spec)
+    x = crandom.random((18, 16), chunks=(9, 8), spec=spec)
+    y = crandom.random((18, 16), chunks=(9, 8), spec=spec)
+    arrays_to_plan(a, b, x, y).execute(executor=dry, array_names=[a.name, b.name, x.name, y.name])
+    dry.launched.clear()
+    m = xp.mean(a[1:] * x + b[1:] * y)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    assert len(fused) == 1
+    f = fused[0]
+    assert f.ngroups == 1 and f.ntasks == 4 * 2 * 2  # source chunks x kept blocks
+    assert sorted(r.extent[3] for r in f.layout.rows) == [9] * 4 + [10] * 12
+
+
 def test_rechunk_then_mean_reads_the_source(built, dry):
     """rechunk rows -> columns then mean(axis=0): no copy launch; the mean's
     tasks are cut into per-source-chunk pieces (partials + grouped finish)."""

@@ -280,3 +280,18 @@ def test_zarr_refuses_what_it_cannot_decode(tmp_path, built):
     json.dump(meta, open(tmp_path / "q.zarr" / ".zarray", "w"))
     with pytest.raises(NotImplementedError, match="zstd"):
         Z.open_array(str(tmp_path / "q.zarr"))
+
+
+def test_zarr_overwrite_removes_nested_chunks(tmp_path, built):
+    """mode='w' over a '/'-separated array: chunks in nested directories go
+    too, so a chunk the new write never touches reads back as fill_value."""
+    p = str(tmp_path / "n.zarr")
+    a = Z.ZarrV2Array.create(p, (4, 4), np.float64, (2, 2), fill_value=0.0, dimension_separator="/")
+    a[...] = np.arange(16.0).reshape(4, 4)
+    assert os.path.isdir(os.path.join(p, "1"))
+    b = Z.ZarrV2Array.create(p, (4, 4), np.float64, (2, 2), fill_value=-2.0, mode="w",
+                             dimension_separator="/")
+    assert sorted(os.listdir(p)) == [".zarray"]
+    b.write_chunk((0, 0), np.ones((2, 2)))
+    got = Z.open_array(p)[...]
+    assert np.array_equal(got[:2, :2], np.ones((2, 2))) and np.all(got[2:] == -2.0) and np.all(got[:, 2:] == -2.0)
