@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 6  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 7  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -160,8 +160,10 @@ def lib():
                                        c_void_p, c_int64, c_int64, c_void_p, c_void_p]
     L.cubed_combine_groups.restype = c_int
     L.cubed_fold_groups.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
-                                    c_void_p, c_int64, c_void_p, c_void_p]
+                                    c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]
     L.cubed_fold_groups.restype = c_int
+    L.cubed_fold_groups_splits.argtypes = [c_int64, c_int64]
+    L.cubed_fold_groups_splits.restype = c_int64
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]
     L.cubed_combine_partials.restype = c_int
@@ -197,7 +199,7 @@ EXPORTED_SYMBOLS = (
     "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
-    "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups",
+    "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
     "cubed_gemm_batched", "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_gemm_chain", "cubed_gemm_chain_path",
 )

@@ -108,7 +108,11 @@ __device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
   __builtin_amdgcn_global_load_lds((const CUBED_G void*)(uintptr_t)src, (CUBED_L void*)dst, 16, 0, 0);
 }
 
-template <bool OUT_BF16>
+// ABL: ablation bits for tools/gemm_bf16_probe.hip only (0 in the library):
+// 1 = no K-loop staging, 2 = no B fragment reads, 4 = no A fragment reads,
+// 8 = no K-loop barrier.  Any nonzero value computes wrong results.
+// PP: ping-pong schedule (see the K loop).
+template <bool OUT_BF16, int ABL = 0, bool PP = false>
 __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                          const cubed_gemm_seg_t* __restrict__ segs,
                                                          int64_t tiles_m, int64_t tiles_n,
@@ -221,30 +225,88 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 bf[4];
 
   const int64_t nst = (KT + HB_BK - 1) / HB_BK;
   // prologue: steps 0, 1, 2 in flight
   for (int64_t p = 0; p < 3 && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
+  // retire this wave's loads of step q (4 per step; steps up to q + 2 issued)
+  auto wait_step = [&](int64_t q) {
+    const int64_t younger = nst - 1 - q;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if constexpr (PP) {
+    // Ping-pong: the two wave rows (wr = 0, 1: one wave of each per SIMD)
+    // run one barrier-delimited slot apart, alternating a memory slot M(p)
+    // -- step p's fragments into registers, step p+3's global->LDS loads --
+    // and a compute slot C(p) of 32 MFMAs, so each SIMD's matrix core is fed
+    // by one wave while the other reads LDS.  Global slot 2p: row 0 in M(p),
+    // row 1 in C(p-1); slot 2p+1: row 0 in C(p), row 1 in M(p).
+    // RAW: every wave retires its step p+1 loads at the end of M(p) (slot 2p
+    //   or 2p+1), before the barrier ending slot 2p+1; step p+1 is read in
+    //   slot 2p+2 at the earliest.
+    // WAR: M(p) restages slot (p+3)%4 = step p-1's, whose last reader (row 1,
+    //   M(p-1), slot 2p-1) retired its reads (lgkmcnt(0)) before the barrier
+    //   ending slot 2p-1.
+    if (nst > 0) wait_step(0);
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8 af[8];
+    for (int64_t p = 0; p < nst; ++p) {
+      // ---- M(p)
+      const CUBED_L char* bufc = lds + (p & (HB_NS - 1)) * HB_STAGE;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
+        s16x4 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(pb));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(pb));
+        bf[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb) af[mb] = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
+      if (p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (p + 1 < nst) wait_step(p + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- C(p)
+#pragma unroll
+      for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb], bf[nb], acc[mb][nb], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // same barrier count in both rows
+  } else
   for (int64_t p = 0; p < nst; ++p) {
     // this wave's loads of step p have landed once at most the younger
     // steps' loads (4 per step) are outstanding
     const int64_t younger = nst - 1 - p;
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if (ABL & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // every wave's step p landed; every wave finished reading step p-1's slot
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(ABL & 8)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
+    if (!(ABL & 1) && p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
     const CUBED_L char* bufc = lds + (p & (HB_NS - 1)) * HB_STAGE;
     // B fragments by transposed reads.  Inline asm: the builtin has no memory
     // operand, so hipcc would put an s_waitcnt vmcnt(0) in front of it --
     // draining the three K steps in flight -- and the reads only touch slot
     // p, which the vmcnt + barrier above already made visible.
-    bf16x8 bf[4];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
+      if ((ABL & 2) && p > 0) break;
       const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
       s16x4 lo, hi;
       asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(pb));
@@ -256,7 +318,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
     // (s_setprio(1) around this MFMA cluster measured 1046 vs 1069 TF: not used)
 #pragma unroll
     for (int mb = 0; mb < 8; ++mb) {
-      const bf16x8 af = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
+      const bf16x8 af = (ABL & 4) ? bf[mb & 3] : *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb)
         acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[nb], acc[mb][nb], 0, 0, 0);

@@ -468,6 +468,31 @@ CUBED_DEV void combine_groups_body(
   }
 }
 
+// Workgroup fold of per-thread accumulators (64-wide shuffle tree, then the
+// waves in order through LDS); thread 0 stores out[f * stride + idx].
+CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIELDS],
+                                Acc (&red)[kBlock / 64][CUBED_MAX_FIELDS], Acc* __restrict__ out,
+                                int64_t stride, int64_t idx) {
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) red[wave][f] = a[f];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
+      Acc x = red[0][f];
+      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
+      out[f * stride + idx] = x;
+    }
+  }
+}
+
 // Full reductions run "lifted": the innermost reduced dims are walked as if
 // kept (kernel A / streaming, one lane per element, rows in flight), leaving
 // per-element partials; this fold then reduces each group's rows AND kept
@@ -495,24 +520,55 @@ CUBED_DEV void fold_groups_body(
           a[f] = acc_combine(a[f], soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
     }
   }
+  block_fold_store(P, a, red, out, ngroups, g);
+}
+
+// Split fold for few groups of many rows (e.g. one scalar over 720 source
+// chunks): workgroup b = (group g, split s) folds rows gs[g] + s, + nsplit,
+// ... into out_split[f][b]; fold_splits_body then folds the nsplit values of
+// each group.  Same combine operators, a fixed (shape-determined) order.
+CUBED_DEV void fold_groups_split_body(
+    const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
+    int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
+    int64_t nsplit, Acc* __restrict__ out_split, int kd0, int kd1) {
+  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
+  const int64_t b = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  if (b >= ngroups * nsplit) return;
+  const int64_t g = b / nsplit, sp = b - g * nsplit;
+  const int64_t n = ntasks * max_kept;
+  Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
+  for (int64_t t = gs[g] + sp; t < gs[g + 1]; t += nsplit) {
+    const cubed_task_t* __restrict__ T = tasks + t;
+    int64_t nk = 1;
+    for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
+    for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) red[wave][f] = a[f];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-      Acc x = red[0][f];
-      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
-      out[f * ngroups + g] = x;
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < P.nfields)
+          a[f] = acc_combine(a[f], soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
     }
   }
+  block_fold_store(P, a, red, out_split, ngroups * nsplit, b);
+}
+
+CUBED_DEV void fold_splits_body(const cubed_program_t& P, const Acc* __restrict__ in_split,
+                                int64_t ngroups, int64_t nsplit, Acc* __restrict__ out) {
+  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
+  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  if (g >= ngroups) return;
+  const int64_t ns = ngroups * nsplit;
+  Acc a[CUBED_MAX_FIELDS];
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
+  for (int64_t s = threadIdx.x; s < nsplit; s += kBlock) {
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+      if (f < P.nfields)
+        a[f] = acc_combine(a[f], in_split[f * ns + g * nsplit + s], P.field_rop[f], P.field_acc[f]);
+  }
+  block_fold_store(P, a, red, out, ngroups, g);
 }
 
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in

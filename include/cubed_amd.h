@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 6
+#define CUBED_ABI_VERSION 7
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -269,7 +269,12 @@ int cubed_combine_groups(const cubed_program_t* prog, const cubed_program_t* d_p
 int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
                       const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                       const void* d_row_partials, const int64_t* d_group_start,
-                      int64_t ngroups, void* d_group_partials, void* stream);
+                      int64_t ngroups, void* d_group_partials, int64_t nsplit,
+                      void* d_split_ws, void* stream);
+/* Splits per group cubed_fold_groups should use (few groups of many rows:
+ * each group's rows spread over nsplit workgroups, then folded); d_split_ws
+ * then holds nfields x ngroups x nsplit 8-byte accumulators. */
+int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);

@@ -21,8 +21,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #define G __attribute__((address_space(1)))
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
-template <int UN, bool NT>
-__global__ __launch_bounds__(256) void k_seg(const u32x4* __restrict__ src, u32x4* __restrict__ dst, long nw, long segs_per_block) {
+template <int UN, bool NT, int WAVES = 4>
+__global__ __launch_bounds__(WAVES * 64) void k_seg(const u32x4* __restrict__ src, u32x4* __restrict__ dst, long nw, long segs_per_block) {
   constexpr long kSeg = 64 * UN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const long w0 = (long)blockIdx.x * segs_per_block * kSeg;
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_seg(const u32x4* __restrict__ src, u32x
   if (w1 > nw) w1 = nw;
   const G u32x4* s = (const G u32x4*)src;
   G u32x4* d = (G u32x4*)dst;
-  for (long i0 = w0 + wave * kSeg; i0 < w1; i0 += 4 * kSeg) {
+  for (long i0 = w0 + wave * kSeg; i0 < w1; i0 += WAVES * kSeg) {
     u32x4 v[UN];
 #pragma unroll
     for (int k = 0; k < UN; ++k) {
@@ -43,6 +43,22 @@ __global__ __launch_bounds__(256) void k_seg(const u32x4* __restrict__ src, u32x
       if (i < w1) { if (NT) __builtin_nontemporal_store(v[k], d + i); else d[i] = v[k]; }
     }
   }
+}
+
+// read-only stream (xor-reduce, one store per lane) and write-only fill:
+// the two halves of a copy measured alone
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ src, u32x4* __restrict__ out, long nw) {
+  const G u32x4* s = (const G u32x4*)src;
+  u32x4 acc = {0, 0, 0, 0};
+  const long n0 = (long)blockIdx.x * 4096;
+  for (long i = n0 + threadIdx.x; i < n0 + 4096 && i < nw; i += 256) acc ^= __builtin_nontemporal_load(s + i);
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[threadIdx.x] = acc;
+}
+__global__ __launch_bounds__(256) void k_write(u32x4* __restrict__ dst, long nw) {
+  G u32x4* d = (G u32x4*)dst;
+  const long n0 = (long)blockIdx.x * 4096;
+  const u32x4 v = {1u, 2u, 3u, (unsigned)blockIdx.x};
+  for (long i = n0 + threadIdx.x; i < n0 + 4096 && i < nw; i += 256) __builtin_nontemporal_store(v, d + i);
 }
 
 // persistent: wave-contiguous runs, register double buffer
@@ -196,6 +212,26 @@ int main(int argc, char** argv) {
       ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16; long per = c->spb * 256;
         hipLaunchKernelGGL((k_seg<4, false>), dim3((nw + per - 1) / per), dim3(256), 0, 0, (const u32x4*)c->src, (u32x4*)c->dst, nw, c->spb); }, &c, 5);
       printf("A' contiguous UN4 plain spb%ld: %.3f ms %.0f GB/s\n", spb, ms, gb / ms * 1e3);
+    }
+    {
+      c.spb = 16;
+      float ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16; long per = c->spb * 256;
+        hipLaunchKernelGGL((k_seg<4, true, 8>), dim3((nw + per - 1) / per), dim3(512), 0, 0, (const u32x4*)c->src, (u32x4*)c->dst, nw, c->spb); }, &c, 5);
+      printf("E contiguous UN4 nt 512-thread WG spb16: %.3f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+      ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16; long per = c->spb * 256;
+        hipLaunchKernelGGL((k_seg<4, true, 16>), dim3((nw + per - 1) / per), dim3(1024), 0, 0, (const u32x4*)c->src, (u32x4*)c->dst, nw, c->spb); }, &c, 5);
+      printf("E' contiguous UN4 nt 1024-thread WG spb16: %.3f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+      ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16; long per = c->spb * 128;
+        hipLaunchKernelGGL((k_seg<2, true, 4>), dim3((nw + per - 1) / per), dim3(256), 0, 0, (const u32x4*)c->src, (u32x4*)c->dst, nw, c->spb); }, &c, 5);
+      printf("E'' contiguous UN2 nt spb16: %.3f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+      ms = timeit([](void* x) { Ctx* c = (Ctx*)x; CHECK(hipMemcpyAsync(c->dst, c->src, c->nbytes, hipMemcpyDeviceToDevice, 0)); }, &c, 5);
+      printf("H hipMemcpyAsync D2D: %.3f ms %.0f GB/s\n", ms, gb / ms * 1e3);
+      ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16;
+        hipLaunchKernelGGL(k_read, dim3((nw + 4095) / 4096), dim3(256), 0, 0, (const u32x4*)c->src, (u32x4*)c->dst, nw); }, &c, 5);
+      printf("F read-only stream: %.3f ms %.0f GB/s (bytes read)\n", ms, gb / 2 / ms * 1e3);
+      ms = timeit([](void* x) { Ctx* c = (Ctx*)x; long nw = c->nbytes / 16;
+        hipLaunchKernelGGL(k_write, dim3((nw + 4095) / 4096), dim3(256), 0, 0, (u32x4*)c->dst, nw); }, &c, 5);
+      printf("G write-only fill: %.3f ms %.0f GB/s (bytes written)\n", ms, gb / 2 / ms * 1e3);
     }
     for (int wpc : {4, 8, 16}) {
       c.spb = wpc;
