@@ -91,7 +91,13 @@ class Array(CoreArray):
     def __abs__(self, /):
         if self.dtype not in _numeric_dtypes:
             raise TypeError("Only numeric dtypes are allowed in __abs__")
-        return elemwise("abs", self, dtype=self.dtype)
+        dtype = np.dtype(f"f{self.dtype.itemsize // 2}") if self.dtype.kind == "c" else self.dtype
+        return elemwise("abs", self, dtype=dtype)
+
+    def __complex__(self, /):
+        if self.ndim != 0:
+            raise TypeError("complex is only allowed on arrays with 0 dimensions")
+        return complex(self.compute())
 
     def __invert__(self, /):
         if self.dtype not in _dtype_categories["integer or boolean"]:
@@ -101,6 +107,8 @@ class Array(CoreArray):
     def __float__(self, /):
         if self.ndim != 0:
             raise TypeError("float is only allowed on arrays with 0 dimensions")
+        if self.dtype.kind == "c":
+            raise TypeError("float is not allowed on complex floating-point arrays")
         return float(self.compute())
 
     def __int__(self, /):

@@ -68,7 +68,35 @@ def _binary(name, cat, rule="promote", op=None):
     return f
 
 
-abs = _unary("abs", "numeric")
+_complex_cat = ((np.dtype("complex64"), np.dtype("complex128")), "complex floating-point")
+
+
+def _part_dtype(dt):
+    return np.dtype(f"f{np.dtype(dt).itemsize // 2}")
+
+
+def abs(x, /):
+    """|x|; complex arrays give their part dtype (elementwise_functions.py:22-31)."""
+    _check("abs", "numeric", x)
+    dtype = _part_dtype(x.dtype) if x.dtype.kind == "c" else x.dtype
+    return elemwise("abs", x, dtype=dtype)
+
+
+def _complex_only(name, part_result):
+    def f(x, /):
+        if x.dtype not in _complex_cat[0]:
+            raise TypeError(f"Only complex floating-point dtypes are allowed in {name}")
+        return elemwise(name, x, dtype=_part_dtype(x.dtype) if part_result else x.dtype)
+
+    f.__name__ = name
+    f.__doc__ = (f"Elementwise ``{name}`` of a complex array (elementwise_functions.py); "
+                 "computed on its real/imaginary slabs (cubed_amd/complex.py).")
+    return f
+
+
+conj = _complex_only("conj", False)
+real = _complex_only("real", True)
+imag = _complex_only("imag", True)
 acos = _unary("acos", "floating")
 acosh = _unary("acosh", "floating")
 asin = _unary("asin", "floating")

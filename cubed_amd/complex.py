@@ -1,0 +1,342 @@
+"""Complex dtypes (complex64 / complex128) on the MI355X path.
+
+The reference computes complex chunks with numpy (array_api/dtypes.py
+complex64/complex128; elementwise_functions.py real/imag/conj/abs and the
+arithmetic operators; statistical_functions.py sum/prod promoting complex64
+to complex128; nan_functions.py nansum).  Here a complex array is stored
+as two HBM slabs per chunk -- the ``real`` and ``imag`` parts, each a real
+array of the part dtype (f32 / f64), the same SoA layout as the structured
+reduction intermediates (storage.DeviceArray) -- and every chunk program
+that touches complex values is rewritten, before lowering, into a program
+over real expressions (``split_program``): a complex leaf becomes its two
+part leaves, complex arithmetic becomes the real formulas numpy evaluates
+(npymath's nc_sum/nc_diff/nc_prod and Smith's division, hypot for abs), a
+complex output becomes the structured output {real, imag}, and a complex
+reduction field becomes one field per part.  Layout copies (rechunk, index,
+concat) move each part slab.
+
+Ops with no real-pair form here (complex powers, trigonometric functions,
+ordering comparisons, prod over complex values) raise LoweringError.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, Optional, Tuple, Union
+
+import numpy as np
+
+from . import ir
+
+PARTS = ("real", "imag")
+
+
+def is_complex(dt) -> bool:
+    return np.dtype(dt).kind == "c"
+
+
+def part_dtype(dt) -> np.dtype:
+    """complex64 -> float32, complex128 -> float64."""
+    dt = np.dtype(dt)
+    return np.dtype(f"f{dt.itemsize // 2}")
+
+
+def complex_dtype(part) -> np.dtype:
+    return np.dtype(f"c{np.dtype(part).itemsize * 2}")
+
+
+class ComplexLoweringError(Exception):
+    pass
+
+
+def _err(msg):
+    from .lowering import LoweringError
+
+    return LoweringError(msg)
+
+
+# a decomposed value: ("r", expr) or ("c", re, im)
+Val = Union[Tuple[str, ir.Expr], Tuple[str, ir.Expr, ir.Expr]]
+
+
+def _bin(op, a, b, dt):
+    return ir.Binary(op, a, b, np.dtype(dt))
+
+
+def _un(op, a, dt):
+    return ir.Unary(op, a, np.dtype(dt))
+
+
+def _const(v, dt):
+    return ir.Const(np.array(v, dtype=dt).item(), np.dtype(dt))
+
+
+class _Splitter:
+    def __init__(self):
+        self.memo: Dict[int, Val] = {}
+
+    def pair(self, e: ir.Expr, part) -> Tuple[ir.Expr, ir.Expr]:
+        """(re, im) of e as values of dtype ``part`` (a real e gets im = 0)."""
+        v = self.split(e)
+        if v[0] == "c":
+            return ir.cast(v[1], part), ir.cast(v[2], part)
+        return ir.cast(v[1], part), _const(0, part)
+
+    def split(self, e: ir.Expr) -> Val:
+        key = id(e)
+        if key in self.memo:
+            return self.memo[key]
+        out = self._split(e)
+        self.memo[key] = out
+        return out
+
+    def _split(self, e: ir.Expr) -> Val:
+        dt = np.dtype(e.dtype)
+        if isinstance(e, ir.Const):
+            if is_complex(dt):
+                v = complex(e.value)
+                p = part_dtype(dt)
+                return ("c", _const(v.real, p), _const(v.imag, p))
+            return ("r", e)
+        if isinstance(e, ir.Field):
+            if is_complex(dt):
+                p = part_dtype(dt)
+                return ("c", ir.Field(e.name + "#re", p), ir.Field(e.name + "#im", p))
+            return ("r", e)
+        if isinstance(e, (ir.Arg, ir.Region)):  # incl. ReshapeArg, Concat
+            if is_complex(dt):
+                if e.field is not None:
+                    raise _err("complex fields of structured arrays are not lowered")
+                p = part_dtype(dt)
+                return ("c", dataclasses.replace(e, dtype=p, field="real"),
+                        dataclasses.replace(e, dtype=p, field="imag"))
+            return ("r", e)
+        if isinstance(e, ir.LEAF_TYPES):
+            return ("r", e)
+        if isinstance(e, ir.Cast):
+            return self._cast(e)
+        if isinstance(e, ir.Where):
+            c = self.split(e.c)
+            if c[0] == "c":
+                raise _err("a complex where() condition")
+            if is_complex(dt):
+                p = part_dtype(dt)
+                ar, ai = self.pair(e.a, p)
+                br, bi = self.pair(e.b, p)
+                return ("c", ir.Where(c[1], ar, br, p), ir.Where(c[1], ai, bi, p))
+            return ("r", ir.Where(c[1], self.real(e.a), self.real(e.b), dt))
+        if isinstance(e, ir.Unary):
+            return self._unary(e)
+        if isinstance(e, ir.Binary):
+            return self._binary(e)
+        raise _err(f"complex rewrite: unknown node {type(e).__name__}")
+
+    def real(self, e):
+        v = self.split(e)
+        if v[0] == "c":
+            raise _err("a complex value where a real one is required")
+        return v[1]
+
+    def _cast(self, e: ir.Cast) -> Val:
+        dt = np.dtype(e.dtype)
+        v = self.split(e.x)
+        if is_complex(dt):
+            p = part_dtype(dt)
+            re, im = self.pair(e.x, p)
+            return ("c", re, im)
+        if v[0] == "r":
+            return ("r", ir.cast(v[1], dt))
+        # complex -> real (numpy discards the imaginary part); -> bool: z != 0
+        if dt.kind == "b":
+            p = np.dtype(v[1].dtype)
+            z = _const(0, p)
+            return ("r", _bin("logical_or", _bin("not_equal", v[1], z, np.bool_),
+                              _bin("not_equal", v[2], z, np.bool_), np.bool_))
+        return ("r", ir.cast(v[1], dt))
+
+    def _unary(self, e: ir.Unary) -> Val:
+        v = self.split(e.x)
+        if v[0] == "r":
+            if e.op == "conj":
+                return ("r", e.x if np.dtype(e.x.dtype) == np.dtype(e.dtype) else ir.cast(e.x, e.dtype))
+            if e.op in ("real",):
+                return ("r", ir.cast(e.x, e.dtype))
+            if e.op == "imag":
+                return ("r", _const(0, e.dtype))
+            return ("r", e)
+        _, re, im = v
+        p = np.dtype(re.dtype)
+        op = e.op
+        if op in ("negative",):
+            return ("c", _un("negative", re, p), _un("negative", im, p))
+        if op in ("positive",):
+            return ("c", re, im)
+        if op == "conj":
+            return ("c", re, _un("negative", im, p))
+        if op == "real":
+            return ("r", re)
+        if op == "imag":
+            return ("r", im)
+        if op == "abs":
+            return ("r", _bin("hypot", re, im, p))
+        if op == "isnan":
+            return ("r", _bin("logical_or", _un("isnan", re, np.bool_), _un("isnan", im, np.bool_), np.bool_))
+        if op == "isinf":
+            return ("r", _bin("logical_or", _un("isinf", re, np.bool_), _un("isinf", im, np.bool_), np.bool_))
+        if op == "isfinite":
+            return ("r", _bin("logical_and", _un("isfinite", re, np.bool_), _un("isfinite", im, np.bool_),
+                              np.bool_))
+        if op == "square":
+            return self._mul(re, im, re, im, p)
+        if op == "reciprocal":
+            return self._div(_const(1, p), _const(0, p), re, im, p)
+        if op == "exp":
+            # npy_cexp for finite values: exp(re) * (cos im, sin im); a zero
+            # imaginary part stays exact (exp(inf + 0j) = inf + 0j)
+            r = _un("exp", re, p)
+            cr = _bin("multiply", r, _un("cos", im, p), p)
+            ci = _bin("multiply", r, _un("sin", im, p), p)
+            zero = _bin("equal", im, _const(0, p), np.bool_)
+            return ("c", ir.Where(zero, r, cr, p), ir.Where(zero, im, ci, p))
+        if op == "log":
+            return ("c", _un("log", _bin("hypot", re, im, p), p), _bin("atan2", im, re, p))
+        if op == "sqrt":
+            return self._sqrt(re, im, p)
+        if op == "sign":
+            # numpy 2: z / |z|, 0 at 0
+            a = _bin("hypot", re, im, p)
+            z = _bin("equal", a, _const(0, p), np.bool_)
+            return ("c", ir.Where(z, _const(0, p), _bin("divide", re, a, p), p),
+                    ir.Where(z, _const(0, p), _bin("divide", im, a, p), p))
+        raise _err(f"complex {op} is not lowered on the MI355X executor")
+
+    def _sqrt(self, re, im, p) -> Val:
+        # npy_csqrt (principal branch): t = sqrt((|re| + |z|) / 2);
+        # re >= 0: (t, im / 2t); re < 0: (|im| / 2t, copysign(t, im)); z = 0: (0, im)
+        a = _bin("hypot", re, im, p)
+        t = _un("sqrt", _bin("multiply", _bin("add", _un("abs", re, p), a, p), _const(0.5, p), p), p)
+        t2 = _bin("multiply", t, _const(2, p), p)
+        pos = _bin("greater_equal", re, _const(0, p), np.bool_)
+        zero = _bin("equal", a, _const(0, p), np.bool_)
+        r_pos, i_pos = t, _bin("divide", im, t2, p)
+        r_neg, i_neg = _bin("divide", _un("abs", im, p), t2, p), _bin("copysign", t, im, p)
+        rr = ir.Where(zero, _const(0, p), ir.Where(pos, r_pos, r_neg, p), p)
+        ii = ir.Where(zero, im, ir.Where(pos, i_pos, i_neg, p), p)
+        return ("c", rr, ii)
+
+    def _mul(self, ar, ai, br, bi, p) -> Val:
+        # nc_prod: (ar*br - ai*bi, ar*bi + ai*br)
+        return ("c", _bin("subtract", _bin("multiply", ar, br, p), _bin("multiply", ai, bi, p), p),
+                _bin("add", _bin("multiply", ar, bi, p), _bin("multiply", ai, br, p), p))
+
+    def _div(self, ar, ai, br, bi, p) -> Val:
+        # numpy's complex division (Smith's algorithm, loops.c.src):
+        # |br| >= |bi|: rat = bi/br, scl = 1/(br + bi*rat),
+        #               ((ar + ai*rat)*scl, (ai - ar*rat)*scl)   [br = bi = 0: (ar/|br|, ai/|bi|)]
+        # else:         rat = br/bi, scl = 1/(bi + br*rat),
+        #               ((ar*rat + ai)*scl, (ai*rat - ar)*scl)
+        abr, abi = _un("abs", br, p), _un("abs", bi, p)
+        first = _bin("greater_equal", abr, abi, np.bool_)
+        one = _const(1, p)
+        rat1 = _bin("divide", bi, br, p)
+        scl1 = _bin("divide", one, _bin("add", br, _bin("multiply", bi, rat1, p), p), p)
+        r1 = _bin("multiply", _bin("add", ar, _bin("multiply", ai, rat1, p), p), scl1, p)
+        i1 = _bin("multiply", _bin("subtract", ai, _bin("multiply", ar, rat1, p), p), scl1, p)
+        rat2 = _bin("divide", br, bi, p)
+        scl2 = _bin("divide", one, _bin("add", bi, _bin("multiply", br, rat2, p), p), p)
+        r2 = _bin("multiply", _bin("add", _bin("multiply", ar, rat2, p), ai, p), scl2, p)
+        i2 = _bin("multiply", _bin("subtract", _bin("multiply", ai, rat2, p), ar, p), scl2, p)
+        both0 = _bin("logical_and", _bin("equal", abr, _const(0, p), np.bool_),
+                     _bin("equal", abi, _const(0, p), np.bool_), np.bool_)
+        r0, i0 = _bin("divide", ar, abr, p), _bin("divide", ai, abi, p)
+        re = ir.Where(both0, r0, ir.Where(first, r1, r2, p), p)
+        im = ir.Where(both0, i0, ir.Where(first, i1, i2, p), p)
+        return ("c", re, im)
+
+    def _binary(self, e: ir.Binary) -> Val:
+        va, vb = self.split(e.a), self.split(e.b)
+        if va[0] == "r" and vb[0] == "r":
+            return ("r", e)
+        dt = np.dtype(e.dtype)
+        ct = dt if is_complex(dt) else np.result_type(
+            *[x.dtype for x in (e.a, e.b)])
+        if not is_complex(ct):
+            raise _err(f"complex operand of {e.op} with a real result")
+        p = part_dtype(ct)
+        ar, ai = self.pair(e.a, p)
+        br, bi = self.pair(e.b, p)
+        op = e.op
+        if op in ("add", "subtract"):
+            return ("c", _bin(op, ar, br, p), _bin(op, ai, bi, p))
+        if op == "multiply":
+            return self._mul(ar, ai, br, bi, p)
+        if op == "divide":
+            return self._div(ar, ai, br, bi, p)
+        if op == "equal":
+            return ("r", _bin("logical_and", _bin("equal", ar, br, np.bool_), _bin("equal", ai, bi, np.bool_),
+                              np.bool_))
+        if op == "not_equal":
+            return ("r", _bin("logical_or", _bin("not_equal", ar, br, np.bool_),
+                              _bin("not_equal", ai, bi, np.bool_), np.bool_))
+        raise _err(f"complex {op} is not lowered on the MI355X executor")
+
+
+def program_has_complex(p) -> bool:
+    if not isinstance(p, ir.ExprProgram):
+        return False
+    seen = set()
+
+    def walk(e):
+        if id(e) in seen:
+            return False
+        seen.add(id(e))
+        if is_complex(e.dtype):
+            return True
+        return any(walk(c) for c in e.children())
+
+    if any(walk(e) for e in p.all_exprs()):
+        return True
+    return p.reduce is not None and any(is_complex(f.dtype) for f in p.reduce.fields)
+
+
+def split_program(p: ir.ExprProgram) -> ir.ExprProgram:
+    """The program over real expressions that computes ``p``'s complex values
+    part by part (unchanged when ``p`` has no complex value)."""
+    if not program_has_complex(p):
+        return p
+    s = _Splitter()
+    reduce = p.reduce
+    if reduce is not None:
+        fields = []
+        for f in reduce.fields:
+            v = s.split(f.expr)
+            if not is_complex(f.dtype):
+                if v[0] == "c":
+                    raise _err(f"a complex value reduced into the real field {f.name}")
+                fields.append(dataclasses.replace(f, expr=v[1]))
+                continue
+            if f.rop not in ("sum", "nansum"):
+                raise _err(f"{f.rop} of complex values is not lowered (sum/nansum are)")
+            pt = part_dtype(f.dtype)
+            re, im = s.pair(f.expr, pt)
+            rop = f.rop
+            if rop == "nansum":
+                # numpy's nansum drops an element whose real OR imaginary part is NaN
+                nan = _bin("logical_or", _un("isnan", re, np.bool_), _un("isnan", im, np.bool_), np.bool_)
+                re, im = ir.Where(nan, _const(0, pt), re, pt), ir.Where(nan, _const(0, pt), im, pt)
+                rop = "sum"
+            fields.append(ir.ReduceField(f.name + "#re", rop, re, pt))
+            fields.append(ir.ReduceField(f.name + "#im", rop, im, pt))
+        reduce = dataclasses.replace(reduce, fields=tuple(fields))
+    if p.structured:
+        items = []
+        for name, e in p.outputs:
+            v = s.split(e)
+            if v[0] == "c":
+                raise _err("complex fields of structured outputs are not lowered")
+            items.append((name, v[1]))
+        outputs = tuple(items)
+    else:
+        v = s.split(p.outputs)
+        outputs = (("real", v[1]), ("imag", v[2])) if v[0] == "c" else v[1]
+    return dataclasses.replace(p, outputs=outputs, reduce=reduce)

@@ -687,6 +687,17 @@ def reduction(x: "Array", func, combine_func=None, aggegrate_func=None, axis=Non
                             f"Not enough memory for reduction. Increase allowed_mem ({allowed_mem}) "
                             "or decrease chunk size")
                     target_chunks[i] = min(s, target_chunk_size)
+        if all(target_chunks[i] == result.chunksize[i] for i in axis):
+            # multi-axis with unit source chunks along a reduced axis: the
+            # per-axis target above would merge nothing (and loop forever);
+            # merge along the first unfinished axis by the memory bound
+            i = next(i for i in axis if result.numblocks[i] > 1)
+            target_chunk_size = (max_mem - chunk_mem) // (chunk_mem * 4)
+            if target_chunk_size <= 1:
+                raise ValueError(
+                    f"Not enough memory for reduction. Increase allowed_mem ({allowed_mem}) "
+                    "or decrease chunk size")
+            target_chunks[i] = min(result.shape[i], target_chunk_size)
         result = merge_chunks(result, tuple(target_chunks))
         if any(s > 1 for i, s in enumerate(result.chunksize) if i in axis):
             adjust_chunks = {i: (1,) * len(c) if i in axis else c for i, c in enumerate(result.chunks)}

@@ -18,7 +18,11 @@
 //                      128 x 64 = 8 x 4 accumulators), K staged 32 deep
 //                      straight from HBM into LDS with global_load_lds
 //                      (16 B per lane) through a 4-slot ring: three K steps
-//                      in flight while the fourth feeds the MFMAs.
+//                      in flight while the fourth feeds the MFMAs.  The two
+//                      wave rows run "ping-pong", one barrier apart: on each
+//                      SIMD one wave issues its 32 MFMAs while the other
+//                      reads the next step's fragments and issues the
+//                      staging loads.
 //                      A is staged k-contiguous [m][64] (XOR-swizzled 16-B
 //                      chunks, conflict-free ds_read_b128 fragments); B is
 //                      staged as it lies in HBM, [k][256] rows, and read
@@ -112,15 +116,17 @@ __device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
 // 1 = no K-loop staging, 2 = no B fragment reads, 4 = no A fragment reads,
 // 8 = no K-loop barrier.  Any nonzero value computes wrong results.
 // PP: ping-pong schedule (see the K loop).
-template <bool OUT_BF16, int ABL = 0, bool PP = false>
+// NS: ring slots (each step p+NS-1 is staged while step p is consumed);
+// GM: tile rows per XCD tile group.
+template <bool OUT_BF16, int ABL = 0, bool PP = false, int NS = HB_NS, int GM = 4>
 __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                          const cubed_gemm_seg_t* __restrict__ segs,
                                                          int64_t tiles_m, int64_t tiles_n,
                                                          const char* __restrict__ zero) {
-  __shared__ __attribute__((aligned(1024))) char lds_[HB_NS * HB_STAGE];
+  __shared__ __attribute__((aligned(1024))) char lds_[NS * HB_STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
-  tile_of<HB_BM, HB_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  tile_of<HB_BM, HB_BN, GM>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
   const int64_t M = T->m, N = T->n, KT = T->ktot;
   if (m0 >= M || n0 >= N) return;
@@ -228,15 +234,20 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   bf16x8 bf[4];
 
   const int64_t nst = (KT + HB_BK - 1) / HB_BK;
-  // prologue: steps 0, 1, 2 in flight
-  for (int64_t p = 0; p < 3 && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
-  // retire this wave's loads of step q (4 per step; steps up to q + 2 issued)
+  constexpr int D = NS - 1;  // steps staged ahead
+  // prologue: steps 0 .. D-1 in flight
+  for (int64_t p = 0; p < D && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
+  // retire this wave's loads of step q (4 per step; steps up to q + D - 1 issued)
   auto wait_step = [&](int64_t q) {
-    const int64_t younger = nst - 1 - q;
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    int64_t younger = nst - 1 - q;
+    if (younger > D - 1) younger = D - 1;
+    if (younger >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
+  static_assert(NS >= 3 && NS <= 5, "ring of 3..5 slots");
+  int rd = 0, wr_slot = D % NS;  // ring slots of steps p and p + D
   if constexpr (PP) {
     // Ping-pong: the two wave rows (wr = 0, 1: one wave of each per SIMD)
     // run one barrier-delimited slot apart, alternating a memory slot M(p)
@@ -257,7 +268,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
     bf16x8 af[8];
     for (int64_t p = 0; p < nst; ++p) {
       // ---- M(p)
-      const CUBED_L char* bufc = lds + (p & (HB_NS - 1)) * HB_STAGE;
+      const CUBED_L char* bufc = lds + rd * HB_STAGE;
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) {
         const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
@@ -268,7 +279,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
       }
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb) af[mb] = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
-      if (p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
+      if (p + D < nst) stage((p + D) * HB_BK, lds + wr_slot * HB_STAGE);
+      rd = rd + 1 == NS ? 0 : rd + 1;
+      wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (p + 1 < nst) wait_step(p + 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -289,17 +302,16 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   for (int64_t p = 0; p < nst; ++p) {
     // this wave's loads of step p have landed once at most the younger
     // steps' loads (4 per step) are outstanding
-    const int64_t younger = nst - 1 - p;
     if (ABL & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else wait_step(p);
     // every wave's step p landed; every wave finished reading step p-1's slot
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (!(ABL & 8)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (!(ABL & 1) && p + 3 < nst) stage((p + 3) * HB_BK, lds + ((p + 3) & (HB_NS - 1)) * HB_STAGE);
-    const CUBED_L char* bufc = lds + (p & (HB_NS - 1)) * HB_STAGE;
+    if (!(ABL & 1) && p + D < nst) stage((p + D) * HB_BK, lds + wr_slot * HB_STAGE);
+    const CUBED_L char* bufc = lds + rd * HB_STAGE;
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
     // B fragments by transposed reads.  Inline asm: the builtin has no memory
     // operand, so hipcc would put an s_waitcnt vmcnt(0) in front of it --
     // draining the three K steps in flight -- and the reads only touch slot
@@ -641,10 +653,12 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     if (blocks > 0x7fffffff) return fail("grid too large");
     const dim3 grid((unsigned)blocks), blk(512);
     const char* z = (const char*)d_zero;
+    // ping-pong schedule: 1072-1098 TF vs 1021-1041 for the single-slot loop
+    // on config 5 (profiles/r02_gemm_bf16_variants.log)
     if (out_dtype == CUBED_BF16)
-      hipLaunchKernelGGL(k_gemm_bf16_chain<true>, grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
+      hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
     else
-      hipLaunchKernelGGL(k_gemm_bf16_chain<false>, grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
+      hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
   } else if (path == CUBED_GEMM_MFMA && in_dtype == CUBED_F32) {
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
     const int64_t blocks = ntasks * tm * tn;

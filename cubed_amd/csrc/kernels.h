@@ -694,8 +694,7 @@ CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
         else ld4c<V>(inv[l], p[l]);
       }
   }
-  for (; r + U <= hi; r += U) {
-    V buf[U][NL][4];
+  auto load_batch = [&](V (&buf)[U][NL][4]) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -709,14 +708,25 @@ CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
         }
       }
 #pragma unroll
+    for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
+  };
+  auto reduce_batch = [&](V (&buf)[U][NL][4]) {
+#pragma unroll
     for (int u = 0; u < U; ++u) {
       set_leaves<NL, V>(regs, buf[u]);
       CUBED_RUN_PROLOGUE(V, 4, regs);
       accumulate_nocount<V>(acc, regs, P);
     }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
+  };
+  // (a software-pipelined form -- batch r + U loading while batch r reduces --
+  // and U = 2 / 8 measured equal or slower on quad-means, config 1 and
+  // vorticity: profiles/r02_stream_ab.log)
+  for (; r + U <= hi; r += U) {
+    V buf[U][NL][4];
+    load_batch(buf);
+    reduce_batch(buf);
   }
+
   for (; r < hi; ++r) {
     V buf[NL][4];
 #pragma unroll

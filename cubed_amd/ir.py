@@ -108,6 +108,8 @@ BINARY_OPS = {
 COMPARISONS = {"equal", "not_equal", "less", "less_equal", "greater", "greater_equal",
                "logical_and", "logical_or", "logical_xor"}
 UNARY_BOOL_RESULT = {"isnan", "isinf", "isfinite", "logical_not", "signbit"}
+# complex-only elementwise functions (no VM opcode: rewritten by complex.py)
+COMPLEX_PARTS_OPS = {"conj", "real", "imag"}
 
 # reduction ops (enum cubed_rop)
 ROPS = {"sum": 1, "nansum": 2, "count": 3, "count_nonnan": 4, "max": 5, "min": 6,
@@ -484,10 +486,16 @@ def apply_op(op: str, xs: Sequence[Expr], out_dtype, compute_dtype=None) -> Expr
         return Where(cast(c, np.bool_), cast(a, ct), cast(b, ct), ct)
     if op == "astype":
         return cast(xs[0], out_dtype)
+    if op in COMPLEX_PARTS_OPS:
+        # complex -> part / conjugate: computed on the complex value itself
+        # (cubed_amd/complex.py rewrites it into real expressions)
+        return Unary(op, xs[0], out_dtype)
     if op in UNARY_OPS:
         x = xs[0]
         if op == "positive":
             return cast(x, out_dtype)
+        if op == "abs" and np.dtype(x.dtype).kind == "c":
+            return Unary(op, x, out_dtype)  # |z|, a real result
         if op in UNARY_BOOL_RESULT:
             return Unary(op, x, np.dtype(np.bool_))
         ct = np.dtype(compute_dtype) if compute_dtype is not None else out_dtype
@@ -708,6 +716,9 @@ def _np_name_map():
     m[np.round] = "round"
     m[np.true_divide] = "divide"
     m[np.absolute] = "abs"
+    m[np.conj] = m[np.conjugate] = "conj"
+    m[np.real] = "real"
+    m[np.imag] = "imag"
     return m
 
 

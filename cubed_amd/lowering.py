@@ -1011,9 +1011,14 @@ class Lowerer:
         else:
             return None
         if isinstance(arr, VirtualFullArray):
-            return arr.fill_value
+            v = arr.fill_value
+            if np.dtype(arr.dtype).kind == "c" and leaf.field in ("real", "imag"):
+                return getattr(complex(v), leaf.field)
+            return v
         if isinstance(arr, VirtualInMemoryArray) and arr.array.size == 1:
             v = arr.array.reshape(-1)[0]
+            if np.dtype(arr.dtype).kind == "c" and leaf.field in ("real", "imag"):
+                return getattr(v, leaf.field).item()
             if leaf.field is not None:
                 v = v[leaf.field]
             return v.item()

@@ -130,3 +130,25 @@ def elide_rechunks(dag, array_names):
                 dag.remove_node(n2)
             dag.add_edge(x_name, name)
     return dag, elided
+
+
+def split_complex(dag):
+    """Every blockwise program that computes complex values rewritten into
+    real expressions over the values' real / imaginary slabs
+    (cubed_amd/complex.py).  Returns the DAG (a copy when anything changed)."""
+    from .complex import program_has_complex, split_program
+
+    todo = [n for n, d in dag.nodes(data=True)
+            if "pipeline" in d and d["pipeline"].function is apply_blockwise
+            and program_has_complex(d["pipeline"].config.function)]
+    if not todo:
+        return dag
+    dag = dag.copy()
+    for name in todo:
+        nd = dag.nodes[name]
+        spec = nd["pipeline"].config
+        spec = dataclasses.replace(spec, function=split_program(spec.function))
+        pipeline = dataclasses.replace(nd["pipeline"], config=spec)
+        nd["pipeline"] = pipeline
+        nd["primitive_op"] = dataclasses.replace(nd["primitive_op"], pipeline=pipeline)
+    return dag

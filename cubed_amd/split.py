@@ -138,7 +138,7 @@ def _space_geometry(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys)
     ident = tuple(range(program.ndim))
     ref = None
     for leaf in collect_leaves(_pre_exprs(program)):
-        if type(leaf) is ir.Arg and tuple(leaf.axes) == ident and leaf.field is None:
+        if type(leaf) is ir.Arg and tuple(leaf.axes) == ident:  # any field: same geometry
             ref = leaf
             break
     if ref is None:

@@ -116,8 +116,11 @@ class DeviceArray(ChunkGrid):
     def __init__(self, shape, dtype, chunks, name: Optional[str] = None):
         super().__init__(shape, dtype, chunks)
         self.name = name
+        # structured dtypes: one slab per field; complex: a real and an
+        # imaginary slab (cubed_amd/complex.py)
         self.fields: Tuple[Optional[str], ...] = (
-            tuple(self.dtype.names) if self.dtype.names else (None,))
+            tuple(self.dtype.names) if self.dtype.names else
+            ("real", "imag") if self.dtype.kind == "c" else (None,))
         self.slabs: Dict[Optional[str], object] = {}
         self.rank, self.world = 0, 1
         self.written = False
@@ -132,6 +135,8 @@ class DeviceArray(ChunkGrid):
     def field_dtype(self, field: Optional[str]) -> np.dtype:
         if field is None:
             return self.dtype
+        if self.dtype.kind == "c":
+            return np.dtype(f"f{self.dtype.itemsize // 2}")
         return self.dtype.fields[field][0]
 
     @property
@@ -208,6 +213,11 @@ class DeviceArray(ChunkGrid):
         return raw, dt
 
     def read_chunk(self, coords, field=None) -> np.ndarray:
+        if field is None and self.dtype.kind == "c":
+            out = np.empty(self.chunk_extent(coords), dtype=self.dtype)
+            out.real = self.read_chunk(coords, "real")
+            out.imag = self.read_chunk(coords, "imag")
+            return out
         ext = self.chunk_extent(coords)
         raw, dt = self._slab_view(field, self.local_slot(coords), ext)
         host = raw.cpu().numpy()
@@ -215,6 +225,12 @@ class DeviceArray(ChunkGrid):
 
     def write_chunk(self, coords, value: np.ndarray, field=None):
         import torch
+
+        if field is None and self.dtype.kind == "c":
+            v = np.asarray(value, dtype=self.dtype)
+            self.write_chunk(coords, v.real, "real")
+            self.write_chunk(coords, v.imag, "imag")
+            return
 
         ext = self.chunk_extent(coords)
         dt = self.field_dtype(field)

@@ -82,13 +82,13 @@ int main(int argc, char** argv) {
   struct V { const char* name; kfn f; bool check; };
   V vs[] = {
       {"base (4-slot ring)", k_gemm_bf16_chain<false, 0>, false},
-      {"ping-pong (2 wave rows)", k_gemm_bf16_chain<false, 0, true>, true},
+      {"ping-pong NS4", k_gemm_bf16_chain<false, 0, true>, true},
+      {"base NS5", k_gemm_bf16_chain<false, 0, false, 5>, true},
+      {"ping-pong NS5", k_gemm_bf16_chain<false, 0, true, 5>, true},
+      {"ping-pong NS4 GM8", k_gemm_bf16_chain<false, 0, true, 4, 8>, true},
+      {"ping-pong NS5 GM8", k_gemm_bf16_chain<false, 0, true, 5, 8>, true},
+      {"ping-pong NS4 GM2", k_gemm_bf16_chain<false, 0, true, 4, 2>, true},
       {"abl: no staging", k_gemm_bf16_chain<false, 1>, false},
-      {"abl: no B reads", k_gemm_bf16_chain<false, 2>, false},
-      {"abl: no A reads", k_gemm_bf16_chain<false, 4>, false},
-      {"abl: no A+B reads", k_gemm_bf16_chain<false, 6>, false},
-      {"abl: no barrier", k_gemm_bf16_chain<false, 8>, false},
-      {"abl: MFMA only", k_gemm_bf16_chain<false, 15>, false},
   };
   for (const V& v : vs) {
     float best = 1e30f;
