@@ -399,13 +399,34 @@ class Codegen:
         return dtype in (np.dtype(np.int64), np.dtype(np.uint64))
 
     # -- expression codegen --------------------------------------------------
+    def _last_use(self, key) -> bool:
+        """Count one use of ``key``; True if it was the last one."""
+        if not hasattr(self, "remaining"):
+            self.remaining = dict(self.uses)
+        n = self.remaining.get(key, 0) - 1
+        self.remaining[key] = n
+        return n == 0 and key in self.uses
+
     def gen(self, e) -> Tuple[int, bool]:
-        """Return (register, owned) holding the value of ``e``."""
+        """Return (register, owned) holding the value of ``e``.  A leaf or
+        common subexpression at its last use is handed over as owned, so
+        the consumer computes in place instead of copying it to a fresh
+        register (complex products read 4 leaves and keep 2 parts live)."""
+        pinned = getattr(self, "pinned", ())
         if id(e) in self.leaf_regs:
-            return self.leaf_regs[id(e)], False
+            r = self.leaf_regs[id(e)]
+            if self._last_use(self.skey(e)) and r in self.reserved and r not in pinned and \
+                    sum(1 for v in self.leaf_regs.values() if v == r) == 1:
+                self.reserved.discard(r)  # leaves reload every element: free to overwrite
+                return r, True
+            return r, False
         key = self.skey(e)
         if key in self.cache:
-            return self.cache[key], False
+            r = self.cache[key]
+            if self._last_use(key) and r not in pinned:
+                del self.cache[key]
+                return r, True
+            return r, False
         if isinstance(e, ir.Const):
             r = self.alloc()
             self.code.append((ir_op("CONST"), r, 0, 0, 0, self.const_index(e.value, e.dtype)))
@@ -431,7 +452,9 @@ class Codegen:
         if isinstance(e, ir.Where):
             ra = self.owned(*self.gen(e.a))
             rb, ob = self.gen(e.b)
+            self.pin(rb)  # read by the WHERE below: c's code must not reuse it
             rc, oc = self.gen(e.c)
+            self.unpin(rb)
             self.code.append((ir_op("WHERE"), ra, rb, rc, 0, 0))
             if ob:
                 self.release(rb)
@@ -439,6 +462,18 @@ class Codegen:
                 self.release(rc)
             return self._finish(e, ra)
         raise LoweringError(f"cannot generate code for {type(e).__name__}")
+
+    def pin(self, r):
+        """Keep register r's value intact: no later last-use handover of it
+        (operands awaiting their instruction, program outputs)."""
+        if not hasattr(self, "pinned"):
+            self.pinned = {}
+        self.pinned[r] = self.pinned.get(r, 0) + 1
+
+    def unpin(self, r):
+        self.pinned[r] -= 1
+        if not self.pinned[r]:
+            del self.pinned[r]
 
     def owned(self, r, owned) -> int:
         if owned:
@@ -580,7 +615,7 @@ def program_fits(p: ir.ExprProgram) -> bool:
         cg = Codegen(choose_vtype(pre, leaves), leaf_regs)
         cg.count_uses(pre)
         for e in pre:
-            cg.gen(e)
+            cg.pin(cg.gen(e)[0])  # as the lowering does: outputs stay live
         if len(cg.code) > nat.MAX_INSNS or len(cg.consts) > nat.MAX_CONSTS:
             return False
         if p.reduce is not None and not all(isinstance(e, ir.Field) for e in exprs[:len(outs)]):
@@ -595,7 +630,7 @@ def program_fits(p: ir.ExprProgram) -> bool:
                         ecg.leaf_regs[id(lf)] = fidx[lf.name]
             ecg.count_uses(exprs[:len(outs)])
             for e in exprs[:len(outs)]:
-                ecg.gen(e)
+                ecg.pin(ecg.gen(e)[0])
             if len(ecg.code) > nat.MAX_EPI:
                 return False
         return True
@@ -849,6 +884,7 @@ class Lowerer:
             srcs = []
             for _, e in out_items:
                 r, _ = cg.gen(e)
+                cg.pin(r)
                 srcs.append(r)
             P.nfields = 0
             P.nepi = -1
@@ -859,6 +895,7 @@ class Lowerer:
                 raise LoweringError("too many reduced fields")
             for i, f in enumerate(rfields):
                 r, _ = cg.gen(f.expr)
+                cg.pin(r)
                 P.field_src[i] = r
                 P.field_rop[i] = ir.ROPS[f.rop]
                 P.field_acc[i] = 1 if ir.acc_is_int(f.rop, f.dtype) else 0
@@ -887,6 +924,7 @@ class Lowerer:
                 out_regs = []
                 for _, e in out_items:
                     r, _ = ecg.gen(e)
+                    ecg.pin(r)
                     out_regs.append(r)
                 if len(ecg.code) > nat.MAX_EPI:
                     raise LoweringError("epilogue too long")

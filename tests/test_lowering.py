@@ -40,7 +40,7 @@ def test_quad_means_is_one_streaming_launch(built, dry):
     assert P.mode & MODE_STREAM and P.mode & 4
     assert (P.ndim, P.nred, P.nleaves, P.nfields) == (2, 1, 2, 2)
     assert L.max_red == 200 and L.max_kept == 16 * 32
-    assert P.ninsns == 2  # MOV + MUL: the product is shared by the n and total fields
+    assert P.ninsns == 1  # MUL in place on the first leaf register (its last use)
 
 
 def test_chain_fusion_can_be_disabled(built, dry):
@@ -451,9 +451,9 @@ def test_complex_programs_lower_to_real_slabs(built, dry):
     p = z * w
     arrays_to_plan(p).execute(executor=dry, resume=True, array_names=[p.name])
     f = _fused(dry)
-    # (the product's 4 part leaves + 2 live parts exceed the VM's 6 registers:
-    # split.py computes the parts through HBM temporaries, then writes both)
-    assert f and f[-1].prog.nouts == 2 and all(l.prog.nleaves <= 4 for l in f)
+    # 4 part leaves + 2 live parts in the VM's 6 registers: the leaf registers
+    # are computed in place at their last use (Codegen.gen), one launch
+    assert len(f) == 1 and f[0].prog.nleaves == 4 and f[0].prog.nouts == 2
     dry.launched.clear()
     s = xp.sum(z * w, axis=0)
     arrays_to_plan(s).execute(executor=dry, resume=True, array_names=[s.name])
