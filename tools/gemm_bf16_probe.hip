@@ -90,7 +90,9 @@ int main(int argc, char** argv) {
       {"ping-pong NS4 GM2", k_gemm_bf16_chain<false, 0, true, 4, 2>, true},
       {"abl: no staging", k_gemm_bf16_chain<false, 1>, false},
   };
+  const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
   for (const V& v : vs) {
+    if (only >= 0 && &v - vs != only) continue;
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
