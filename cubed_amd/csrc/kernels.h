@@ -320,6 +320,39 @@ CUBED_DEV void fused_b_body(
 }
 
 // ---------------------------------------------------------------- finalize
+// Fold the nsplit split partials of element (t, k) in split order into
+// x[f]: batches of 8 splits are loaded before they are combined, so a
+// thread keeps 8 x nfields loads in flight instead of one (the finalize of a
+// 100-way split read one dependent partial at a time).  Same order, same bits.
+CUBED_DEV void fold_splits_of(const cubed_program_t& P, const Acc* __restrict__ ws, int32_t nsplit,
+                              int64_t ntasks, int64_t t, int64_t max_kept, int64_t k,
+                              Acc (&x)[CUBED_MAX_FIELDS]) {
+  const int nf = P.nfields;
+  const int64_t sstride = ntasks * max_kept * nf;
+  const Acc* __restrict__ p = ws + (t * max_kept + k) * nf;
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    if (f < nf) x[f] = p[f];
+  int s = 1;
+  for (; s + 8 <= nsplit; s += 8) {
+    Acc v[8][CUBED_MAX_FIELDS];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < nf) v[u][f] = p[(int64_t)(s + u) * sstride + f];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < nf) x[f] = acc_combine(x[f], v[u][f], P.field_rop[f], P.field_acc[f]);
+  }
+  for (; s < nsplit; ++s)
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+      if (f < nf) x[f] = acc_combine(x[f], p[(int64_t)s * sstride + f], P.field_rop[f], P.field_acc[f]);
+}
+
 CUBED_DEV void finalize_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, int32_t nsplit, const Acc* __restrict__ ws, int kd0, int kd1) {
@@ -338,14 +371,10 @@ CUBED_DEV void finalize_body(
     kk = q;
     for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
   }
+  Acc x[CUBED_MAX_FIELDS];
+  fold_splits_of(P, ws, nsplit, ntasks, t, max_kept, k, x);
   Acc fin[CUBED_MAX_FIELDS][1];
-  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-    Acc x = ws[(t * max_kept + k) * P.nfields + f];
-    for (int s = 1; s < nsplit; ++s)
-      x = acc_combine(x, ws[(((int64_t)s * ntasks + t) * max_kept + k) * P.nfields + f],
-                      P.field_rop[f], P.field_acc[f]);
-    fin[f][0] = x;
-  }
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) fin[f][0] = x[f];
   finish<1>(P, T, fin, ooff);
 }
 
@@ -366,16 +395,10 @@ CUBED_DEV void collect_body(
   int64_t nk = 1;
   for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
   const int64_t n = ntasks * max_kept;
-  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-    Acc x = acc_init(P.field_rop[f], P.field_acc[f]);
-    if (k < nk) {
-      x = ws[(t * max_kept + k) * P.nfields + f];
-      for (int s = 1; s < nsplit; ++s)
-        x = acc_combine(x, ws[(((int64_t)s * ntasks + t) * max_kept + k) * P.nfields + f],
-                        P.field_rop[f], P.field_acc[f]);
-    }
-    soa[f * n + i] = x;
-  }
+  Acc x[CUBED_MAX_FIELDS];
+  if (k < nk) fold_splits_of(P, ws, nsplit, ntasks, t, max_kept, k, x);
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f)
+    soa[f * n + i] = k < nk ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
 }
 
 // Epilogue + store from combined SoA partials (the last step of a reduction
