@@ -114,7 +114,9 @@ __device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
 
 // ABL: ablation bits for tools/gemm_bf16_probe.hip only (0 in the library):
 // 1 = no K-loop staging, 2 = no B fragment reads, 4 = no A fragment reads,
-// 8 = no K-loop barrier.  Any nonzero value computes wrong results.
+// 8 = no K-loop barrier; ping-pong only: 16 = no vmcnt wait in the K loop,
+// 32 = every K step staged from step 0's addresses (L2-resident), 1 = no
+// K-loop staging.  Any nonzero value computes wrong results.
 // PP: ping-pong schedule (see the K loop).
 // NS: ring slots (each step p+NS-1 is staged while step p is consumed);
 // GM: tile rows per XCD tile group.
@@ -279,11 +281,11 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
       }
 #pragma unroll
       for (int mb = 0; mb < 8; ++mb) af[mb] = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
-      if (p + D < nst) stage((p + D) * HB_BK, lds + wr_slot * HB_STAGE);
+      if (!(ABL & 1) && p + D < nst) stage((ABL & 32) ? 0 : (p + D) * HB_BK, lds + wr_slot * HB_STAGE);
       rd = rd + 1 == NS ? 0 : rd + 1;
       wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (p + 1 < nst) wait_step(p + 1);
+      if (!(ABL & 16) && p + 1 < nst) wait_step(p + 1);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -654,7 +656,9 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     const dim3 grid((unsigned)blocks), blk(512);
     const char* z = (const char*)d_zero;
     // ping-pong schedule: 1072-1098 TF vs 1021-1041 for the single-slot loop
-    // on config 5 (profiles/r02_gemm_bf16_variants.log)
+    // on config 5 (profiles/r02_gemm_bf16_variants.log); the 4-phase and
+    // one-wave-per-SIMD experiments in tools/gemm_bf16_probe.hip measured
+    // slower (profiles/r02_gemm_bf16_q4_w4.log)
     if (out_dtype == CUBED_BF16)
       hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
     else

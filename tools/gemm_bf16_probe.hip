@@ -14,6 +14,7 @@ namespace cubed {
 thread_local char g_err[512];
 }
 #include "../cubed_amd/csrc/gemm_chain.hip"
+#include "gemm_bf16_experiments.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -79,16 +80,17 @@ int main(int argc, char** argv) {
   float* dmax;
   CHECK(hipMalloc(&dmax, 4));
 
-  struct V { const char* name; kfn f; bool check; };
+  struct V { const char* name; kfn f; bool check; int threads = 0; };
   V vs[] = {
-      {"base (4-slot ring)", k_gemm_bf16_chain<false, 0>, false},
-      {"ping-pong NS4", k_gemm_bf16_chain<false, 0, true>, true},
-      {"base NS5", k_gemm_bf16_chain<false, 0, false, 5>, true},
-      {"ping-pong NS5", k_gemm_bf16_chain<false, 0, true, 5>, true},
-      {"ping-pong NS4 GM8", k_gemm_bf16_chain<false, 0, true, 4, 8>, true},
-      {"ping-pong NS5 GM8", k_gemm_bf16_chain<false, 0, true, 5, 8>, true},
-      {"ping-pong NS4 GM2", k_gemm_bf16_chain<false, 0, true, 4, 2>, true},
-      {"abl: no staging", k_gemm_bf16_chain<false, 1>, false},
+      {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, true>, false},
+      {"pp abl: no vmcnt wait", k_gemm_bf16_chain<false, 16, true>, false},
+      {"pp abl: L2-resident staging", k_gemm_bf16_chain<false, 32, true>, false},
+      {"pp abl: no staging", k_gemm_bf16_chain<false, 1 | 16, true>, false},
+      {"pp abl: L2-res + no wait", k_gemm_bf16_chain<false, 32 | 16, true>, false},
+      {"ping-pong NS4 (reference)", k_gemm_bf16_chain<false, 0, true>, false},
+      {"q4 (4-phase BK64)", k_gemm_bf16_q4<false, 4>, true},
+      {"w4 (1 wave/SIMD, 128x128)", k_gemm_bf16_w4<false, 4>, true, 256},
+      {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, true>, true},
   };
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
   for (const V& v : vs) {
@@ -96,7 +98,8 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(v.f, grid, blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z);
+      hipLaunchKernelGGL(v.f, grid, v.threads ? dim3(v.threads) : blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z);
+      CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       float ms;
