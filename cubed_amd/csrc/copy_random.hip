@@ -283,7 +283,15 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
       if (v >= 1 && v <= 1024) spb = v;
     }
     const int64_t nseg = (max_box_elems + 64 * UN - 1) / (64 * UN);
-    const int64_t bpb = (nseg + spb - 1) / spb;
+    int64_t bpb = (nseg + spb - 1) / spb;
+    // a multiple of 8 workgroups per box: workgroup i of box b and of box
+    // b+1 -- the same rows of the next piece of the source rows when the
+    // host orders boxes by source address -- run on the same XCD (round-robin
+    // dispatch) at nearly the same time, so the 128-B line a 4000-B piece
+    // boundary splits is fetched into that XCD's L2 once, not twice
+    // (CUBED_AMD_COPY_XCD=0: round-2 grid)
+    const char* xe = getenv("CUBED_AMD_COPY_XCD");
+    if (!(xe && xe[0] == '0') && nboxes > 1) bpb = (bpb + 7) / 8 * 8;
     const dim3 grid = grid2(nboxes * bpb);
     switch (width) {
       case 16: hipLaunchKernelGGL((k_copy_flat<16, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;

@@ -18,6 +18,7 @@
 //      over workgroups that write partial accumulators to the workspace;
 //      k_finalize combines them in split order and runs the epilogue.
 #include "kernels.h"
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -154,15 +155,47 @@ static int64_t choose_split(int64_t base, int64_t max_split, int64_t resident) {
   return best;
 }
 
+// Kept VEC groups per thread of a streaming JIT kernel: the host picks W
+// (lowering.py _stream_groups) and records it in the mode bits, so the JIT
+// cache key, the kernel and the grid agree.
+int stream_groups(const cubed_program_t& P) {
+  return (P.mode & CUBED_MODE_STREAM_W4) ? 4 : (P.mode & CUBED_MODE_STREAM_W2) ? 2 : 1;
+}
+
+// Streaming launches: a grid that fills the CUs without splitting the
+// reduced dim runs unsplit (a time split costs more than the occupancy it
+// adds: config 2 W = 2 unsplit 6.81 TB/s vs 6.02 for the round-2 3-way
+// split, profiles/r02_stream_ab.log); smaller grids split toward
+// CUBED_AMD_STREAM_TARGET workgroups (default 2048, ~8 per CU: config 1 at
+// 256 took 2.7x longer).
+static int64_t stream_target() {
+  if (const char* e = getenv("CUBED_AMD_STREAM_TARGET")) {
+    const long v = atol(e);
+    if (v >= 1 && v <= (1 << 20)) return v;
+  }
+  return 2048;
+}
+
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
-                              int64_t max_red) {
+                              int64_t max_red, int stream_w) {
   LaunchPlan L;
   L.kernel = P->mode & 3;
   L.vec = (P->mode & 4) ? 4 : 1;
   L.nsplit = 1;
   L.bpt = 1;
   const int64_t target = 2048;  // ~8 workgroups per CU
-  if (L.kernel == 0) {
+  if (P->mode & CUBED_MODE_STREAM) {
+    // stream_body: whole waves of W groups of 4 kept elements per thread
+    const int64_t W = stream_w;
+    const int64_t slots = ((max_kept + 256 * W - 1) / (256 * W)) * 64;
+    L.bpt = (slots + kBlock - 1) / kBlock;
+    if (L.bpt < 1) L.bpt = 1;
+    if (L.bpt > 65536) L.bpt = 65536;
+    const int64_t base = ntasks * L.bpt;
+    if (P->nfields > 0 && base < (256 * 9) / 10 && max_red >= 64)
+      L.nsplit = (int32_t)choose_split(base, max_red / 16, stream_target());
+    L.blocks = ntasks * L.nsplit * L.bpt;
+  } else if (L.kernel == 0) {
     const int64_t items = (max_kept + L.vec - 1) / L.vec;
     L.bpt = (items + kBlock - 1) / kBlock;
     if (L.bpt < 1) L.bpt = 1;
@@ -230,6 +263,11 @@ int check_program(const cubed_program_t& P) {
     set_err("cubed_fused_chunks: stream mode needs kernel A, VEC=4, one kept dim and <= 2 reduced dims");
     return CUBED_E_LAYOUT;
   }
+  if ((P.mode & (CUBED_MODE_STREAM_W2 | CUBED_MODE_STREAM_W4)) &&
+      (!(P.mode & CUBED_MODE_STREAM) || (P.mode & CUBED_MODE_STREAM_W2 && P.mode & CUBED_MODE_STREAM_W4))) {
+    set_err("cubed_fused_chunks: stream group bits need stream mode (one of W2 / W4)");
+    return CUBED_E_LAYOUT;
+  }
   if (P.mode & CUBED_MODE_STREAM) {
     const int want = P.vtype == CUBED_V_F32 ? CUBED_F32 : P.vtype == CUBED_V_F64 ? CUBED_F64 : CUBED_I64;
     for (int l = 0; l < P.nleaves; ++l)
@@ -248,7 +286,12 @@ using namespace cubed;
 extern "C" int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
                                                int64_t max_kept, int64_t max_red) {
   if (!prog || ntasks <= 0) return 0;
-  return plan_launch(prog, ntasks, max_kept, max_red).ws_bytes;
+  // enough for the interpreted (W = 1) and the JIT streaming grid
+  const int64_t a = plan_launch(prog, ntasks, max_kept, max_red).ws_bytes;
+  const int64_t b = (prog->mode & CUBED_MODE_STREAM)
+                        ? plan_launch(prog, ntasks, max_kept, max_red, stream_groups(*prog)).ws_bytes
+                        : 0;
+  return a > b ? a : b;
 }
 
 extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_program_t* d_prog,

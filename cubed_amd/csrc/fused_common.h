@@ -113,7 +113,12 @@ void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const La
                    int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st);
 
 dim3 grid_of(int64_t blocks);
-LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept, int64_t max_red);
+// stream_w: kept VEC groups per thread of a streaming launch (1 for the
+// interpreted kernels of stream.hip, stream_groups(P) for JIT kernels)
+LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept, int64_t max_red,
+                       int stream_w = 1);
+// Streaming JIT kernels: kept VEC groups per thread (1, 2 or 4; fused.hip)
+int stream_groups(const cubed_program_t& P);
 int check_program(const cubed_program_t& P);
 void kept_dims(const cubed_program_t& P, int& kd0, int& kd1);
 int launch_collect(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,

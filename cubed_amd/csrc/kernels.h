@@ -698,79 +698,115 @@ CUBED_DEV void accumulate_nocount(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& r
   }
 }
 
-// Rows [lo, hi) of one kept VEC group: U rows of loads in flight, then the
-// program and the accumulation; MIXED: some leaves are re-read (cached loads).
-template <typename V, int NL, int U, bool MIXED>
-CUBED_DEV void stream_rows(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
+// Rows [lo, hi) of W kept VEC groups (group j at element offset go[j], pair
+// distance dk[j] for 8-byte elements, gv[j] = inside the kept extent): U rows
+// x W groups of loads in flight, then the program and the accumulation per
+// group; MIXED: some leaves are re-read (cached loads).  p[l] points at the
+// row's element 0.
+template <typename V, int NL, int U, int W, bool MIXED>
+CUBED_DEV void stream_rows(Acc (&acc)[W][CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
                            const cubed_program_t& P, const CUBED_G V* (&p)[NL],
-                           const int64_t (&rs)[NL], int64_t lo, int64_t hi, int64_t dk) {
+                           const int64_t (&rs)[NL], int64_t lo, int64_t hi,
+                           const int64_t (&go)[W], const int64_t (&dk)[W], const bool (&gv)[W]) {
   constexpr bool IL = sizeof(V) == 8;
   int64_t r = lo;
+  // one group's 4 elements of leaf l at row pointer q
+  auto ld_group = [&](V (&o)[4], const CUBED_G V* q, int j) {
+    if (!gv[j]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (V)0;
+      return;
+    }
+    if constexpr (IL) ld4h<V>(o, q + go[j], dk[j]);
+    else ld4(o, q + go[j]);
+  };
   // leaves with reduced stride 0 (broadcast operands) are loop-invariant:
   // loaded once here instead of once per row
-  V inv[NL][4];
+  V inv[W][NL][4];
   if (MIXED && lo < hi) {
 #pragma unroll
-    for (int l = 0; l < NL; ++l)
-      if (rs[l] == 0) {
-        if constexpr (IL) ld4ch<V>(inv[l], p[l], dk);
-        else ld4c<V>(inv[l], p[l]);
-      }
+    for (int j = 0; j < W; ++j)
+#pragma unroll
+      for (int l = 0; l < NL; ++l)
+        if (rs[l] == 0) {
+          if (!gv[j]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) inv[j][l][e] = (V)0;
+          } else if constexpr (IL) {
+            ld4ch<V>(inv[j][l], p[l] + go[j], dk[j]);
+          } else {
+            ld4c<V>(inv[j][l], p[l] + go[j]);
+          }
+        }
   }
-  auto load_batch = [&](V (&buf)[U][NL][4]) {
+  auto load_batch = [&](V (&buf)[U][W][NL][4]) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        if (MIXED && rs[l] == 0) {
+      for (int j = 0; j < W; ++j)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) buf[u][l][j] = inv[l][j];
-        } else {
-          if constexpr (IL) ld4h<V>(buf[u][l], p[l] + u * rs[l], dk);
-          else ld4(buf[u][l], p[l] + u * rs[l]);
+        for (int l = 0; l < NL; ++l) {
+          if (MIXED && rs[l] == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) buf[u][j][l][e] = inv[j][l][e];
+          } else {
+            ld_group(buf[u][j][l], p[l] + u * rs[l], j);
+          }
         }
-      }
 #pragma unroll
     for (int l = 0; l < NL; ++l) p[l] += U * rs[l];
   };
-  auto reduce_batch = [&](V (&buf)[U][NL][4]) {
+  auto reduce_batch = [&](V (&buf)[U][W][NL][4]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      set_leaves<NL, V>(regs, buf[u]);
-      CUBED_RUN_PROLOGUE(V, 4, regs);
-      accumulate_nocount<V>(acc, regs, P);
-    }
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        set_leaves<NL, V>(regs, buf[u][j]);
+        CUBED_RUN_PROLOGUE(V, 4, regs);
+        accumulate_nocount<V>(acc[j], regs, P);
+      }
   };
   // (a software-pipelined form -- batch r + U loading while batch r reduces --
   // and U = 2 / 8 measured equal or slower on quad-means, config 1 and
   // vorticity: profiles/r02_stream_ab.log)
   for (; r + U <= hi; r += U) {
-    V buf[U][NL][4];
+    V buf[U][W][NL][4];
     load_batch(buf);
     reduce_batch(buf);
   }
 
   for (; r < hi; ++r) {
-    V buf[NL][4];
+    V buf[W][NL][4];
 #pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      if (MIXED && rs[l] == 0) {
+    for (int j = 0; j < W; ++j)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) buf[l][j] = inv[l][j];
-      } else {
-        if constexpr (IL) ld4h<V>(buf[l], p[l], dk);
-        else ld4(buf[l], p[l]);
+      for (int l = 0; l < NL; ++l) {
+        if (MIXED && rs[l] == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) buf[j][l][e] = inv[j][l][e];
+        } else {
+          ld_group(buf[j][l], p[l], j);
+        }
       }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      set_leaves<NL, V>(regs, buf[j]);
+      CUBED_RUN_PROLOGUE(V, 4, regs);
+      accumulate_nocount<V>(acc[j], regs, P);
     }
-    set_leaves<NL, V>(regs, buf);
-    CUBED_RUN_PROLOGUE(V, 4, regs);
-    accumulate_nocount<V>(acc, regs, P);
 #pragma unroll
     for (int l = 0; l < NL; ++l) p[l] += rs[l];
   }
 }
 
-template <typename V, int NL, int U>
+// W: kept VEC groups per thread (stream_groups()).  The 64 lanes of a wave
+// own a block of 256 * W consecutive kept elements: group j of lane L starts
+// at block + 256 j + 4 L (4-byte elements: every 16-byte load instruction of
+// the wave reads 1 KiB contiguous), or for 8-byte elements at
+// block + 256 j + 2 L as the pairs (k, k+1), (k+128, k+129) (again 1 KiB per
+// instruction); a last partial 256-element run of 8-byte elements falls back
+// to 4 consecutive elements per lane (dk = 2).  W = 1 is the round-2 mapping.
+template <typename V, int NL, int U, int W = 1>
 CUBED_DEV void stream_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
@@ -788,7 +824,8 @@ CUBED_DEV void stream_body(
   const int64_t nrow = nr ? T->extent[nr - 1] : 1;
   const int64_t nq = nr == 2 ? T->extent[0] : 1;
   const int64_t nrd = nq * nrow;
-  const int64_t items = nk >> 2;
+  // thread slots: whole waves of W groups each
+  const int64_t slots = ((nk + 256 * W - 1) / (256 * W)) * 64;
   const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
 
   const CUBED_G V* base[NL];
@@ -806,54 +843,61 @@ CUBED_DEV void stream_body(
 #pragma unroll
   for (int l = 0; l < NL; ++l) all_streamed = all_streamed && rs[l] != 0;
 
-  // 8-byte elements: the 64 lanes of a wave own 256 consecutive kept
-  // elements as pairs (k, k+1) and (k+128, k+129), k = base + 2 * lane, so
-  // each 16-byte load instruction of the wave is 1 KiB contiguous; a last
-  // partial wave falls back to 4 consecutive elements per lane (dk = 2)
   constexpr bool IL = sizeof(V) == 8;
-  for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
-    int64_t k = item * 4, dk = 2;
-    if constexpr (IL) {
-      const int64_t wb = (item >> 6) << 8;
-      if (wb + 256 <= nk) {
-        k = wb + 2 * (item & 63);
-        dk = 128;
-      }
-    }
-    int64_t ooff[CUBED_MAX_OUTS];
+  for (int64_t it = b * kBlock + threadIdx.x; it < slots; it += bpt * kBlock) {
+    const int64_t wb = (it >> 6) * (256 * W);
+    const int lane = (int)(it & 63);
+    int64_t go[W], dk[W];
+    bool gv[W];
 #pragma unroll
-    for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] = k;
+    for (int j = 0; j < W; ++j) {
+      const int64_t sub = wb + 256 * j;
+      if (IL && sub + 256 <= nk) {
+        go[j] = sub + 2 * lane;
+        dk[j] = 128;
+      } else {
+        go[j] = sub + 4 * lane;
+        dk[j] = 2;
+      }
+      gv[j] = go[j] + 4 <= nk || (dk[j] == 128);
+    }
     Regs<V, 4> regs;
     if (P.nfields == 0) {
-      V buf[NL][4];
 #pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        if constexpr (IL) ld4h<V>(buf[l], base[l] + k, dk);
-        else ld4(buf[l], base[l] + k);
-      }
-      set_leaves<NL, V>(regs, buf);
-      CUBED_RUN_PROLOGUE(V, 4, regs);
+      for (int j = 0; j < W; ++j) {
+        if (!gv[j]) continue;
+        V buf[NL][4];
 #pragma unroll
-      for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
-        if (o < P.nouts) {
-          V X[4];
-          fetch(regs, P.out_src[o], X);
-          if constexpr (IL) {
-            V X0[2] = {X[0], X[1]}, X1[2] = {X[2], X[3]};
-            stv<V, 2>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X0);
-            stv<V, 2>((char*)T->out_base[o], ooff[o] + dk, P.out_dtype[o], X1);
-          } else {
-            stv<V, 4>((char*)T->out_base[o], ooff[o], P.out_dtype[o], X);
+        for (int l = 0; l < NL; ++l) {
+          if constexpr (IL) ld4h<V>(buf[l], base[l] + go[j], dk[j]);
+          else ld4(buf[l], base[l] + go[j]);
+        }
+        set_leaves<NL, V>(regs, buf);
+        CUBED_RUN_PROLOGUE(V, 4, regs);
+#pragma unroll
+        for (int o = 0; o < CUBED_MAX_OUTS; ++o) {
+          if (o < P.nouts) {
+            V X[4];
+            fetch(regs, P.out_src[o], X);
+            if constexpr (IL) {
+              V X0[2] = {X[0], X[1]}, X1[2] = {X[2], X[3]};
+              stv<V, 2>((char*)T->out_base[o], go[j], P.out_dtype[o], X0);
+              stv<V, 2>((char*)T->out_base[o], go[j] + dk[j], P.out_dtype[o], X1);
+            } else {
+              stv<V, 4>((char*)T->out_base[o], go[j], P.out_dtype[o], X);
+            }
           }
         }
       }
       continue;
     }
-    Acc acc[CUBED_MAX_FIELDS][4];
+    Acc acc[W][CUBED_MAX_FIELDS][4];
 #pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    for (int j = 0; j < W; ++j)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[f][j] = acc_init(P.field_rop[f], P.field_acc[f]);
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[j][f][e] = acc_init(P.field_rop[f], P.field_acc[f]);
 
     // flattened reduced range [r0, r1) = (chunk q, row) pairs in order
     for (int64_t q = nrow ? r0 / nrow : 0; q < nq && q * nrow < r1; ++q) {
@@ -861,42 +905,49 @@ CUBED_DEV void stream_body(
       const int64_t hi = (r1 < (q + 1) * nrow ? r1 : (q + 1) * nrow) - q * nrow;
       const CUBED_G V* p[NL];
 #pragma unroll
-      for (int l = 0; l < NL; ++l) p[l] = base[l] + k + q * qs[l] + lo * rs[l];
+      for (int l = 0; l < NL; ++l) p[l] = base[l] + q * qs[l] + lo * rs[l];
       if (all_streamed)
-        stream_rows<V, NL, U, false>(acc, regs, P, p, rs, lo, hi, dk);
+        stream_rows<V, NL, U, W, false>(acc, regs, P, p, rs, lo, hi, go, dk, gv);
       else
-        stream_rows<V, NL, U, true>(acc, regs, P, p, rs, lo, hi, dk);
+        stream_rows<V, NL, U, W, true>(acc, regs, P, p, rs, lo, hi, go, dk, gv);
     }
 #pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-      if (f < P.nfields && P.field_rop[f] == CUBED_R_COUNT)
+    for (int j = 0; j < W; ++j) {
+      if (!gv[j]) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[f][j].i += r1 - r0;
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < P.nfields && P.field_rop[f] == CUBED_R_COUNT)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[j][f][e].i += r1 - r0;
 
-    if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
-      if constexpr (IL) {
-        Acc a0[CUBED_MAX_FIELDS][2], a1[CUBED_MAX_FIELDS][2];
+      int64_t ooff[CUBED_MAX_OUTS];
 #pragma unroll
-        for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-          a0[f][0] = acc[f][0]; a0[f][1] = acc[f][1];
-          a1[f][0] = acc[f][2]; a1[f][1] = acc[f][3];
+      for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] = go[j];
+      if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
+        if constexpr (IL) {
+          Acc a0[CUBED_MAX_FIELDS][2], a1[CUBED_MAX_FIELDS][2];
+#pragma unroll
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+            a0[f][0] = acc[j][f][0]; a0[f][1] = acc[j][f][1];
+            a1[f][0] = acc[j][f][2]; a1[f][1] = acc[j][f][3];
+          }
+          int64_t o1[CUBED_MAX_OUTS];
+#pragma unroll
+          for (int o = 0; o < CUBED_MAX_OUTS; ++o) o1[o] = ooff[o] + dk[j];
+          finish<2>(P, T, a0, ooff);
+          finish<2>(P, T, a1, o1);
+        } else {
+          finish<4>(P, T, acc[j], ooff);
         }
-        int64_t o1[CUBED_MAX_OUTS];
-#pragma unroll
-        for (int o = 0; o < CUBED_MAX_OUTS; ++o) o1[o] = ooff[o] + dk;
-        finish<2>(P, T, a0, ooff);
-        finish<2>(P, T, a1, o1);
       } else {
-        finish<4>(P, T, acc, ooff);
-      }
-    } else {
-      Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept) * P.nfields;
+        Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept) * P.nfields;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t e = k + (j >> 1) * dk + (j & 1);
+        for (int e = 0; e < 4; ++e) {
+          const int64_t el = go[j] + (e >> 1) * dk[j] + (e & 1);
 #pragma unroll
-        for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-          if (f < P.nfields) w[e * P.nfields + f] = acc[f][j];
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+            if (f < P.nfields) w[el * P.nfields + f] = acc[j][f][e];
+        }
       }
     }
   }

@@ -274,6 +274,12 @@ class CopyLaunch:
                 # run of destination words
                 self.path = nat.COPY_FLAT
                 self.work = words
+                # source-address order: the pieces of one source row band
+                # sit next to each other, so the workgroups copying the two
+                # sides of a piece boundary share an XCD (cubed_copy_boxes
+                # rounds workgroups per box to a multiple of 8)
+                boxes = sorted(boxes, key=lambda b: b.src)
+                self.boxes = boxes
         elif nd == 2 and all(b.sstride[1] == 1 and b.dstride[0] == 1 for b in boxes):
             self.path = nat.COPY_TILE
             self.lane = 0
@@ -1005,7 +1011,7 @@ class Lowerer:
         P.nred = layout.nred
         P.mode = layout.mode
         if _stream_ok(layout, leaves, kinds, P.vtype, check_outputs=not lifted):
-            P.mode |= MODE_STREAM
+            P.mode |= MODE_STREAM | _stream_groups_mode(P, len(rows), layout.max_kept)
         if partials:
             if P.nfields == 0:
                 raise LoweringError("partials mode needs a reduction")
@@ -1632,6 +1638,41 @@ LIFT_ENABLED = __import__("os").environ.get("CUBED_AMD_LIFT", "1") != "0"
 MODE_STREAM = 8  # include/cubed_amd.h CUBED_MODE_STREAM
 MODE_PARTIALS = 16  # include/cubed_amd.h CUBED_MODE_PARTIALS
 _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64: np.dtype(np.int64)}
+
+
+MODE_STREAM_W2 = 32  # include/cubed_amd.h CUBED_MODE_STREAM_W2
+MODE_STREAM_W4 = 64  # include/cubed_amd.h CUBED_MODE_STREAM_W4
+
+
+def _stream_unroll(itemsize: int, nleaves: int) -> int:
+    """Rows in flight per lane of the streaming kernel (fused_common.h
+    stream_unroll)."""
+    if itemsize == 4:
+        return 8 if nleaves <= 1 else 4 if nleaves == 2 else 2
+    return 4 if nleaves <= 1 else 2
+
+
+def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
+    """Mode bits for the kept groups per thread (W) of a streaming JIT kernel.
+
+    W gives each lane about 256 B of loads in flight (U rows x leaves x W
+    groups x 4 elements), e.g. W = 2 for quad-means' two f32 leaves -- but
+    only when the W-wide grid still fills the CUs without a time split
+    (>= 230 workgroups): the split grids of config 1 and of the elided
+    rechunk+mean ran 2-2.7x slower with W = 2 (profiles/r02_stream_ab.log).
+    CUBED_AMD_STREAM_W (1/2/4) forces W for A/B runs."""
+    isz = 4 if P.vtype == V_F32 else 8
+    nl = max(1, P.nleaves)
+    forced = __import__("os").environ.get("CUBED_AMD_STREAM_W")
+    if forced in ("1", "2", "4"):
+        w = int(forced)
+    else:
+        w = 256 // (_stream_unroll(isz, nl) * nl * 4 * isz)
+        w = 4 if w >= 4 else 2 if w >= 2 else 1
+        slots = -(-max_kept // (256 * w)) * 64
+        if w > 1 and ntasks * -(-slots // 256) < 230:
+            w = 1
+    return MODE_STREAM_W4 if w == 4 else MODE_STREAM_W2 if w == 2 else 0
 
 
 def _stream_ok(layout: Layout, leaves, kinds, vtype, check_outputs=True) -> bool:

@@ -57,6 +57,8 @@ extern "C" {
 /* error codes (negative); positive values are hipError_t */
 #define CUBED_MODE_STREAM 8
 #define CUBED_MODE_PARTIALS 16
+#define CUBED_MODE_STREAM_W2 32
+#define CUBED_MODE_STREAM_W4 64
 
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)
@@ -153,6 +155,10 @@ typedef struct {
                                  /* per-field accumulators as SoA partials  */
                                  /* at the start of the workspace (see      */
                                  /* cubed_fused_finish)                     */
+                                 /* +32 / +64 (CUBED_MODE_STREAM_W2 / _W4): */
+                                 /* streaming JIT kernels give each thread  */
+                                 /* 2 / 4 groups of 4 kept elements         */
+                                 /* (interpreted kernels ignore the bits)   */
   int32_t nleaves;
   uint8_t leaf_kind[CUBED_MAX_LEAVES];
   uint8_t leaf_dtype[CUBED_MAX_LEAVES];

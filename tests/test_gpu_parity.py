@@ -19,6 +19,7 @@ import pytest
 import cubed_amd as cubed
 import cubed_amd.array_api as xp
 import cubed_amd.random as crandom
+import cubed_amd.lowering as L
 from cubed_amd.core.ops import merge_chunks, partial_reduce, reduction
 from cubed_amd.core.plan import arrays_to_plan
 from oracle import cubed_ref as R
@@ -161,6 +162,50 @@ def test_quad_means_f32_stream(ex, T):
     exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
     assert got.dtype == np.float32
     assert np.allclose(got, exp, rtol=1e-6, atol=0)
+
+
+def _fused_launches(e):
+    return [l for lst in e._cache.values() for l in lst[1] if isinstance(l, L.FusedLaunch)]
+
+
+@pytest.mark.parametrize("w", ["1", "2", "4"])
+def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
+    """The streaming kernel with W kept groups per thread (forced by
+    CUBED_AMD_STREAM_W; by default only grids that fill the CUs unsplit take
+    W > 1): f32 quad-means over 72 x 144 kept elements (40.5 wave blocks of
+    256: a partial last block) and an f64 map-reduce over 1000 kept elements
+    (3 lane-interleaved 256-element runs + a 232-element run on the dk = 2
+    fallback), both against the oracle."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    monkeypatch.setenv("CUBED_AMD_STREAM_W", w)
+    e = GpuDagExecutor("cuda:0")
+    spec = mkspec(e)
+    random.seed(4)
+    shape, chunks = (103, 72, 144), (10, 72, 144)
+    u = xp.astype(crandom.random(shape, chunks=chunks, spec=spec), xp.float32)
+    v = xp.astype(crandom.random(shape, chunks=chunks, spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=e, array_names=[u.name, v.name])
+    s1, s2 = seeds(4, 2)
+    U = R.random_array(shape, chunks, s1).astype(np.float32)
+    V = R.random_array(shape, chunks, s2).astype(np.float32)
+    got = xp.mean(u * v, axis=0).compute(resume=True)
+    exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
+    assert np.allclose(got, exp, rtol=1e-6, atol=0)
+
+    random.seed(8)
+    a = crandom.random((200, 1000), chunks=(50, 1000), spec=spec)
+    arrays_to_plan(a).execute(executor=e, array_names=[a.name])  # an array leaf, not a Philox leaf
+    (s,) = seeds(8, 1)
+    x = R.random_array((200, 1000), (50, 1000), s)
+    got = xp.mean((a + 1) * 2, axis=0).compute(resume=True)
+    exp = R.mean((x + 1) * 2, (50, 1000), 0, allowed_mem=2_000_000_000)
+    assert np.allclose(got, exp, rtol=1e-12, atol=0)
+
+    bits = {1: 0, 2: L.MODE_STREAM_W2, 4: L.MODE_STREAM_W4}[int(w)]
+    streams = [l for l in _fused_launches(e) if l.prog.mode & L.MODE_STREAM]
+    assert len(streams) >= 2
+    assert all(l.prog.mode & (L.MODE_STREAM_W2 | L.MODE_STREAM_W4) == bits for l in streams)
 
 
 def test_config1_small(ex):

@@ -38,6 +38,7 @@ def test_quad_means_is_one_streaming_launch(built, dry):
     assert not L.gathers
     P = L.prog
     assert P.mode & MODE_STREAM and P.mode & 4
+    assert not P.mode & (32 | 64)  # 512 kept elements: too small a grid for W > 1
     assert (P.ndim, P.nred, P.nleaves, P.nfields) == (2, 1, 2, 2)
     assert L.max_red == 200 and L.max_kept == 16 * 32
     assert P.ninsns == 1  # MUL in place on the first leaf register (its last use)
@@ -464,3 +465,30 @@ def test_complex_programs_lower_to_real_slabs(built, dry):
     arrays_to_plan(r).execute(executor=dry, resume=True, array_names=[r.name])
     copies = [l for l in dry.launched if isinstance(l, CopyLaunch)]
     assert copies and sum(len(c.boxes) for c in copies) == 2 * 4 * 2  # 2 slabs x 4 targets x 2 pieces
+
+
+def test_stream_groups_per_thread_choice(monkeypatch):
+    """W (kept groups per thread of the streaming JIT kernel, mode bits):
+    ~256 B of loads in flight per lane, and only when the W-wide grid fills
+    the CUs without a time split (profiles/r02_stream_ab.log)."""
+    from types import SimpleNamespace
+
+    from cubed_amd import lowering as Lw
+
+    monkeypatch.delenv("CUBED_AMD_STREAM_W", raising=False)
+
+    def bits(vtype, nleaves, ntasks, max_kept):
+        return Lw._stream_groups_mode(SimpleNamespace(vtype=vtype, nleaves=nleaves), ntasks, max_kept)
+
+    # config 2 quad-means: 2 f32 leaves, 1 task of 720*1440 kept -> W = 2, 506 workgroups
+    assert bits(Lw.V_F32, 2, 1, 720 * 1440) == Lw.MODE_STREAM_W2
+    # config 1: 1 f64 leaf, 20000 kept -> the W = 2 grid (10 workgroups) would split: W = 1
+    assert bits(Lw.V_F64, 1, 1, 20000) == 0
+    # the elided rechunk+mean: 25 tasks of 2000 kept -> W = 1
+    assert bits(Lw.V_F32, 1, 25, 2000) == 0
+    # 4-leaf f64 programs (vorticity) already hold 256 B per lane -> W = 1
+    assert bits(Lw.V_F64, 4, 100, 720000) == 0
+    # a 1-leaf f32 mean over a wide kept dim -> W = 2
+    assert bits(Lw.V_F32, 1, 1, 4 << 20) == Lw.MODE_STREAM_W2
+    monkeypatch.setenv("CUBED_AMD_STREAM_W", "4")
+    assert bits(Lw.V_F64, 1, 1, 20000) == Lw.MODE_STREAM_W4
