@@ -484,8 +484,9 @@ def test_stream_groups_per_thread_choice(monkeypatch):
     assert bits(Lw.V_F32, 2, 1, 720 * 1440) == Lw.MODE_STREAM_W2
     # config 1: 1 f64 leaf, 20000 kept -> the W = 2 grid (10 workgroups) would split: W = 1
     assert bits(Lw.V_F64, 1, 1, 20000) == 0
-    # the elided rechunk+mean: 25 tasks of 2000 kept -> W = 1
-    assert bits(Lw.V_F32, 1, 25, 2000) == 0
+    # the elided rechunk+mean: 2500 source-chunk pieces of 1000 kept -> W = 1
+    # (a W = 2 workgroup would cover 2048 elements: half its waves idle)
+    assert bits(Lw.V_F32, 1, 2500, 1000) == 0
     # 4-leaf f64 programs (vorticity) already hold 256 B per lane -> W = 1
     assert bits(Lw.V_F64, 4, 100, 720000) == 0
     # a 1-leaf f32 mean over a wide kept dim -> W = 2
