@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 7
+#define CUBED_ABI_VERSION 8
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
