@@ -64,3 +64,37 @@ def test_store_rechunks_to_target(tmp_path, spec):
     assert np.array_equal(Z.open_array(str(tmp_path / "s.zarr"))[...], np.arange(600).reshape(20, 30))
     with pytest.raises(ValueError, match="Different number"):
         cubed.store([x, x], [t])
+
+
+def test_reference_quad_means_shape(tmp_path, spec):
+    """The reference's own quad-means test (cubed/tests/test_core.py:540-570):
+    u, v = random((50, 1, 987, 1920), chunks=(10, 1, -1, -1)) f64, mean(u*v,
+    axis=0) computed twice -- default optimizer and fuse_all_optimize_dag --
+    written with to_zarr and read back; the reference asserts the two stores
+    are equal.  Here they must also match the oracle's chunked rounds (f64
+    accumulation in a different association: rtol 1e-12)."""
+    from cubed_amd.core.optimization import fuse_all_optimize_dag
+
+    def quad_means(t_length):
+        u = crandom.random((t_length, 1, 987, 1920), chunks=(10, 1, -1, -1), spec=spec)
+        v = crandom.random((t_length, 1, 987, 1920), chunks=(10, 1, -1, -1), spec=spec)
+        return xp.mean(u * v, axis=0)
+
+    random.seed(42)
+    m0 = quad_means(50)
+    random.seed(42)
+    m1 = quad_means(50)
+    cubed.to_zarr(m0, store=str(tmp_path / "result0"))
+    cubed.to_zarr(m1, store=str(tmp_path / "result1"), optimize_function=fuse_all_optimize_dag)
+    res0 = Z.open_array(str(tmp_path / "result0"))[...]
+    res1 = Z.open_array(str(tmp_path / "result1"))[...]
+    assert res0.shape == (1, 987, 1920) and res0.dtype == np.float64
+    np.testing.assert_array_equal(res0, res1)
+
+    random.seed(42)
+    s1, s2 = [random.getrandbits(128) for _ in range(2)]
+    chunks = (10, 1, 987, 1920)
+    U = R.random_array((50, 1, 987, 1920), chunks, s1)
+    V = R.random_array((50, 1, 987, 1920), chunks, s2)
+    exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
+    assert np.allclose(res0, exp, rtol=1e-12, atol=0)
