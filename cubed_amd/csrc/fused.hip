@@ -166,14 +166,14 @@ int stream_groups(const cubed_program_t& P) {
 // reduced dim runs unsplit (a time split costs more than the occupancy it
 // adds: config 2 W = 2 unsplit 6.81 TB/s vs 6.02 for the round-2 3-way
 // split, profiles/r02_stream_ab.log); smaller grids split toward
-// CUBED_AMD_STREAM_TARGET workgroups (default 2048, ~8 per CU: config 1 at
-// 256 took 2.7x longer).
+// CUBED_AMD_STREAM_TARGET workgroups (default 1024, ~4 per CU: config 1's
+// stream 0.503 ms vs 0.542 at 2048, 0.59-0.62 at 4096-8192, 1.10 at 256).
 static int64_t stream_target() {
   if (const char* e = getenv("CUBED_AMD_STREAM_TARGET")) {
     const long v = atol(e);
     if (v >= 1 && v <= (1 << 20)) return v;
   }
-  return 2048;
+  return 1024;
 }
 
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,

@@ -14,7 +14,10 @@ node dtype, which is exactly the rounding the fused evaluation applies to it
 
 Supported: maps whose output space is the task space (out_axes identity) and
 reductions whose inputs are single chunks at the task's own block (the
-per-chunk stage of ``reduction``, core/ops.py:838-847).  Anything else keeps
+per-chunk stage of ``reduction``, core/ops.py:838-847).  A program drawing
+from more than one random stream (the VM carries one Philox key per task)
+materialises all but one stream the same way: ``mean(u * v)`` of two
+unmaterialised ``random`` arrays (the reference's own quad_means test).  Anything else keeps
 raising LoweringError (there is no host path).
 """
 
@@ -81,7 +84,20 @@ def pick_subexpr(p: ir.ExprProgram) -> Optional[ir.Expr]:
         k = (len(lv), len(collect_leaves_nodes(e)))
         if best_key is None or k > best_key:
             best, best_key = e, k
+    if best is None:
+        # one random stream per fused program (cubed_task_t carries one
+        # Philox key): u * v of two unmaterialised random arrays
+        # (test_core.py:540-570 quad_means) materialises all but one stream
+        rnd = [l for l in collect_leaves(pre) if isinstance(l, ir.Philox)]
+        if len(rnd) > 1:
+            for e in nodes:
+                if isinstance(e, ir.Philox) and _full_space(e, p.ndim):
+                    return e
     return best
+
+
+def _full_space(leaf, ndim: int) -> bool:
+    return tuple(leaf.axes) == tuple(range(ndim))
 
 
 def collect_leaves_nodes(e):
@@ -142,6 +158,15 @@ def _space_geometry(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys)
             ref = leaf
             break
     if ref is None:
+        # only random inputs: the random array's own blocks are the space
+        for leaf in collect_leaves(_pre_exprs(program)):
+            if isinstance(leaf, ir.Philox) and tuple(leaf.axes) == ident:
+                coords = {}
+                for k in keys:
+                    a = cfg.block_function(("out",) + tuple(k))[leaf.block_arg]
+                    coords[tuple(k)] = tuple(a[1:])
+                shape = tuple(int(sum(c)) for c in leaf.chunks)
+                return shape, tuple(tuple(c) for c in leaf.chunks), coords
         raise LoweringError("split: no full-space input defines the reduction's space")
     coords = {}
     arr = None

@@ -201,6 +201,8 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     got = xp.mean((a + 1) * 2, axis=0).compute(resume=True)
     exp = R.mean((x + 1) * 2, (50, 1000), 0, allowed_mem=2_000_000_000)
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
+    # the streaming map branch (no reduction): one IEEE op per element, bit-exact
+    np.testing.assert_array_equal(((a + 1) * 2).compute(resume=True), (x + 1) * 2)
 
     bits = {1: 0, 2: L.MODE_STREAM_W2, 4: L.MODE_STREAM_W4}[int(w)]
     streams = [l for l in _fused_launches(e) if l.prog.mode & L.MODE_STREAM]

