@@ -203,6 +203,16 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
     # the streaming map branch (no reduction): one IEEE op per element, bit-exact
     np.testing.assert_array_equal(((a + 1) * 2).compute(resume=True), (x + 1) * 2)
+    # a full reduction runs "lifted" in partials mode (per-element SoA
+    # partials, then a fold): the W-group partial writes
+    random.seed(9)
+    b = crandom.random((200, 20000), chunks=(50, 20000), spec=spec)
+    arrays_to_plan(b).execute(executor=e, array_names=[b.name])
+    (sb,) = seeds(9, 1)
+    y = R.random_array((200, 20000), (50, 20000), sb)
+    got = xp.mean(b * 3).compute(resume=True)
+    assert np.allclose(got, np.mean(y * 3), rtol=1e-12, atol=0)
+    assert any(l.prog.mode & L.MODE_PARTIALS and l.prog.mode & L.MODE_STREAM for l in _fused_launches(e))
 
     bits = {1: 0, 2: L.MODE_STREAM_W2, 4: L.MODE_STREAM_W4}[int(w)]
     streams = [l for l in _fused_launches(e) if l.prog.mode & L.MODE_STREAM]
