@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void k_copy_rows(const cubed_box_t* __restr
 // words whatever the row length (rechunk pieces of 4000-B rows no longer end
 // in partial lines per wave); each lane finds its source row by one 32-bit
 // division (host guarantees < 2^31 words per box).
-template <int W, int UN>
+template <int W, int UN, bool NTL = true>
 __global__ __launch_bounds__(kBlock) void k_copy_flat(const cubed_box_t* __restrict__ boxes,
                                                       int64_t nboxes, int32_t isz, int64_t bpb,
                                                       int64_t segs_per_block) {
@@ -166,7 +166,8 @@ __global__ __launch_bounds__(kBlock) void k_copy_flat(const cubed_box_t* __restr
       if (i < w_end) {
         const uint32_t r = (uint32_t)i / nw, c = (uint32_t)i - r * nw;
         const CUBED_G T* __restrict__ src = (const CUBED_G T*)(uintptr_t)(sbase + (int64_t)r * sstr);
-        v[k] = __builtin_nontemporal_load(src + c);
+        if constexpr (NTL) v[k] = __builtin_nontemporal_load(src + c);
+        else v[k] = src[c];
       }
     }
 #pragma unroll
@@ -293,7 +294,15 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
     const char* xe = getenv("CUBED_AMD_COPY_XCD");
     if (!(xe && xe[0] == '0') && nboxes > 1) bpb = (bpb + 7) / 8 * 8;
     const dim3 grid = grid2(nboxes * bpb);
-    switch (width) {
+    // cached source loads for 16-B lanes: a 4000-B piece row starts and ends
+    // mid-line, and the neighbouring piece (next box, same XCD) finds the
+    // shared lines in L2 -- non-temporal loads let them go: PMC fetch 1.078x
+    // -> 1.004x algorithmic, config 3 copy 3.81 -> 3.71 ms
+    // (profiles/r02_stream_ab.log); CUBED_AMD_COPY_NTLOAD=1 for A/B runs
+    const char* ne = getenv("CUBED_AMD_COPY_NTLOAD");
+    if (!(ne && ne[0] == '1') && width == 16) {
+      hipLaunchKernelGGL((k_copy_flat<16, UN, false>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb);
+    } else switch (width) {
       case 16: hipLaunchKernelGGL((k_copy_flat<16, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
       case 8: hipLaunchKernelGGL((k_copy_flat<8, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
       case 4: hipLaunchKernelGGL((k_copy_flat<4, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
