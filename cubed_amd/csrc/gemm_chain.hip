@@ -39,6 +39,7 @@
 //                      checked.  Correctness path, not a fast path.
 #include "common.h"
 #include <stdio.h>
+#include <stdlib.h>
 
 namespace cubed {
 extern thread_local char g_err[512];
@@ -376,12 +377,14 @@ constexpr int HF_BM = 128, HF_BN = 128, HF_BK = 32;
 
 struct F4 { float x, y, z, w; };
 
-template <int LDA_S, int LDB_S>
+// DB: two LDS slots -- the next tile's registers are stored into the other
+// slot right after this tile's MFMAs, one barrier per K step instead of two
+template <int LDA_S, int LDB_S, bool DB = false>
 __global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
                                                         int64_t tiles_m, int64_t tiles_n) {
-  __shared__ float As[HF_BK][LDA_S];
-  __shared__ float Bs[HF_BK][LDB_S];
+  __shared__ float As_[DB ? 2 : 1][HF_BK][LDA_S];
+  __shared__ float Bs_[DB ? 2 : 1][HF_BK][LDB_S];
   int64_t t, m0, n0;
   tile_of<HF_BM, HF_BN, 8>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
@@ -452,7 +455,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chai
       ke = ks + segs[s].k;
     }
   };
-  auto store = [&]() {
+  auto store = [&](int slot) {
+    float (*As)[LDA_S] = As_[slot];
+    float (*Bs)[LDB_S] = Bs_[slot];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int f = tid + 256 * i;
@@ -470,15 +475,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chai
 
   load(0);
   advance(HF_BK);
-  store();
+  store(0);
   __syncthreads();
   const int hi = lane >> 5, lo = lane & 31;
+  int cur = 0;
   for (int64_t k0 = 0; k0 < KT; k0 += HF_BK) {
     const bool more = k0 + HF_BK < KT;
     if (more) {
       load(k0 + HF_BK);  // in flight during this tile's MFMAs
       advance(k0 + 2 * HF_BK);
     }
+    const float (*As)[LDA_S] = As_[cur];
+    const float (*Bs)[LDB_S] = Bs_[cur];
 #pragma unroll 4
     for (int kk = 0; kk < HF_BK; kk += 2) {
       const float a0 = As[kk + hi][wm + lo], a1 = As[kk + hi][wm + 32 + lo];
@@ -488,10 +496,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chai
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
-    __syncthreads();
-    if (more) {
-      store();
+    if constexpr (DB) {
+      // the other slot was last read in the previous step, before its barrier
+      if (more) store(cur ^ 1);
       __syncthreads();
+      cur ^= 1;
+    } else {
+      __syncthreads();
+      if (more) {
+        store(0);
+        __syncthreads();
+      }
     }
   }
   CUBED_G float* __restrict__ C = (CUBED_G float*)(uintptr_t)T->c;
@@ -667,8 +682,16 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
     const int64_t blocks = ntasks * tm * tn;
     if (blocks > 0x7fffffff) return fail("grid too large");
-    hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       d_tasks, d_segs, tm, tn);
+    // single LDS slot: the double-buffered form (CUBED_AMD_GEMM_F32_DB=1, one
+    // barrier per step, 75 KB of LDS: 2 instead of 3 waves per SIMD)
+    // measured 101 vs 111 TF on config 5
+    const char* de = getenv("CUBED_AMD_GEMM_F32_DB");
+    if (de && de[0] == '1')
+      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                         d_tasks, d_segs, tm, tn);
+    else
+      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
+                         d_tasks, d_segs, tm, tn);
   } else {
     const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
     const int64_t blocks = ntasks * tm * tn;
