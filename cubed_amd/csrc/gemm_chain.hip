@@ -379,8 +379,8 @@ struct F4 { float x, y, z, w; };
 
 // DB: two LDS slots -- the next tile's registers are stored into the other
 // slot right after this tile's MFMAs, one barrier per K step instead of two
-template <int LDA_S, int LDB_S, bool DB = false>
-__global__ __launch_bounds__(256, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
+template <int LDA_S, int LDB_S, bool DB = false, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
                                                         int64_t tiles_m, int64_t tiles_n) {
   __shared__ float As_[DB ? 2 : 1][HF_BK][LDA_S];
@@ -686,8 +686,12 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     // barrier per step, 75 KB of LDS: 2 instead of 3 waves per SIMD)
     // measured 101 vs 111 TF on config 5
     const char* de = getenv("CUBED_AMD_GEMM_F32_DB");
+    const char* oe = getenv("CUBED_AMD_GEMM_F32_OCC");  // A/B: 128-VGPR build, 4 waves per SIMD
     if (de && de[0] == '1')
       hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                         d_tasks, d_segs, tm, tn);
+    else if (oe && oe[0] == '4')
+      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32, false, 4>), dim3((unsigned)blocks), dim3(256), 0, st,
                          d_tasks, d_segs, tm, tn);
     else
       hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
