@@ -194,6 +194,10 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     const int64_t base = ntasks * L.bpt;
     if (P->nfields > 0 && base < (256 * 9) / 10 && max_red >= 64)
       L.nsplit = (int32_t)choose_split(base, max_red / 16, stream_target());
+    if (const char* e = getenv("CUBED_AMD_STREAM_SPLIT")) {  // A/B runs: a forced split count
+      const long v = atol(e);
+      if (P->nfields > 0 && v >= 1 && v <= 64 && v <= max_red) L.nsplit = (int32_t)v;
+    }
     L.blocks = ntasks * L.nsplit * L.bpt;
   } else if (L.kernel == 0) {
     const int64_t items = (max_kept + L.vec - 1) / L.vec;
