@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := cubed_amd/csrc
-SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm.hip $(CSRC)/gemm_chain.hip $(CSRC)/blas.hip
+SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm_chain.hip
 CPPSRCS := $(CSRC)/codec.cpp
 OBJS := $(SRCS:.hip=.o) $(CPPSRCS:.cpp=.o)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
@@ -18,7 +18,7 @@ $(CSRC)/%.o: $(CSRC)/%.cpp include/cubed_amd.h
 	g++ -O3 -fPIC -std=c++17 -Iinclude -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -L/opt/rocm/lib -lhiprtc -lrocblas -lz -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@ -L/opt/rocm/lib -lhiprtc -lz -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

@@ -59,7 +59,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
-EXTRAS = ("rechunk", "rechunk_mean", "config1", "vorticity", "matmul_f32", "matmul_bf16")
+EXTRAS = ("rechunk", "rechunk_mean", "rechunk_mean_share", "config1", "vorticity", "matmul_f32",
+          "matmul_bf16")
 
 
 def parse(argv=None):
@@ -157,14 +158,21 @@ def max_over_ranks(dt, world):
     return dt
 
 
+HOST_US = []  # host seconds of each call inside the last timed region
+
+
 def timed(fn, steps, world):
     """Mean seconds per call over ``steps`` calls, barrier + synchronize on
-    both sides, max over ranks."""
+    both sides, max over ranks.  The host time of each call (the enqueue:
+    nothing synchronises inside a step) is kept in HOST_US."""
     sync()
     barrier(world)
+    HOST_US.clear()
     t0 = time.perf_counter()
     for _ in range(steps):
+        h0 = time.perf_counter()
         fn()
+        HOST_US.append(time.perf_counter() - h0)
     sync()
     barrier(world)
     return max_over_ranks((time.perf_counter() - t0) / steps, world)
@@ -181,28 +189,38 @@ def timed_launches(ex, fn, steps, world):
     return dt, timer.summary()
 
 
+def overhead(dt, summ, steps):
+    """Per-step time outside the kernels: ``host_overhead_us`` = step time -
+    sum of the step's launch times (HIP events); ``host_enqueue_us`` = the
+    median host time of one step call (DAG walk or schedule replay + launch
+    calls; it overlaps the previous step's kernels)."""
+    launched = sum(c * ms for c, ms in summ.values()) / max(1, steps)
+    return {"host_overhead_us": round((dt * 1e3 - launched) * 1e3, 1),
+            "host_enqueue_us": round(float(np.median(HOST_US)) * 1e6, 1) if HOST_US else None}
+
+
 def fmt_launches(summ):
     return {f"{k[0]}#{k[1]}:{k[2]}": round(v[1], 4) for k, v in summ.items()}
 
 
-def reset_targets(plan, keep):
-    """Mark every array of the plan except ``keep`` unwritten, so the next
-    ``execute(resume=True)`` re-runs every op (inputs stay resident)."""
+def plan_targets(plan, keep):
+    """Every array of the plan except ``keep``: marking them unwritten makes
+    the next ``execute(resume=True)`` re-run every op (inputs stay resident)."""
     from cubed_amd.storage import DeviceArray
 
     keep = keep if isinstance(keep, (tuple, list)) else (keep,)
     kept = {id(a.zarray) for a in keep}
-    for _, d in plan._finalize_dag().nodes(data=True):
-        t = d.get("target")
-        if isinstance(t, DeviceArray) and id(t) not in kept:
-            t.written = False
+    return [d["target"] for _, d in plan._finalize_dag().nodes(data=True)
+            if isinstance(d.get("target"), DeviceArray) and id(d["target"]) not in kept]
 
 
 def step_fn(plan, ex, outs, keep):
     names = [o.name for o in outs]
+    targets = plan_targets(plan, keep)
 
     def step():
-        reset_targets(plan, keep)
+        for t in targets:
+            t.written = False
         plan.execute(executor=ex, resume=True, array_names=names)
     return step
 
@@ -233,6 +251,47 @@ def free_gpu():
 
     gc.collect()
     torch.cuda.empty_cache()
+
+
+# --------------------------------------------------------------------------- value checks
+# Full-size checks of every benchmarked output against a host-side numpy
+# restatement of the reference's arithmetic (f64 sums over the same resident
+# inputs, copied back chunk by chunk).  A failed check makes bench.py exit 1.
+
+CHECKS = []
+
+
+def check_close(got, exp, rtol, what):
+    got = np.asarray(got, dtype=np.float64)
+    exp = np.asarray(exp, dtype=np.float64)
+    rel = np.abs(got - exp) / np.maximum(np.abs(exp), 1e-300)
+    return {"kind": "oracle", "pass": bool(np.all(rel <= rtol)), "rtol": rtol,
+            "max_rel_err": float(np.max(rel)) if rel.size else 0.0, "what": what}
+
+
+def column_means_f64(arr):
+    """f64 mean over axis 0 of a resident 2-d array, chunk rows at a time."""
+    import itertools
+
+    acc = np.zeros(arr.shape[1], dtype=np.float64)
+    for i, j in itertools.product(range(arr.numblocks[0]), range(arr.numblocks[1])):
+        c0 = arr.chunk_start((i, j))[1]
+        blk = arr.read_chunk((i, j))
+        acc[c0:c0 + blk.shape[1]] += np.sum(blk, axis=0, dtype=np.float64)
+    return acc / arr.shape[0]
+
+
+def device_chunk(arr, coords):
+    """torch view (on the device) of one resident chunk, in its dtype."""
+    import torch
+
+    tdt = {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+    ext = arr.chunk_extent(coords)
+    dt = np.dtype(arr.dtype)
+    nb = int(np.prod(ext)) * dt.itemsize
+    start = arr.local_slot(coords) * arr.slot_bytes(None)
+    raw = arr.slabs[None][start:start + nb]
+    return raw.view(tdt.get(dt, torch.bfloat16)).reshape(ext)
 
 
 # --------------------------------------------------------------------------- workloads
@@ -291,18 +350,19 @@ def rechunk_extra(args, ex, rank, world):
         ntasks = [d["primitive_op"].num_tasks for d in ops]
         step = step_fn(plan, ex, [y], x)
         step()
-        dt, summ = timed_launches(ex, step, 5, world)
+        dt, summ = timed_launches(ex, step, 10, world)
         copies = {k: v for k, v in summ.items() if k[2] in ("CopyLaunch", "RechunkLaunch")}
         per_op_ms = [v[1] for v in copies.values()]
         r = dict(metric="rechunk effective input GB/s", value=round(x.nbytes / dt / 1e9, 1),
                  ms=round(dt * 1e3, 4), allowed_mem=mem, ops=len(ops), tasks=ntasks,
-                 launches_ms=fmt_launches(summ))
+                 launches_ms=fmt_launches(summ), **overhead(dt, summ, 10))
         if world == 1 and copies:
             key, ms = max(copies.items(), key=lambda kv: kv[1][1])[0], max(per_op_ms)
             # algorithmic bytes of one copy launch: every element read once + written once
             r["roofline"] = roofline_hbm(2 * x.nbytes, ms, "rechunk_copy", args,
                                          f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
         r["check"] = _rechunk_spot_check(x, y, ex, rank, world)
+        CHECKS.append((f"rechunk {mem}", r["check"]))
         res[f"plan_{mem}"] = r
         if mem == "288GB" and rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_rechunk_baseline(x, ex)
@@ -315,7 +375,7 @@ def _rechunk_spot_check(x, y, ex, rank, world):
     """Bit-exact check of the first and last target column chunks (and one
     in the middle) against the source slices they must hold."""
     if world > 1:
-        return "skipped (distributed: covered by tests/test_gpu_dist.py)"
+        return {"kind": "skipped", "pass": True, "what": "distributed: covered by tests/test_gpu_dist.py"}
     X, Y = x.zarray, y.zarray
     nb = Y.numblocks[1]
     ok = True
@@ -327,7 +387,7 @@ def _rechunk_spot_check(x, y, ex, rank, world):
             src = X.read_chunk((i, 0))[:, c0:c0 + w]
             r0 = X.chunk_start((i, 0))[0]
             ok &= bool(np.array_equal(got[r0:r0 + src.shape[0]].view(np.uint32), src.view(np.uint32)))
-    return "bit-exact" if ok else "MISMATCH"
+    return {"kind": "oracle", "pass": ok, "what": "bit-exact: 3 target column chunks x 3 source row bands"}
 
 
 def rechunk_mean_extra(args, ex, rank, world):
@@ -347,19 +407,65 @@ def rechunk_mean_extra(args, ex, rank, world):
     x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
     arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
     out = {}
+    exp = None
     for mode in ("rechunk elided", "materialised"):
         ex.elide_rechunks = mode == "rechunk elided"
         m = xp.mean(x.rechunk((N, 1000)), axis=0)
         plan = arrays_to_plan(m)
         step = step_fn(plan, ex, [m], x)
         step()
-        dt, summ = timed_launches(ex, step, 5, world)
-        out["elided" if mode.startswith("rechunk") else "materialised"] = dict(
-            metric=f"rechunk+mean effective input GB/s ({mode})", value=round(x.nbytes / dt / 1e9, 1),
-            ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+        dt, summ = timed_launches(ex, step, 10, world)
+        r = dict(metric=f"rechunk+mean effective input GB/s ({mode})", value=round(x.nbytes / dt / 1e9, 1),
+                 ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ), **overhead(dt, summ, 10))
+        if world == 1:
+            if exp is None:
+                exp = column_means_f64(x.zarray).astype(np.float32)
+            got = m.compute(resume=True)
+            r["check"] = check_close(got, exp, 1e-6, "oracle: f64 column means of the resident input")
+            CHECKS.append((f"rechunk_mean {mode}", r["check"]))
+        out["elided" if mode.startswith("rechunk") else "materialised"] = r
         del m, plan
         ex._exec_dags.clear()
     ex.elide_rechunks = True
+    return out
+
+
+def rechunk_mean_share_extra(args, ex, rank, world):
+    """The per-rank share of config 3's rechunk+mean on 8 GPUs, timed on one:
+    mean(x.rechunk(columns), axis=0) over 6250 of the 50000 source rows
+    (row chunks of 1000: 6 full + one of 250), rechunk elided.  With the
+    block-cyclic layout the busiest of 8 ranks holds 7 of the 50 row chunks
+    (7000 rows); DESIGN.md (e) predicts the 8-GPU step from this piece, the
+    per-rank partials (50000 x {n, total}) and one RCCL reduce."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    out = {}
+    for rows in (6250, 7000):
+        N = 50000
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2001)
+        x = xp.astype(crandom.random((rows, N), chunks=(1000, N), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        m = xp.mean(x.rechunk((rows, 1000)), axis=0)
+        plan = arrays_to_plan(m)
+        step = step_fn(plan, ex, [m], x)
+        step()
+        step()
+        dt, summ = timed_launches(ex, step, 20, world)
+        r = dict(metric=f"rechunk+mean share ({rows} of 50000 rows) effective input GB/s",
+                 value=round(x.nbytes / dt / 1e9, 1), ms=round(dt * 1e3, 4),
+                 launches_ms=fmt_launches(summ), **overhead(dt, summ, 20))
+        if world == 1:
+            got = m.compute(resume=True)
+            exp = column_means_f64(x.zarray).astype(np.float32)
+            r["check"] = check_close(got, exp, 1e-6, "oracle: f64 column means of the resident input")
+            CHECKS.append((f"rechunk_mean_share {rows}", r["check"]))
+        out[f"rows_{rows}"] = r
+        del x, m, plan
+        free_gpu()
     return out
 
 
@@ -379,13 +485,25 @@ def config1_extra(args, ex, rank, world):
     step = step_fn(plan, ex, [m], a)
     for _ in range(2):
         step()
-    dt, summ = timed_launches(ex, step, 5, world)
+    dt, summ = timed_launches(ex, step, 10, world)
     r = dict(metric="config1 (a+1)*2 -> mean(axis=0) effective input GB/s",
-             value=round(a.nbytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+             value=round(a.nbytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ),
+             **overhead(dt, summ, 10))
     if world == 1:
         key, ms = dominant(summ, "FusedLaunch")
         r["roofline"] = roofline_hbm(a.nbytes, ms, "config1_stream", args,
                                      f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+        import itertools
+
+        A = a.zarray
+        acc = np.zeros(A.shape[1], dtype=np.float64)
+        for i, j in itertools.product(range(A.numblocks[0]), range(A.numblocks[1])):
+            c0 = A.chunk_start((i, j))[1]
+            blk = A.read_chunk((i, j))
+            acc[c0:c0 + blk.shape[1]] += np.sum((blk + 1) * 2, axis=0, dtype=np.float64)
+        r["check"] = check_close(m.compute(resume=True), acc / A.shape[0], 1e-12,
+                                 "oracle: f64 column sums of (a+1)*2 over the resident 20000^2 input")
+        CHECKS.append(("config1", r["check"]))
     return r
 
 
@@ -409,16 +527,32 @@ def vorticity_extra(args, ex, rank, world, T=1000):
     plan = arrays_to_plan(m)
     step = step_fn(plan, ex, [m], (a, b, x, y))
     step()
-    dt, summ = timed_launches(ex, step, 3, world)
+    dt, summ = timed_launches(ex, step, 10, world)
     in_bytes = a.nbytes + b.nbytes + x.nbytes + y.nbytes
     r = dict(metric="vorticity mean(a[1:]*x + b[1:]*y) effective input GB/s",
-             value=round(in_bytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ))
+             value=round(in_bytes / dt / 1e9, 1), ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ),
+             **overhead(dt, summ, 10))
     if world == 1:
         key, ms = dominant(summ, "FusedLaunch")
         # the dominant launch reads a[1:] and b[1:] (x, y broadcast: L2-resident)
         algo = 2 * (T - 1) * 900 * 800 * 8 + 2 * 900 * 800 * 8
         r["roofline"] = roofline_hbm(algo, ms, "vorticity_pieces", args,
                                      f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+        import itertools
+
+        A, B, X, Y = a.zarray, b.zarray, x.zarray, y.zarray
+        xs = {c: X.read_chunk(c) for c in itertools.product(*[range(n) for n in X.numblocks])}
+        ys = {c: Y.read_chunk(c) for c in itertools.product(*[range(n) for n in Y.numblocks])}
+        total = 0.0
+        for c in itertools.product(*[range(n) for n in A.numblocks]):
+            ca, cb = A.read_chunk(c), B.read_chunk(c)
+            if c[0] == 0:  # a[1:]: the first time row is not read
+                ca, cb = ca[1:], cb[1:]
+            total += float(np.sum(ca * xs[c[1:]] + cb * ys[c[1:]], dtype=np.float64))
+        exp = total / ((T - 1) * 900 * 800)
+        r["check"] = check_close(m.compute(resume=True), exp, 1e-12,
+                                 "oracle: chunked f64 sum over the resident (1000,900,800) inputs")
+        CHECKS.append(("vorticity", r["check"]))
     return r
 
 
@@ -445,7 +579,7 @@ def matmul_extra(args, ex, rank, world, dt_name):
     flop = 2.0 * n ** 3
     gemm = [v for k, v in summ.items() if k[2] == "GemmLaunch"]
     r = dict(metric=f"matmul {dt_name} TFLOP/s (whole plan)", value=round(flop / dt / 1e12, 1),
-             ms=round(dt * 1e3, 3), n=n, chunk=c, launches_ms=fmt_launches(summ))
+             ms=round(dt * 1e3, 3), n=n, chunk=c, launches_ms=fmt_launches(summ), **overhead(dt, summ, 2))
     if gemm and world == 1:
         gms = gemm[0][1]
         tf = flop / (gms * 1e-3) / 1e12
@@ -453,7 +587,36 @@ def matmul_extra(args, ex, rank, world, dt_name):
                          "unit": "TFLOP/s", "frac": round(tf / MFMA_PEAK_TFS[dt_name], 4),
                          "traffic": load_traffic(args.traffic_json, f"matmul_{dt_name}"),
                          "algo_flops": flop, "kernel": f"GemmLaunch, mean {gms:.3f} ms/launch"}
+    if world == 1:
+        r["check"] = matmul_check(A.zarray, B.zarray, m.zarray, n, c, dt_name == "bf16")
+        CHECKS.append((f"matmul_{dt_name}", r["check"]))
     return r
+
+
+def matmul_check(A, B, C, n, c, bf16):
+    """64 output entries (8 rows x 8 columns, seeded) against f64 dot products
+    of the copied-back operand rows / columns.  Bound (tests/test_gpu_matmul.py):
+    8 sqrt(K) 2^-24 sum|a||b| (+ 2^-8 |C| for a bf16 output)."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    rows = np.sort(rng.choice(n, 8, replace=False))
+    cols = np.sort(rng.choice(n, 8, replace=False))
+    nk = -(-n // c)
+    Ar = torch.stack([torch.cat([device_chunk(A, (i // c, kk))[i % c] for kk in range(nk)])
+                      for i in rows]).double().cpu().numpy()
+    Bc = torch.stack([torch.cat([device_chunk(B, (kk, j // c))[:, j % c] for kk in range(nk)])
+                      for j in cols], dim=1).double().cpu().numpy()
+    got = np.array([[float(device_chunk(C, (i // c, j // c))[i % c, j % c].double()) for j in cols]
+                    for i in rows])
+    exp = Ar @ Bc
+    bound = 8.0 * np.sqrt(n) * 2.0 ** -24 * (np.abs(Ar) @ np.abs(Bc))
+    if bf16:
+        bound = bound + 2.0 ** -8 * np.abs(exp)
+    err = np.abs(got - exp)
+    return {"kind": "bound", "pass": bool(np.all(err <= bound)), "entries": int(got.size),
+            "max_err_over_bound": float(np.max(err / bound)),
+            "what": "64 sampled entries vs f64 products of the resident rounded operands"}
 
 
 # --------------------------------------------------------------------------- CPU baselines
@@ -567,10 +730,11 @@ def main(argv=None):
     # algorithmic bytes of the dominant launch: the fused u*v -> mean kernel
     # reads this rank's u and v once (2 x 4.147e9 B at T=1000)
     algo = in_bytes // world
-    extra = {"launches_ms": fmt_launches(res["summ"])}
+    extra = {"launches_ms": fmt_launches(res["summ"]), **overhead(dt, res["summ"], args.steps)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(res, ex)
+        CHECKS.append(("quad-means", {"pass": cpu["gpu_matches_oracle_full_size"]}))
     del res
     free_gpu()
     wanted = [e for e in EXTRAS if not args.only or e in args.only.split(",")]
@@ -584,14 +748,17 @@ def main(argv=None):
                 extra[name] = rechunk_extra(args, ex, rank, world)
             elif name == "rechunk_mean":
                 extra[name] = rechunk_mean_extra(args, ex, rank, world)
+            elif name == "rechunk_mean_share":
+                extra[name] = rechunk_mean_share_extra(args, ex, rank, world)
             elif name == "config1":
                 extra[name] = config1_extra(args, ex, rank, world)
             elif name == "vorticity":
                 extra[name] = vorticity_extra(args, ex, rank, world)
             elif name.startswith("matmul"):
                 extra[name] = matmul_extra(args, ex, rank, world, name.split("_")[1])
-        except Exception as e:  # pragma: no cover - reported, not fatal
+        except Exception as e:  # pragma: no cover - reported, then fails the run
             extra[name] = {"error": repr(e)}
+            CHECKS.append((name, {"pass": False, "error": repr(e)}))
         free_gpu()
     line = {
         "metric": "effective input GB/s (node) for fused elementwise+mean (quad-means)",
@@ -610,19 +777,26 @@ def main(argv=None):
         "config": {"workload": "quad-means: mean(u*v, axis=0), u,v (1000,720,1440) f32 per GPU, "
                                "chunks (10,720,1440), Spec(allowed_mem=2GB, reserved_mem=100MB)",
                    "t_length_per_gpu": args.t_length, "parallelism": f"block-cyclic dp{world}",
-                   "extras_scaling": "strong (rechunk 50000^2 total), weak (others per GPU)"},
+                   "extras_scaling": "strong: every extra keeps its total size as N grows (rechunk and "
+                                     "rechunk+mean 50000^2, config 1 20000^2, vorticity T=1000, matmul "
+                                     "40000^2); only the headline quad-means weak-scales"},
         "roofline": roofline_hbm(algo, ms, "quad_means_fused", args,
                                  f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch"),
         "extra": extra,
     }
     if cpu is not None:
         line["cpu_baseline"] = cpu
+    failed = [name for name, c in CHECKS if not c.get("pass", False)]
+    line["checks_failed"] = failed
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    if failed:
+        sys.stderr.write(f"bench.py: value checks failed: {failed}\n")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

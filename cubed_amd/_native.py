@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 8  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 9  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -84,13 +84,6 @@ BOX_DTYPE = np.dtype([
     ("dst_stride", np.int64, (MAX_DIMS,)),
 ])
 
-GEMM_DTYPE = np.dtype([
-    ("a", np.int64), ("b", np.int64), ("c", np.int64),
-    ("m", np.int64), ("n", np.int64), ("k", np.int64),
-    ("lda", np.int64), ("ldb", np.int64), ("ldc", np.int64),
-    ("accumulate", np.int64),
-])
-
 # cubed_gemm_chain_t / cubed_gemm_seg_t (chained chunk GEMMs)
 CHAIN_DTYPE = np.dtype([
     ("c", np.int64), ("m", np.int64), ("n", np.int64), ("ldc", np.int64),
@@ -134,8 +127,6 @@ def lib():
     L.cubed_copy_boxes.argtypes = [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
                                    c_int64, c_int64, c_void_p]
     L.cubed_copy_boxes.restype = c_int
-    L.cubed_gemm_chunks.argtypes = [c_void_p, c_int64, c_int32, c_int64, c_int64, c_void_p]
-    L.cubed_gemm_chunks.restype = c_int
     L.cubed_gemm_chain_path.argtypes = [c_void_p, c_int64, c_void_p, c_int32, c_int32]
     L.cubed_gemm_chain_path.restype = c_int
     L.cubed_gemm_chain.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32, c_int32,
@@ -167,9 +158,6 @@ def lib():
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]
     L.cubed_combine_partials.restype = c_int
-    L.cubed_gemm_batched.argtypes = [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64,
-                                     c_int64, c_int64, c_int64, c_int64, c_int32, c_void_p]
-    L.cubed_gemm_batched.restype = c_int
     L.cubed_blosc_header.argtypes = [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64),
                                      POINTER(c_int), POINTER(c_int)]
     L.cubed_blosc_header.restype = c_int
@@ -196,11 +184,11 @@ def check(rc: int, what: str):
 
 EXPORTED_SYMBOLS = (
     "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_random_chunks",
-    "cubed_copy_boxes", "cubed_gemm_chunks", "cubed_abi_version", "cubed_last_error",
+    "cubed_copy_boxes", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
-    "cubed_gemm_batched", "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
+    "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_gemm_chain", "cubed_gemm_chain_path",
 )
 

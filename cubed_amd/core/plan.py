@@ -10,7 +10,6 @@ from __future__ import annotations
 import inspect
 import uuid
 from datetime import datetime
-from functools import lru_cache
 from typing import Callable, Optional
 
 import networkx as nx
@@ -82,12 +81,19 @@ class Plan:
                 dag.add_edge("arrays", n)
         return dag
 
-    @lru_cache
     def _finalize_dag(self, optimize_graph: bool = True, optimize_function=None) -> nx.MultiDiGraph:
-        dag = self.optimize(optimize_function).dag if optimize_graph else self.dag
-        dag = dag.copy()
-        dag = self._create_arrays_node(dag)
-        return nx.freeze(dag)
+        # cached on the plan (the reference's lru_cache, core/plan.py:178, would
+        # keep up to 128 finalized DAGs -- and the HBM of the launches an
+        # executor caches for them -- alive after their plans are dropped)
+        cache = self.__dict__.setdefault("_finalized", {})
+        key = (optimize_graph, optimize_function)
+        dag = cache.get(key)
+        if dag is None:
+            dag = self.optimize(optimize_function).dag if optimize_graph else self.dag
+            dag = dag.copy()
+            dag = self._create_arrays_node(dag)
+            dag = cache[key] = nx.freeze(dag)
+        return dag
 
     def execute(self, executor=None, callbacks=None, optimize_graph=True, optimize_function=None,
                 resume=None, spec=None, array_names=None, **kwargs):

@@ -276,13 +276,8 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
     if (nd != 2) return fail("cubed_copy_boxes: flat path needs 2-d boxes");
     if (max_box_elems <= 0 || max_box_elems >= ((int64_t)1 << 31)) return fail("cubed_copy_boxes: flat path box size");
     constexpr int UN = 4;
-    // segments per workgroup (16 = 64 KiB with 16-B lanes); CUBED_AMD_COPY_SPB
-    // overrides for A/B runs
-    int64_t spb = 16;
-    if (const char* e = getenv("CUBED_AMD_COPY_SPB")) {
-      const long v = atol(e);
-      if (v >= 1 && v <= 1024) spb = v;
-    }
+    // segments per workgroup (16 = 64 KiB with 16-B lanes)
+    const int64_t spb = 16;
     const int64_t nseg = (max_box_elems + 64 * UN - 1) / (64 * UN);
     int64_t bpb = (nseg + spb - 1) / spb;
     // a multiple of 8 workgroups per box: workgroup i of box b and of box
@@ -290,20 +285,16 @@ extern "C" int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int3
     // host orders boxes by source address -- run on the same XCD (round-robin
     // dispatch) at nearly the same time, so the 128-B line a 4000-B piece
     // boundary splits is fetched into that XCD's L2 once, not twice
-    // (CUBED_AMD_COPY_XCD=0: round-2 grid)
-    const char* xe = getenv("CUBED_AMD_COPY_XCD");
-    if (!(xe && xe[0] == '0') && nboxes > 1) bpb = (bpb + 7) / 8 * 8;
+    if (nboxes > 1) bpb = (bpb + 7) / 8 * 8;
     const dim3 grid = grid2(nboxes * bpb);
     // cached source loads for 16-B lanes: a 4000-B piece row starts and ends
     // mid-line, and the neighbouring piece (next box, same XCD) finds the
     // shared lines in L2 -- non-temporal loads let them go: PMC fetch 1.078x
     // -> 1.004x algorithmic, config 3 copy 3.81 -> 3.71 ms
-    // (profiles/r02_stream_ab.log); CUBED_AMD_COPY_NTLOAD=1 for A/B runs
-    const char* ne = getenv("CUBED_AMD_COPY_NTLOAD");
-    if (!(ne && ne[0] == '1') && width == 16) {
+    // (profiles/r02_stream_ab.log)
+    if (width == 16) {
       hipLaunchKernelGGL((k_copy_flat<16, UN, false>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb);
     } else switch (width) {
-      case 16: hipLaunchKernelGGL((k_copy_flat<16, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
       case 8: hipLaunchKernelGGL((k_copy_flat<8, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
       case 4: hipLaunchKernelGGL((k_copy_flat<4, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;
       default: hipLaunchKernelGGL((k_copy_flat<1, UN>), grid, dim3(kBlock), 0, st, d_boxes, nboxes, isz, bpb, spb); break;

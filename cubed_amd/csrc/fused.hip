@@ -166,15 +166,9 @@ int stream_groups(const cubed_program_t& P) {
 // reduced dim runs unsplit (a time split costs more than the occupancy it
 // adds: config 2 W = 2 unsplit 6.81 TB/s vs 6.02 for the round-2 3-way
 // split, profiles/r02_stream_ab.log); smaller grids split toward
-// CUBED_AMD_STREAM_TARGET workgroups (default 1024, ~4 per CU: config 1's
-// stream 0.503 ms vs 0.542 at 2048, 0.59-0.62 at 4096-8192, 1.10 at 256).
-static int64_t stream_target() {
-  if (const char* e = getenv("CUBED_AMD_STREAM_TARGET")) {
-    const long v = atol(e);
-    if (v >= 1 && v <= (1 << 20)) return v;
-  }
-  return 1024;
-}
+// 1024 workgroups (~4 per CU: config 1's stream 0.503 ms vs 0.542 at 2048,
+// 0.59-0.62 at 4096-8192, 1.10 at 256).
+static constexpr int64_t kStreamTarget = 1024;
 
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red, int stream_w) {
@@ -193,11 +187,7 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     if (L.bpt > 65536) L.bpt = 65536;
     const int64_t base = ntasks * L.bpt;
     if (P->nfields > 0 && base < (256 * 9) / 10 && max_red >= 64)
-      L.nsplit = (int32_t)choose_split(base, max_red / 16, stream_target());
-    if (const char* e = getenv("CUBED_AMD_STREAM_SPLIT")) {  // A/B runs: a forced split count
-      const long v = atol(e);
-      if (P->nfields > 0 && v >= 1 && v <= 64 && v <= max_red) L.nsplit = (int32_t)v;
-    }
+      L.nsplit = (int32_t)choose_split(base, max_red / 16, kStreamTarget);
     L.blocks = ntasks * L.nsplit * L.bpt;
   } else if (L.kernel == 0) {
     const int64_t items = (max_kept + L.vec - 1) / L.vec;

@@ -682,20 +682,10 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
     const int64_t blocks = ntasks * tm * tn;
     if (blocks > 0x7fffffff) return fail("grid too large");
-    // single LDS slot: the double-buffered form (CUBED_AMD_GEMM_F32_DB=1, one
-    // barrier per step, 75 KB of LDS: 2 instead of 3 waves per SIMD)
-    // measured 101 vs 111 TF on config 5
-    const char* de = getenv("CUBED_AMD_GEMM_F32_DB");
-    const char* oe = getenv("CUBED_AMD_GEMM_F32_OCC");  // A/B: 128-VGPR build, 4 waves per SIMD
-    if (de && de[0] == '1')
-      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32, true>), dim3((unsigned)blocks), dim3(256), 0, st,
-                         d_tasks, d_segs, tm, tn);
-    else if (oe && oe[0] == '4')
-      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32, false, 4>), dim3((unsigned)blocks), dim3(256), 0, st,
-                         d_tasks, d_segs, tm, tn);
-    else
-      hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
-                         d_tasks, d_segs, tm, tn);
+    // single LDS slot: the double-buffered form (one barrier per step, 75 KB
+    // of LDS: 2 instead of 3 waves per SIMD) measured 101 vs 111 TF on config 5
+    hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       d_tasks, d_segs, tm, tn);
   } else {
     const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
     const int64_t blocks = ntasks * tm * tn;

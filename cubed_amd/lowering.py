@@ -242,6 +242,9 @@ def canonical_boxes(boxes: List[Box]):
     return nd, out
 
 
+COPY_FLAT = True  # tests set False to run packed pieces on the per-row kernel
+
+
 class CopyLaunch:
     """One cubed_copy_boxes launch."""
 
@@ -268,8 +271,8 @@ class CopyLaunch:
             self.work = max(math.prod(b.extent[:-1]) for b in boxes)
             self.row_bytes = max(b.extent[-1] for b in boxes) * itemsize
             words = max(b.extent[0] * b.extent[1] * itemsize // lane for b in boxes) if nd == 2 else 0
-            if (nd == 2 and 0 < words < 2 ** 31 and all(b.dstride[0] == b.extent[1] for b in boxes)
-                    and os.environ.get("CUBED_AMD_COPY_FLAT", "1") != "0"):
+            if COPY_FLAT and nd == 2 and 0 < words < 2 ** 31 and \
+                    all(b.dstride[0] == b.extent[1] for b in boxes):
                 # packed destinations (rechunk pieces): walk each box as one
                 # run of destination words
                 self.path = nat.COPY_FLAT
@@ -737,16 +740,11 @@ class FusedLaunch:
                                        self.ws_bytes, stream), "cubed_fused_chunks")
 
 
-GEMM_PATH = __import__("os").environ.get("CUBED_AMD_GEMM", "native")  # "native" | "blas"
-
-
 class GemmLaunch:
     """Chained chunk GEMMs of one matmul / tensordot (``cubed_gemm_chain``):
     one task per output chunk, each summing its segment products in one K
     loop (a per-chunk product is a chain of one segment).  The hand-written
-    MFMA kernels (csrc/gemm_chain.hip) run every dtype; CUBED_AMD_GEMM=blas
-    sends single-segment f32 / f64 products to rocBLAS instead, kept only
-    as the library comparator of bench.py / tools/gemm_probe.py."""
+    kernels of csrc/gemm_chain.hip run every dtype (MFMA for bf16 / f32)."""
 
     def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None):
         import torch
@@ -758,22 +756,7 @@ class GemmLaunch:
         self.zero = zero_ptr
         self.path = nat.GEMM_AUTO if path is None else path
         self.flops = 2.0 * float(sum(int(t["m"]) * int(t["n"]) * int(t["ktot"]) for t in self.tasks))
-        self.blas = (GEMM_PATH == "blas" and in_code == out_code and
-                     in_code in (ir.dtype_code(np.float32), ir.dtype_code(np.float64)) and
-                     self.n and all(int(t["nseg"]) == 1 for t in self.tasks))
-        self.groups = []
         if not self.n:
-            return
-        if self.blas:
-            by_shape = {}
-            for t in self.tasks:
-                sg = self.segs[int(t["seg0"])]
-                key = (int(t["m"]), int(t["n"]), int(sg["k"]), int(sg["lda"]), int(sg["ldb"]),
-                       int(t["ldc"]), int(t["accumulate"]))
-                by_shape.setdefault(key, []).append((int(sg["a"]), int(sg["b"]), int(t["c"])))
-            for key, ptrs in by_shape.items():
-                arr = torch.tensor(np.array(ptrs, dtype=np.int64).T.copy(), device=device)  # (3, batch)
-                self.groups.append((key, arr))
             return
         self.d_tasks = torch.from_numpy(self.tasks.view(np.uint8).copy()).to(device)
         self.d_segs = torch.from_numpy(self.segs.view(np.uint8).copy()).to(device)
@@ -789,14 +772,6 @@ class GemmLaunch:
         if not self.n:
             return
         L = nat.lib()
-        if self.blas:
-            for (m, n, k, lda, ldb, ldc, acc), arr in self.groups:
-                base = arr.data_ptr()
-                batch = arr.shape[1]
-                nat.check(L.cubed_gemm_batched(self.in_code, base, base + 8 * batch, base + 16 * batch,
-                                               batch, m, n, k, lda, ldb, ldc, acc, stream),
-                          "cubed_gemm_batched")
-            return
         nat.check(L.cubed_gemm_chain(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.n,
                                      self.segs.ctypes.data, self.d_segs.data_ptr(), len(self.segs),
                                      self.in_code, self.out_code, self.zero, self.path, stream),
@@ -1634,7 +1609,7 @@ def _lift_dims(rows, n):
     if not kept or vol / kept < LIFT_MIN_ROWS:
         return set()
     return set(inner)
-LIFT_ENABLED = __import__("os").environ.get("CUBED_AMD_LIFT", "1") != "0"
+LIFT_ENABLED = True
 MODE_STREAM = 8  # include/cubed_amd.h CUBED_MODE_STREAM
 MODE_PARTIALS = 16  # include/cubed_amd.h CUBED_MODE_PARTIALS
 _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64: np.dtype(np.int64)}
@@ -1652,6 +1627,9 @@ def _stream_unroll(itemsize: int, nleaves: int) -> int:
     return 4 if nleaves <= 1 else 2
 
 
+FORCE_STREAM_W = None  # tests set 1 / 2 / 4 to run one program at every W
+
+
 def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
     """Mode bits for the kept groups per thread (W) of a streaming JIT kernel.
 
@@ -1661,13 +1639,11 @@ def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
     (>= 230 workgroups; config 1's split grid ran 2.7x slower with W = 2)
     and a task's kept extent fills at least 8 workgroups of 1024 W elements
     (the elided rechunk+mean's 1000-wide pieces left half of every
-    workgroup idle with W = 2: 2.7x slower; profiles/r02_stream_ab.log).
-    CUBED_AMD_STREAM_W (1/2/4) forces W for A/B runs."""
+    workgroup idle with W = 2: 2.7x slower; profiles/r02_stream_ab.log)."""
     isz = 4 if P.vtype == V_F32 else 8
     nl = max(1, P.nleaves)
-    forced = __import__("os").environ.get("CUBED_AMD_STREAM_W")
-    if forced in ("1", "2", "4"):
-        w = int(forced)
+    if FORCE_STREAM_W is not None:  # tests: every W on one program
+        w = FORCE_STREAM_W
     else:
         w = 256 // (_stream_unroll(isz, nl) * nl * 4 * isz)
         w = 4 if w >= 4 else 2 if w >= 2 else 1

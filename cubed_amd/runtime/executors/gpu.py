@@ -156,7 +156,14 @@ class GpuDagExecutor(DagExecutor):
         self.check_memory = check_memory
         self._cache: Dict[int, tuple] = {}
         self._uploads: Dict[int, DeviceArray] = {}
+        # device buffers made while lowering (scratch gathers, split
+        # temporaries) go to the cache entry being built, so they live as
+        # long as the launches that use them; outside a compile they belong
+        # to the executor
         self._scratch: List = []
+        self._sink: List = self._scratch
+        self._schedules: Dict = {}
+        self.replays = 0  # execute_dag calls served from a recorded schedule
         self.lowerer = Lowerer(self)
         self.comm = None
         self.rank, self.world = 0, 1
@@ -169,6 +176,7 @@ class GpuDagExecutor(DagExecutor):
         self.elide_rechunks = True
         self._agreed = set()
         self.elided = set()
+        self._resident_bytes = 0
 
     # -- plumbing used by the lowerer ------------------------------------------
     @property
@@ -242,9 +250,44 @@ class GpuDagExecutor(DagExecutor):
             return 0
 
         buf = torch.empty(max(nbytes, 16) + 256, dtype=torch.uint8, device=self.device)
-        self._scratch.append(buf)
+        self._sink.append(buf)
         p = buf.data_ptr()
         return (p + 255) // 256 * 256
+
+    def own(self, arr: DeviceArray):
+        """Tie an HBM temporary made while lowering (cubed_amd/split.py) to
+        the cache entry being built, after checking it fits next to the
+        plan's resident arrays."""
+        need = sum(arr.slot_bytes(f) for f in arr.fields) * arr.nchunks
+        if self.check_memory and self._resident_bytes + self.owned_bytes() + need > HBM_BYTES_PER_GPU:
+            raise MemoryError(f"a {need}-byte split temporary does not fit next to the plan's "
+                              f"{self._resident_bytes} bytes of HBM-resident arrays")
+        self._sink.append(arr)
+
+    def owned_bytes(self) -> int:
+        """HBM held by buffers of cached launches and of the executor."""
+        total = sum(_nbytes(b) for b in self._scratch)
+        for entry in self._cache.values():
+            total += sum(_nbytes(b) for b in entry[2])
+        return total
+
+    def _cache_put(self, key, obj, launches, owned):
+        """Cache ``launches`` (and the buffers they own) for ``obj``; the
+        entry goes when ``obj`` is collected (its id may then be reused)."""
+        self._cache[key] = (weakref.ref(obj), launches, owned)
+        weakref.finalize(obj, _drop_entry, weakref.ref(self), "_cache", key)
+
+    class _Collect:
+        def __init__(self, ex):
+            self.ex, self.owned = ex, []
+
+        def __enter__(self):
+            self.prev, self.ex._sink = self.ex._sink, self.owned
+            return self.owned
+
+        def __exit__(self, *exc):
+            self.ex._sink = self.prev
+            return False
 
     def gather_region(self, arr: DeviceArray, region, field, gathers) -> ArrView:
         """Copy a multi-chunk region into contiguous scratch; return its view
@@ -635,17 +678,18 @@ class GpuDagExecutor(DagExecutor):
         if entry is not None and entry[0]() is pipeline:
             return entry[1]
         err = None
-        try:
-            launches = self.lower_node(name, node)
-        except LoweringError as e:
-            err = e
+        with self._Collect(self) as owned:
+            try:
+                launches = self.lower_node(name, node)
+            except LoweringError as e:
+                err = e
         if self.world > 1 and not self.comm.all_ok(err is None):
             # a pipeline that cannot be lowered on one rank fails on all of them
             # (instead of leaving the others waiting in a collective)
             raise err or LoweringError(f"op {name} could not be lowered on another rank")
         if err is not None:
             raise err
-        self._cache[id(pipeline)] = (weakref.ref(pipeline), launches)
+        self._cache_put(id(pipeline), pipeline, launches, owned)
         return launches
 
     def chains_of(self, dag, array_names):
@@ -676,16 +720,25 @@ class GpuDagExecutor(DagExecutor):
                 if t is not ch.final_target:
                     self.elided.add(id(t))
         self._chains[key] = (weakref.ref(dag), (chains, members))
+        weakref.finalize(dag, _drop_entry, weakref.ref(self), "_chains", key)
         return chains, members
 
     def compiled_chain(self, chain):
         from ...gemm_chains import GemmChain
 
-        if isinstance(chain, GemmChain):
-            return self.compiled_gemm_chain(chain)
-        entry = self._cache.get(("chain", id(chain.first_spec)))
+        key = ("gemm" if isinstance(chain, GemmChain) else "chain", id(chain.first_spec))
+        entry = self._cache.get(key)
         if entry is not None and entry[0]() is chain.first_spec:
             return entry[1]
+        with self._Collect(self) as owned:
+            if isinstance(chain, GemmChain):
+                launches = self._lower_gemm_chain(chain)
+            else:
+                launches = self._lower_chain(chain)
+        self._cache_put(key, chain.first_spec, launches, owned)
+        return launches
+
+    def _lower_chain(self, chain):
         from ...chains import chain_rows, contributing_keys
 
         target = chain.final_target
@@ -701,31 +754,21 @@ class GpuDagExecutor(DagExecutor):
                 chain.program, chain.first_spec, target, keys,
                 rows_fn=lambda leaves, kinds: chain_piece_rows(self.lowerer, chain, leaves, kinds, keys),
                 sample_key=contributing_keys(chain, keys[0])[0])
-            launches = _with_gathers(launch, self.device)
-            self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
-            return launches
+            return _with_gathers(launch, self.device)
         if self.world > 1:
-            launches = self._compiled_chain_dist(chain, target, keys)
-            self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
-            return launches
+            return self._compiled_chain_dist(chain, target, keys)
         launch = self.lowerer.lower_expr_pipeline(
             chain.program, chain.first_spec, target, keys,
             rows_fn=lambda leaves, kinds: chain_rows(self.lowerer, chain, leaves, kinds, keys),
             sample_key=contributing_keys(chain, keys[0])[0])
-        launches = _with_gathers(launch, self.device)
-        self._cache[("chain", id(chain.first_spec))] = (weakref.ref(chain.first_spec), launches)
-        return launches
+        return _with_gathers(launch, self.device)
 
-    def compiled_gemm_chain(self, chain):
+    def _lower_gemm_chain(self, chain):
         """matmul's chunk products + k-sum as ONE cubed_gemm_chain launch
         (gemm_chains.py); with several GPUs each rank computes the output
         chunks it owns, after fetching the A row / B column chunks it lacks."""
         from ...gemm_chains import K_AXIS, chain_tables
 
-        key = ("gemm", id(chain.first_spec))
-        entry = self._cache.get(key)
-        if entry is not None and entry[0]() is chain.first_spec:
-            return entry[1]
         F = chain.final_target
         self.allocate(F)
         keys = self._task_keys(F)
@@ -755,7 +798,6 @@ class GpuDagExecutor(DagExecutor):
             raise LoweringError(f"matmul of {in_dt} is not lowered (f32, bf16, f64, int64)")
         out.append(GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
                               self.zero_page()))
-        self._cache[key] = (weakref.ref(chain.first_spec), out)
         return out
 
     def _compiled_chain_dist(self, chain, target, keys):
@@ -818,6 +860,7 @@ class GpuDagExecutor(DagExecutor):
             if isinstance(t, DeviceArray):
                 self.elided.add(id(t))
         self._exec_dags[key] = (weakref.ref(dag), new)
+        weakref.finalize(dag, _drop_entry, weakref.ref(self), "_exec_dags", key)
         return new
 
     def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
@@ -835,14 +878,24 @@ class GpuDagExecutor(DagExecutor):
 
     def _execute_dag(self, dag, callbacks, array_names, resume):
         stream = self.stream
+        key = (id(dag), tuple(array_names or ()), bool(resume), self.elide_rechunks, self.fuse_producers,
+               self.fuse_reductions, self.fuse_gemm_sums)
+        book = self._schedules.get(key)
+        if book is not None and book.dag_ref() is dag:
+            sched = book.lookup()
+            if sched is not None:
+                self.replays += 1
+                return self._run_schedule(sched, stream, callbacks)
+        plan_dag = dag
         dag = self.exec_dag(dag, array_names)
         nodes = dict(dag.nodes(data=True))
         chains, members = self.chains_of(dag, array_names)
         if self.check_memory:
             self._check_hbm(dag)
-        timing = self.timing
+        targets = [d["target"] for _, d in dag.nodes(data=True) if isinstance(d.get("target"), DeviceArray)]
+        state = tuple(t.written for t in targets)
+        steps = []
         for name, node in visit_nodes(dag, resume=resume):
-            t0 = time.time()
             if name in members:
                 launches = []  # ran as part of its chain's fused launch
             elif name in chains:
@@ -861,7 +914,7 @@ class GpuDagExecutor(DagExecutor):
                         self._agreed.add((name, id(ch)))
                         if not ok:
                             self._cache.pop(("chain", id(ch.first_spec)), None)
-                        self._cache.pop(("gemm", id(ch.first_spec)), None)
+                            self._cache.pop(("gemm", id(ch.first_spec)), None)
                     if not ok:
                         # not fusable after all: run the chain's pipelines one by one
                         chains.pop(name)
@@ -878,31 +931,68 @@ class GpuDagExecutor(DagExecutor):
                         launches = self.compiled(name, node)
             else:
                 launches = self.compiled(name, node)
-            for i, launch in enumerate(launches):
-                if timing is not None:
+            marks = []
+            if name not in chains:  # a chain head's partials are never materialised
+                marks = [nodes[out].get("target") for out in dag.successors(name)
+                         if isinstance(nodes[out].get("target"), DeviceArray)]
+            op = node.get("primitive_op")
+            events = list(node.get("fused_from", ())) + [(name, op.num_tasks if op is not None else 1)]
+            steps.append((name, tuple(launches), tuple(marks), tuple(events)))
+        sched = _Schedule(steps)
+        self._run_schedule(sched, stream, callbacks)
+        # later calls with the same plan, names, resume flag and written
+        # state replay the launch list without re-walking the DAG
+        if book is None or book.dag_ref() is not plan_dag:
+            book = self._schedules[key] = _Schedules(plan_dag, targets)
+            weakref.finalize(plan_dag, _drop_entry, weakref.ref(self), "_schedules", key)
+        book.add(state, sched)
+
+    def _run_schedule(self, sched, stream, callbacks):
+        timing = self.timing
+        gpu_events = callbacks is not None and self.device.type == "cuda"
+        marks_ev = []
+        if gpu_events:
+            import torch
+
+            ext = torch.cuda.ExternalStream(stream, device=self.device)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(ext)
+            marks_ev.append(ev)
+        host = [time.time()]
+        for name, launches, marks, _ in sched.steps:
+            if timing is None:
+                for launch in launches:
+                    launch.run(stream)
+            else:
+                for i, launch in enumerate(launches):
                     ev0, ev1 = timing.events()
                     ev0.record()
                     launch.run(stream)
                     ev1.record()
                     timing.add((name, i, type(launch).__name__), ev0, ev1)
-                else:
-                    launch.run(stream)
-            if name not in chains:  # a chain head's partials are never materialised
-                for out in dag.successors(name):
-                    target = nodes[out].get("target")
-                    if isinstance(target, DeviceArray):
-                        target.written = True
-            if callbacks is not None:
-                for fname, ntasks in node.get("fused_from", ()):
-                    ev = TaskEndEvent(array_name=fname, num_tasks=ntasks, function_start_tstamp=t0,
-                                      function_end_tstamp=time.time())
-                    ev.task_result_tstamp = time.time()
-                    for cb in callbacks:
-                        cb.on_task_end(ev)
-                op = node.get("primitive_op")
-                ev = TaskEndEvent(array_name=name, num_tasks=op.num_tasks if op is not None else 1,
-                                  function_start_tstamp=t0, function_end_tstamp=time.time())
-                ev.task_result_tstamp = time.time()
+            for t in marks:
+                t.written = True
+            if gpu_events:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(ext)
+                marks_ev.append(ev)
+            elif callbacks is not None:
+                host.append(time.time())
+        if callbacks is None:
+            return
+        if gpu_events:
+            # TaskEndEvents carry completion times: each op's end is its
+            # stream event, placed on the host clock from the last one
+            marks_ev[-1].synchronize()
+            t_end = time.time()
+            times = [t_end - ev.elapsed_time(marks_ev[-1]) * 1e-3 for ev in marks_ev]
+        else:
+            times = host
+        for i, (_, _, _, events) in enumerate(sched.steps):
+            for aname, ntasks in events:
+                ev = TaskEndEvent(array_name=aname, num_tasks=ntasks, function_start_tstamp=times[i],
+                                  function_end_tstamp=times[i + 1])
+                ev.task_result_tstamp = times[i + 1]
                 for cb in callbacks:
                     cb.on_task_end(ev)
 
@@ -917,9 +1007,69 @@ class GpuDagExecutor(DagExecutor):
                     total += -(-t.nchunks // self.world) * sum(t.slot_bytes(f) for f in t.fields)
         # uploaded host / in-memory sources are replicated on every rank
         total += sum(d.device_bytes() for d in self._uploads.values() if d.allocated)
+        self._resident_bytes = total
+        # scratch gathers and split temporaries of cached launches
+        total += self.owned_bytes()
         if total > HBM_BYTES_PER_GPU:
             raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")
+
+
+class _Schedule:
+    """One recorded execute_dag: per op, its launches, the targets it marks
+    written and the TaskEndEvents it emits."""
+
+    def __init__(self, steps):
+        from ...storage import alloc_epoch
+
+        self.steps = steps
+        self.epoch = alloc_epoch()
+
+
+class _Schedules:
+    """The recorded schedules of one (plan DAG, array names, resume) by the
+    written state of the plan's targets they start from.  A schedule is
+    replayed while the DAG is alive and no array was released or moved
+    since it was recorded (storage.alloc_epoch)."""
+
+    def __init__(self, dag, targets):
+        self.dag_ref = weakref.ref(dag)
+        self.targets = targets
+        self.by_state = {}
+
+    def lookup(self):
+        from ...storage import alloc_epoch
+
+        sched = self.by_state.get(tuple(t.written for t in self.targets))
+        if sched is not None and sched.epoch == alloc_epoch():
+            return sched
+        return None
+
+    def add(self, state, sched):
+        if len(self.by_state) > 16:
+            self.by_state.clear()
+        self.by_state[state] = sched
+
+
+def _nbytes(b) -> int:
+    if isinstance(b, DeviceArray):
+        return b.device_bytes() if b.allocated else 0
+    return b.numel() * b.element_size()
+
+
+def _drop_entry(ex_ref, attr, key):
+    """Finalizer: drop a cache entry whose key object was collected (unless
+    the slot was already reused by a live object)."""
+    ex = ex_ref()
+    if ex is None:
+        return
+    cache = getattr(ex, attr)
+    entry = cache.get(key)
+    if entry is None:
+        return
+    ref = entry.dag_ref if isinstance(entry, _Schedules) else entry[0]
+    if ref() is None:
+        cache.pop(key, None)
 
 
 def _drop_upload(ex_ref, key):

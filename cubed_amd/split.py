@@ -193,8 +193,8 @@ def split_launches(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys):
     for sub, dt in parts:
         name = f"split-{next(_temp_ids)}"
         T = DeviceArray(shape, dt, chunks, name=name)
+        ex.own(T)  # fits next to the plan? then it lives as long as the cached launches
         ex.allocate(T)
-        ex._scratch.append(T)  # lives as long as the executor's cached launches
         prev = list(temps)
 
         def bf_sub(out_key, _prev=prev, _inv={v: k for k, v in coords.items()}):

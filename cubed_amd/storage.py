@@ -106,6 +106,14 @@ def c_strides(extent: Sequence[int]) -> Tuple[int, ...]:
     return tuple(reversed(out))
 
 
+_ALLOC_EPOCH = [0]
+
+
+def alloc_epoch() -> int:
+    """Bumped whenever an allocated array's slabs are freed or replaced."""
+    return _ALLOC_EPOCH[0]
+
+
 class DeviceArray(ChunkGrid):
     """HBM-resident chunked array (replaces LazyZarrArray for intermediates).
 
@@ -173,6 +181,8 @@ class DeviceArray(ChunkGrid):
 
         if self.slabs and self.device == device and (self.rank, self.world) == (rank, world):
             return
+        if self.slabs:  # addresses change: recorded launch lists are stale
+            _ALLOC_EPOCH[0] += 1
         self.rank, self.world, self.device = rank, world, device
         self.slabs = {}
         for f in self.fields:
@@ -181,6 +191,10 @@ class DeviceArray(ChunkGrid):
         self.written = False
 
     def release(self):
+        """Free the slabs.  Launch lists the executor recorded against them
+        are invalidated (alloc_epoch)."""
+        if self.slabs:
+            _ALLOC_EPOCH[0] += 1
         self.slabs = {}
         self.written = False
 

@@ -30,9 +30,11 @@
  *                           map_direct region reads _copy_chunk
  *                           (core/ops.py:784-787) / _read_index_chunk
  *                           (core/ops.py:481-486).
- *   cubed_gemm_chunks    -> _matmul / _tensordot chunk products
- *                           cubed/array_api/linear_algebra_functions.py:62-64,
- *                           :139-149 (numpy BLAS sgemm/dgemm per task).
+ *   cubed_gemm_chain     -> _matmul / _tensordot chunk products together
+ *                           with the _sum_wo_cat k-sum
+ *                           cubed/array_api/linear_algebra_functions.py
+ *                           :35-78, :139-149 (numpy BLAS sgemm/dgemm per task
+ *                           + a reduction over k).
  */
 #ifndef CUBED_AMD_H
 #define CUBED_AMD_H
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 8
+#define CUBED_ABI_VERSION 9
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -319,21 +321,6 @@ int cubed_copy_boxes(const cubed_box_t* d_boxes, int64_t nboxes, int32_t ndim,
                      int32_t itemsize, int32_t path, int32_t lane_bytes,
                      int64_t work, int64_t row_bytes, void* stream);
 
-/* Batched chunk GEMM on MFMA: for each task t, C_t = A_t @ B_t (+ C_t when
- * accumulate) with row-major views (lda/ldb/ldc in elements).  dtype is
- * CUBED_F32 (f32-input MFMA, exact f32 products), CUBED_BF16 (bf16 inputs,
- * f32 accumulate/out) or CUBED_F64 (f64 vector FMA). */
-typedef struct {
-  int64_t a, b, c;        /* device byte addresses                          */
-  int64_t m, n, k;
-  int64_t lda, ldb, ldc;
-  int64_t accumulate;     /* 1: C += A@B, 0: C = A@B                         */
-} cubed_gemm_task_t;
-
-int cubed_gemm_chunks(const cubed_gemm_task_t* d_tasks, int64_t ntasks,
-                      int32_t dtype, int64_t max_m, int64_t max_n,
-                      void* stream);
-
 /* Chained chunk GEMMs (blockwise matmul / tensordot with the k-sum fused):
  * task t computes C_t (=|+=) sum over its segments s of A_s @ B_s, row-major
  * views, every A_s m x k_s, every B_s k_s x n, accumulated in one continuous
@@ -374,15 +361,6 @@ int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* 
                      int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
                      int32_t path, void* stream);
 
-/* library info */
-/* Plain chunk GEMMs through rocBLAS (cubed_amd/csrc/blas.hip): ``batch``
- * row-major products C_i (+)= A_i @ B_i of one shape, device arrays of
- * pointers; dtype CUBED_F32 or CUBED_F64.  Replaces the numpy BLAS call of
- * _matmul (linear_algebra_functions.py:62-64) like cubed_gemm_chunks. */
-int cubed_gemm_batched(int32_t dtype, const void* d_a_ptrs, const void* d_b_ptrs, const void* d_c_ptrs,
-                       int64_t batch, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb,
-                       int64_t ldc, int32_t accumulate, void* stream);
-
 /* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
  * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and
  * writes (storage/zarr.py:8-103 LazyZarrArray.create/open; the chunk I/O of
@@ -398,6 +376,7 @@ int64_t cubed_blosc_max_compressed(int64_t nbytes);
 int64_t cubed_blosc_compress(const void* src, int64_t nbytes, int typesize, int shuffle, void* dst,
                              int64_t dstcap);
 
+/* library info */
 int cubed_abi_version(void);
 const char* cubed_last_error(void);
 int cubed_device_count(void);

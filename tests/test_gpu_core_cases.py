@@ -194,7 +194,8 @@ def test_different_specs_fail(ex):
         cubed.compute(c1, c2)
 
 
-def test_default_spec_limits():
+def test_default_spec_limits(ex):
+    # the default spec's executor is the MI355X one: needs the GPU (ex skips without it)
     a = xp.ones((3, 3), chunks=(2, 2))
     assert np.array_equal(xp.negative(a).compute(), -np.ones((3, 3)))
     with pytest.raises(ValueError):

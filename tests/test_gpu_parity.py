@@ -168,7 +168,7 @@ def _fused_launches(e):
     return [l for lst in e._cache.values() for l in lst[1] if isinstance(l, L.FusedLaunch)]
 
 
-@pytest.mark.parametrize("w", ["1", "2", "4"])
+@pytest.mark.parametrize("w", [1, 2, 4])
 def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     """The streaming kernel with W kept groups per thread (forced by
     CUBED_AMD_STREAM_W; by default only grids that fill the CUs unsplit take
@@ -178,7 +178,7 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     fallback), both against the oracle."""
     from cubed_amd.runtime.executors.gpu import GpuDagExecutor
 
-    monkeypatch.setenv("CUBED_AMD_STREAM_W", w)
+    monkeypatch.setattr(L, "FORCE_STREAM_W", w)
     e = GpuDagExecutor("cuda:0")
     spec = mkspec(e)
     random.seed(4)
@@ -318,7 +318,7 @@ def test_rechunk_int_dtypes(ex):
     assert np.array_equal(b.compute(), x)
 
 
-@pytest.mark.parametrize("flat", ["1", "0"])
+@pytest.mark.parametrize("flat", [True, False])
 @pytest.mark.parametrize("dtype, shape, source, target", [
     (np.float64, (300, 4000), (30, 4000), (300, 250)),   # 2000-B rows: 16-B lanes
     (np.int32, (512, 1000), (64, 1000), (512, 250)),     # 1000-B rows: 8-B lanes
@@ -327,9 +327,9 @@ def test_rechunk_int_dtypes(ex):
 ])
 def test_rechunk_copy_paths_bit_exact(ex, monkeypatch, flat, dtype, shape, source, target):
     # packed-destination pieces take k_copy_flat (CUBED_COPY_FLAT) unless
-    # CUBED_AMD_COPY_FLAT=0 selects the per-row kernel; boxes span several
-    # workgroups so segment and row boundaries fall mid-wave
-    monkeypatch.setenv("CUBED_AMD_COPY_FLAT", flat)
+    # lowering.COPY_FLAT = False selects the per-row kernel; boxes span
+    # several workgroups so segment and row boundaries fall mid-wave
+    monkeypatch.setattr(L, "COPY_FLAT", flat)
     x = np.random.default_rng(5).integers(0, 2**31, size=shape).astype(dtype)
     spec = cubed.Spec(allowed_mem=10**9, executor=ex)
     b = cubed.from_array(x, chunks=source, spec=spec).rechunk(target)
@@ -380,16 +380,11 @@ def test_matmul_f32_tiles(ex, shape_a, shape_b, ca, cb):
     assert np.all(np.abs(got - exp) <= 1e-6 * scale + 1e-30)
 
 
-@pytest.mark.parametrize("path", ["blas", "native"])
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
-def test_matmul_blas_and_native_paths(ex, monkeypatch, path, dtype):
-    """f32/f64 chunk products through rocBLAS (default) and the hand-written
-    kernels (CUBED_AMD_GEMM=native), ragged chunks (several shapes per
-    launch), against an f64 product; bound = the f32 (or f64) rounding of a
-    length-K dot product plus the k-chunk sums."""
-    import cubed_amd.lowering as L
-
-    monkeypatch.setattr(L, "GEMM_PATH", path)
+def test_matmul_ragged_chunks(ex, dtype):
+    """f32/f64 chunk products on the hand-written kernels, ragged chunks
+    (several shapes per launch), against an f64 product; bound = the f32 (or
+    f64) rounding of a length-K dot product plus the k-chunk sums."""
     r = np.random.default_rng(21)
     x = (r.random((150, 130)) - 0.5).astype(dtype)
     y = (r.random((130, 170)) - 0.5).astype(dtype)

@@ -348,7 +348,9 @@ def test_copy_launch_picks_flat_path_for_packed_destinations(monkeypatch):
     # destination rows not packed (dst stride 400): per-row kernel
     strided = Box(1 << 20, 1 << 30, [30, 250], [4000, 1], [400, 1])
     assert CopyLaunch([strided], 8, "cpu").path == nat.COPY_ROWS
-    monkeypatch.setenv("CUBED_AMD_COPY_FLAT", "0")
+    import cubed_amd.lowering as Lw
+
+    monkeypatch.setattr(Lw, "COPY_FLAT", False)
     assert CopyLaunch([packed], 8, "cpu").path == nat.COPY_ROWS
 
 
@@ -475,8 +477,6 @@ def test_stream_groups_per_thread_choice(monkeypatch):
 
     from cubed_amd import lowering as Lw
 
-    monkeypatch.delenv("CUBED_AMD_STREAM_W", raising=False)
-
     def bits(vtype, nleaves, ntasks, max_kept):
         return Lw._stream_groups_mode(SimpleNamespace(vtype=vtype, nleaves=nleaves), ntasks, max_kept)
 
@@ -491,7 +491,7 @@ def test_stream_groups_per_thread_choice(monkeypatch):
     assert bits(Lw.V_F64, 4, 100, 720000) == 0
     # a 1-leaf f32 mean over a wide kept dim -> W = 2
     assert bits(Lw.V_F32, 1, 1, 4 << 20) == Lw.MODE_STREAM_W2
-    monkeypatch.setenv("CUBED_AMD_STREAM_W", "4")
+    monkeypatch.setattr(Lw, "FORCE_STREAM_W", 4)
     assert bits(Lw.V_F64, 1, 1, 20000) == Lw.MODE_STREAM_W4
 
 

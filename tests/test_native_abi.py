@@ -27,7 +27,7 @@ def header_functions():
 
 def test_header_declares_entry_points():
     fns = header_functions()
-    for f in ("cubed_fused_chunks", "cubed_copy_boxes", "cubed_random_chunks", "cubed_gemm_chunks"):
+    for f in ("cubed_fused_chunks", "cubed_copy_boxes", "cubed_random_chunks", "cubed_gemm_chain"):
         assert f in fns
 
 
@@ -64,13 +64,12 @@ LAYOUT_C = r"""
 #define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F))
 #define S(T) printf(#T " %zu\n", sizeof(T))
 int main(void) {
-  S(cubed_insn_t); S(cubed_program_t); S(cubed_task_t); S(cubed_box_t); S(cubed_gemm_task_t);
+  S(cubed_insn_t); S(cubed_program_t); S(cubed_task_t); S(cubed_box_t);
   P(cubed_program_t, insns); P(cubed_program_t, epi); P(cubed_program_t, consts);
   P(cubed_program_t, leaf_kind); P(cubed_program_t, out_dtype); P(cubed_program_t, ninsns);
   P(cubed_task_t, leaf_base); P(cubed_task_t, leaf_stride); P(cubed_task_t, out_base);
   P(cubed_task_t, out_stride); P(cubed_task_t, key_lo); P(cubed_task_t, block_offset);
   P(cubed_box_t, src_stride); P(cubed_box_t, dst_stride);
-  P(cubed_gemm_task_t, ldc); P(cubed_gemm_task_t, accumulate);
   S(cubed_gemm_chain_t); S(cubed_gemm_seg_t);
   P(cubed_gemm_chain_t, seg0); P(cubed_gemm_chain_t, ktot); P(cubed_gemm_chain_t, accumulate);
   P(cubed_gemm_seg_t, k); P(cubed_gemm_seg_t, ldb);
@@ -108,9 +107,6 @@ def test_struct_layouts_match_binding(c_layout):
     assert nat.BOX_DTYPE.itemsize == c_layout["cubed_box_t"]
     for f in ("src_stride", "dst_stride"):
         assert nat.BOX_DTYPE.fields[f][1] == c_layout[f"cubed_box_t.{f}"], f
-    assert nat.GEMM_DTYPE.itemsize == c_layout["cubed_gemm_task_t"]
-    for f in ("ldc", "accumulate"):
-        assert nat.GEMM_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_task_t.{f}"], f
     assert nat.CHAIN_DTYPE.itemsize == c_layout["cubed_gemm_chain_t"]
     for f in ("seg0", "ktot", "accumulate"):
         assert nat.CHAIN_DTYPE.fields[f][1] == c_layout[f"cubed_gemm_chain_t.{f}"], f
@@ -161,3 +157,24 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(nat, "_lib", None)
     with pytest.raises(nat.NativeError):
         nat.lib()
+
+
+def test_product_library_has_no_vendor_blas(built):
+    """One GEMM path: the product library links no rocBLAS / hipBLASLt and
+    exports no library-comparator entry points."""
+    from cubed_amd import _native as nat
+
+    out = subprocess.run(["ldd", nat.LIB_PATH], capture_output=True, text=True).stdout
+    assert "rocblas" not in out and "hipblas" not in out
+    lib = ctypes.CDLL(nat.LIB_PATH)
+    for f in ("cubed_gemm_batched", "cubed_gemm_chunks"):
+        assert not hasattr(lib, f)
+
+
+def test_no_environment_switches_in_kernels():
+    """The C library's launch paths read no environment variables (no A/B
+    switch can silently change the kernel that runs)."""
+    csrc = os.path.join(ROOT, "cubed_amd", "csrc")
+    for name in os.listdir(csrc):
+        if name.endswith((".hip", ".h", ".cpp")):
+            assert "getenv" not in open(os.path.join(csrc, name)).read(), name

@@ -1,0 +1,161 @@
+"""The executor's recorded launch schedules and buffer lifetimes (CPU, dry
+lowering: the exact launch objects the GPU path would run, none executed).
+
+* A repeated ``Plan.execute`` with the same plan, array names, resume flag
+  and written state replays the recorded launch list instead of re-walking
+  the DAG (runtime/executors/python.py:17-32 is the loop this replaces);
+  a different written state re-walks it.
+* Scratch gathers and split temporaries belong to the cache entry of the
+  launches that use them: dropping the plan frees them.
+* TaskEndEvents carry per-op start/end times and the reference's counts.
+"""
+
+import gc
+import random
+
+import numpy as np
+
+import cubed_amd as cubed
+import cubed_amd.array_api as xp
+import cubed_amd.random as crandom
+from cubed_amd.core.plan import arrays_to_plan
+from cubed_amd.storage import DeviceArray
+
+
+def _reset(plan, keep):
+    kept = {id(a.zarray) for a in keep}
+    for _, d in plan._finalize_dag().nodes(data=True):
+        t = d.get("target")
+        if isinstance(t, DeviceArray) and id(t) not in kept:
+            t.written = False
+
+
+def test_repeat_execute_replays_the_recorded_launches(built, dry):
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(7)
+    u = xp.astype(crandom.random((40, 30, 20), chunks=(10, 30, 20), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((40, 30, 20), chunks=(10, 30, 20), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=dry, array_names=[u.name, v.name])
+    m = xp.mean(u * v, axis=0)
+    plan = arrays_to_plan(m)
+    runs = []
+    for _ in range(3):
+        _reset(plan, (u, v))
+        dry.launched.clear()
+        before = dry.replays
+        plan.execute(executor=dry, resume=True, array_names=[m.name])
+        runs.append((dry.replays - before, [id(l) for l in dry.launched]))
+    assert runs[0][0] == 0 and runs[1][0] == 1 and runs[2][0] == 1
+    assert runs[0][1] == runs[1][1] == runs[2][1] and runs[0][1]
+    # the inputs were not regenerated (resume): only the mean's launch ran
+    assert len(runs[0][1]) == 1
+
+
+def test_changed_written_state_rewalks_the_dag(built, dry):
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(8)
+    a = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    m = xp.mean((a + 1) * 2, axis=0)
+    plan = arrays_to_plan(m)
+    dry.launched.clear()
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    assert dry.launched
+    # everything is written now: resume skips every op (a new state, so the
+    # DAG is walked again and the empty schedule recorded)
+    dry.launched.clear()
+    before = dry.replays
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    assert dry.replays == before and not dry.launched
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    assert dry.replays == before + 1 and not dry.launched
+    # back to the first state: its recorded schedule replays
+    _reset(plan, ())
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    assert dry.replays == before + 2 and dry.launched
+
+
+def test_released_array_invalidates_the_schedule(built, dry):
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(9)
+    a = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    m = xp.sum(a, axis=0)
+    plan = arrays_to_plan(m)
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    _reset(plan, (a,))
+    m.zarray.release()
+    before = dry.replays
+    plan.execute(executor=dry, resume=True, array_names=[m.name])
+    assert dry.replays == before
+
+
+def test_split_temporaries_are_freed_with_their_plan(built, dry):
+    """split temporaries lived as long as the executor.  They
+    now belong to the cached launches of their pipeline."""
+    from cubed_amd.core.optimization import fuse_all_optimize_dag
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    gc.collect()
+    base = dry.owned_bytes()
+    for seed in range(3):
+        random.seed(seed)
+        u = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+        v = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+        m = xp.mean(u * v, axis=0)
+        arrays_to_plan(m).execute(executor=dry, array_names=[m.name],
+                                  optimize_function=fuse_all_optimize_dag)
+        # one materialised random stream: 50 x 98 x 192 f64
+        assert dry.owned_bytes() - base >= 50 * 98 * 192 * 8
+        del u, v, m
+        gc.collect()
+        assert dry.owned_bytes() == base
+    assert not [k for k in dry._cache if dry._cache[k][0]() is None]
+
+
+def test_split_temporary_checked_against_hbm(built, dry, monkeypatch):
+    import pytest
+
+    import cubed_amd.runtime.executors.gpu as g
+    from cubed_amd.core.optimization import fuse_all_optimize_dag
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(3)
+    u = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+    v = crandom.random((50, 1, 98, 192), chunks=(10, 1, -1, -1), spec=spec)
+    m = xp.mean(u * v, axis=0)
+    monkeypatch.setattr(g, "HBM_BYTES_PER_GPU", 50 * 98 * 192 * 8)
+    with pytest.raises(MemoryError, match="split temporary"):
+        arrays_to_plan(m).execute(executor=dry, array_names=[m.name],
+                                  optimize_function=fuse_all_optimize_dag)
+
+
+def test_task_end_events_per_op_with_times(built, dry):
+    from cubed_amd.runtime.types import Callback
+
+    class Rec(Callback):
+        def __init__(self):
+            self.events = []
+
+        def on_task_end(self, event):
+            self.events.append(event)
+
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(10)
+    a = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    m = xp.mean(a, axis=0)
+    plan = arrays_to_plan(m)
+    for _ in range(2):  # recorded, then replayed: same events
+        rec = Rec()
+        _reset(plan, ())
+        plan.execute(executor=dry, callbacks=[rec], resume=True, array_names=[m.name])
+        names = [e.array_name for e in rec.events]
+        assert len(names) == len(set(names))
+        assert all(e.function_end_tstamp >= e.function_start_tstamp for e in rec.events)
+        ends = [e.function_end_tstamp for e in rec.events]
+        assert ends == sorted(ends)
+        tasks = {e.array_name: e.num_tasks for e in rec.events}
+        dag = plan._finalize_dag()
+        for name, d in dag.nodes(data=True):
+            if name in tasks and "primitive_op" in d:
+                assert tasks[name] == d["primitive_op"].num_tasks
+    assert np.isfinite(ends[-1])
