@@ -132,6 +132,64 @@ def elide_rechunks(dag, array_names):
     return dag, elided
 
 
+def compose_rechunks(dag, array_names):
+    """A two-op rechunk (source -> ``{name}-int`` -> target, primitive/
+    rechunk.py:144-155, planned when the source and target chunks do not fit
+    ``max_mem`` together) whose intermediate is read only by the second copy
+    and is not requested becomes ONE copy from the source straight into the
+    target chunks: every target chunk is assembled from the source chunk
+    pieces it covers (the intermediate's chunk grid only bounded the
+    reference's per-task memory, which HBM-resident boxes do not need).
+    Values are bit-identical; the first op keeps its TaskEndEvent and task
+    count (``fused_from``).  Returns (DAG copy, elided targets)."""
+    import networkx as nx
+
+    from .core.optimization import predecessors
+
+    requested = set(array_names or ())
+    todo = []
+    for name, nd in dag.nodes(data=True):
+        if "pipeline" not in nd or nd["pipeline"].function is not copy_read_to_write:
+            continue
+        srcs = [p for p in predecessors(dag, name) if p != "arrays"]
+        if len(srcs) != 1:
+            continue
+        mid = srcs[0]
+        if mid in requested or dag.out_degree(mid) != 1:
+            continue
+        pres = [p for p in predecessors(dag, mid)]
+        if len(pres) != 1:
+            continue
+        op1 = pres[0]
+        od = dag.nodes[op1]
+        if "pipeline" not in od or od["pipeline"].function is not copy_read_to_write:
+            continue
+        x = [p for p in predecessors(dag, op1) if p != "arrays"]
+        if len(x) != 1:
+            continue
+        todo.append((op1, mid, name, x[0]))
+    if not todo:
+        return dag, []
+    dag = nx.MultiDiGraph(dag)  # an unfrozen copy
+    elided = []
+    for op1, mid, op2, x in todo:
+        d1, d2 = dag.nodes[op1], dag.nodes[op2]
+        read = d1["pipeline"].config.read
+        spec = dataclasses.replace(d2["pipeline"].config, read=read)
+        pipeline = dataclasses.replace(d2["pipeline"], config=spec)
+        d2["pipeline"] = pipeline
+        d2["primitive_op"] = dataclasses.replace(d2["primitive_op"], pipeline=pipeline)
+        d2["fused_from"] = list(d1.get("fused_from", ())) + [(op1, d1["primitive_op"].num_tasks)] + \
+            list(d2.get("fused_from", ()))
+        t = dag.nodes[mid].get("target")
+        if isinstance(t, DeviceArray):
+            elided.append(t)
+        dag.remove_node(op1)
+        dag.remove_node(mid)
+        dag.add_edge(x, op2)
+    return dag, elided
+
+
 def split_complex(dag):
     """Every blockwise program that computes complex values rewritten into
     real expressions over the values' real / imaginary slabs

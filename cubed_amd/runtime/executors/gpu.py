@@ -848,11 +848,12 @@ class GpuDagExecutor(DagExecutor):
         if entry is not None and entry[0]() is dag:
             return entry[1]
         from ...chains import fuse_elementwise_producers
-        from ...rewrites import elide_rechunks, split_complex
+        from ...rewrites import compose_rechunks, elide_rechunks, split_complex
 
-        new, absorbed = split_complex(dag), []
+        new, absorbed = compose_rechunks(split_complex(dag), array_names)
         if self.elide_rechunks:
-            new, absorbed = elide_rechunks(new, array_names)
+            new, more = elide_rechunks(new, array_names)
+            absorbed += more
         if self.fuse_producers:
             new, more = fuse_elementwise_producers(new, array_names)
             absorbed += more

@@ -82,6 +82,60 @@ def test_rechunk_lowers_to_one_copy_launch(built, dry):
     assert sum(int(np.prod(b.extent)) for b in boxes) == 64 * 48
 
 
+def test_two_op_rechunk_is_one_direct_copy(built, dry):
+    """The reference plans rows -> columns under a small allowed_mem as two
+    copy ops through an intermediate (primitive/rechunk.py:144-155; config
+    3's 2 GB plan: 625 + 25 tasks).  The executor composes them into ONE
+    copy from the source into the target chunks (rewrites.compose_rechunks):
+    the intermediate is never allocated, every target element is written
+    once, and both ops still report their TaskEndEvents and task counts."""
+    from cubed_amd.runtime.types import Callback
+
+    class Count(Callback):
+        def __init__(self):
+            self.tasks = {}
+
+        def on_task_end(self, e):
+            self.tasks[e.array_name] = e.num_tasks
+
+    spec = cubed.Spec(allowed_mem=1_200_000, reserved_mem=0, executor=dry)
+    x = cubed.from_array(np.arange(500 * 600, dtype=np.float32).reshape(500, 600), chunks=(10, 600),
+                         spec=spec)
+    arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
+    y = x.rechunk((500, 10))
+    plan = arrays_to_plan(y)
+    ops = {n: d["primitive_op"].num_tasks for n, d in plan._finalize_dag().nodes(data=True)
+           if d.get("op_name") == "rechunk"}
+    assert len(ops) == 2  # the reference's two-stage plan
+    dry.launched.clear()
+    cb = Count()
+    plan.execute(executor=dry, resume=True, array_names=[y.name], callbacks=[cb])
+    copies = [l for l in dry.launched if isinstance(l, CopyLaunch)]
+    assert len(copies) == 1
+    boxes = copies[0].boxes
+    assert sum(int(np.prod(b.extent)) for b in boxes) == 500 * 600
+    # boxes read the SOURCE chunks: no box crosses a 10-row source band
+    assert all(b.extent[0] <= 10 for b in boxes)
+    for n, t in ops.items():
+        assert cb.tasks[n] == t
+    ints = [d["target"] for _, d in plan._finalize_dag().nodes(data=True)
+            if str(d.get("name", "")).endswith("-int")]
+    assert ints and all(not t.allocated for t in ints)
+
+
+def test_requested_intermediate_keeps_both_copies(built, dry):
+    spec = cubed.Spec(allowed_mem=1_200_000, reserved_mem=0, executor=dry)
+    x = cubed.from_array(np.arange(500 * 600, dtype=np.float32).reshape(500, 600), chunks=(10, 600),
+                         spec=spec)
+    arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
+    y = x.rechunk((500, 10))
+    dag = arrays_to_plan(y)._finalize_dag()
+    mid = [n for n in dag.nodes if str(n).endswith("-int")][0]
+    dry.launched.clear()
+    arrays_to_plan(y).execute(executor=dry, resume=True, array_names=[y.name, mid])
+    assert len([l for l in dry.launched if isinstance(l, CopyLaunch)]) == 2
+
+
 def test_task_table_rows_match_tasks(built, dry):
     spec = cubed.Spec(allowed_mem=10**8, executor=dry)
     a = cubed.from_array(np.ones((30, 40)), chunks=(7, 9), spec=spec)
