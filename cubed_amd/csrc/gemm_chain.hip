@@ -32,8 +32,10 @@
 //                      clamped (results discarded), k past the chain's end
 //                      reads a zero page.
 //   k_gemm_f32_chain   f32 on v_mfma_f32_32x32x2_f32 (exact f32 products, f32
-//                      accumulate): 128 x 128 tile, K staged 32 deep through
-//                      registers (float4) into k-major LDS.
+//                      accumulate): the bf16 kernel's 256 x 256 tile and
+//                      global_load_lds ring, K 16 deep per step, ds_read_b128
+//                      fragments for both operands (k and column
+//                      permutations, see the kernel).
 //   k_gemm_any_chain   any dtype (f64 / int64 / ragged bf16 or f32 shapes):
 //                      64 x 64 tiles of scalar FMAs, every element bounds-
 //                      checked.  Correctness path, not a fast path.
@@ -368,163 +370,192 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 }
 
 // ------------------------------------------------------------------ f32 MFMA
-// 128x128 tile per 256-thread workgroup: 2x2 waves, each a 64x64 sub-tile of
-// 2x2 v_mfma_f32_32x32x2_f32 accumulators; K staged 32 deep through
-// registers (float4) into k-major LDS; next tile's loads in flight during the
-// current tile's MFMAs.  Segments as in the bf16 kernel (k % 4 == 0 per
-// segment, so a float4 never straddles two).
-constexpr int HF_BM = 128, HF_BN = 128, HF_BK = 32;
+// v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate): lane l gives
+// A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31].  256x256 output tile per
+// 512-thread workgroup (8 waves, 4 (M) x 2 (N), each 64 x 128 = 2 x 4
+// accumulators of 32x32), K staged 16 deep straight from HBM into LDS by
+// global_load_lds (16 B per lane) through a 4-slot ring (three steps in
+// flight), counted vmcnt + raw s_barrier, one barrier per step -- the bf16
+// kernel's pipeline.  Both operands are read with ds_read_b128 by two
+// permutations that change no value:
+//  * K: a lane's 16-B A read holds 4 consecutive k of its row; in an 8-deep
+//    k group g the MFMA of step j (0..3) pairs k = 8g+j (lanes 0-31) with
+//    k = 8g+4+j (lanes 32-63), and B supplies the same k rows;
+//  * N: a lane's 16-B B read holds 4 consecutive columns of one k row, one
+//    per accumulator q: accumulator q covers columns wn + 4j + q (j = lane
+//    column), so the epilogue stores the 4 accumulators of a row as one
+//    float4.
+// Each output element is one f32 fma chain over its K (the per-element
+// order is (segment, k group, j, half), every product exact).
+// LDS slot: A [256 rows][16 k] (64-B rows, 16-B chunk c of row r at
+// position c ^ ((r >> 2) & 3): conflict-free b128 reads) + B [16 k][256 n]
+// (1 KiB rows, as in HBM).
+constexpr int HF_BM = 256, HF_BN = 256, HF_BK = 16, HF_NS = 4;
+constexpr int HF_A = HF_BM * HF_BK * 4;  // 16 KiB
+constexpr int HF_B = HF_BK * HF_BN * 4;  // 16 KiB
+constexpr int HF_STAGE = HF_A + HF_B;
 
-struct F4 { float x, y, z, w; };
-
-// DB: two LDS slots -- the next tile's registers are stored into the other
-// slot right after this tile's MFMAs, one barrier per K step instead of two
-template <int LDA_S, int LDB_S, bool DB = false, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
+__global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
-                                                        int64_t tiles_m, int64_t tiles_n) {
-  __shared__ float As_[DB ? 2 : 1][HF_BK][LDA_S];
-  __shared__ float Bs_[DB ? 2 : 1][HF_BK][LDB_S];
+                                                        int64_t tiles_m, int64_t tiles_n,
+                                                        const char* __restrict__ zero) {
+  __shared__ __attribute__((aligned(1024))) char lds_[HF_NS * HF_STAGE];
+  CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
-  tile_of<HF_BM, HF_BN, 8>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  tile_of<HF_BM, HF_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
   const int64_t M = T->m, N = T->n, KT = T->ktot;
   if (m0 >= M || n0 >= N) return;
   const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
-  int64_t s = seg0, ks = 0, ke = segs[seg0].k;
-  const float* a_cur = (const float*)(uintptr_t)segs[s].a;
-  const float* b_cur = (const float*)(uintptr_t)segs[s].b;
-  int64_t lda = segs[s].lda, ldb = segs[s].ldb;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 128;
 
-  // 2x2 accumulators of 32x32 per wave (a 16x16x4 form with 4x4 accumulators
-  // measured 109.6 vs 112.0 TF on config 5: not used)
-  f32x16 acc[2][2];
+  // ---- staging geometry (constant over the K loop)
+  // A: wave w instruction i stages rows 16*(2w+i) + lane>>2; LDS position
+  // lane&3 of the row holds global chunk (lane&3) ^ ((lane>>4)&3)
+  int64_t gmA[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  for (int i = 0; i < 2; ++i) {
+    const int64_t r = 16 * (2 * w + i) + (lane >> 2);
+    gmA[i] = (m0 + r < M ? m0 + r : M - 1);
+  }
+  const int kA = 4 * ((lane & 3) ^ ((lane >> 4) & 3));  // k offset of this lane's chunk
+  // B: wave w instruction i stages k-row 2w+i, columns n0 + 4*lane .. +3
+  const int rB0 = 2 * w;
+  const int64_t gnB = (n0 + 4 * lane + 4 <= N ? n0 + 4 * lane : N - 4);
 
-  F4 ra[4], rb[4];
-  auto load = [&](int64_t k0) {
-    const bool inside = k0 + HF_BK <= ke;
-    const float* a_n = nullptr;
-    const float* b_n = nullptr;
-    int64_t lda_n = 0, ldb_n = 0;
-    if (!inside && s + 1 < segN) {
-      a_n = (const float*)(uintptr_t)segs[s + 1].a;
-      b_n = (const float*)(uintptr_t)segs[s + 1].b;
-      lda_n = segs[s + 1].lda;
-      ldb_n = segs[s + 1].ldb;
+  int64_t s = seg0, ks = 0;
+  const char* a_cur = (const char*)(uintptr_t)segs[s].a;
+  const char* b_cur = (const char*)(uintptr_t)segs[s].b;
+  int64_t lda4 = segs[s].lda * 4, ldb4 = segs[s].ldb * 4;
+  int64_t ke = segs[s].k;
+
+  auto stage = [&](int64_t k0, CUBED_L char* buf) {
+    const char* sa[2];
+    const char* sb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      sa[i] = a_cur + gmA[i] * lda4 + (k0 - ks + kA) * 4;
+      sb[i] = b_cur + (k0 - ks + rB0 + i) * ldb4 + gnB * 4;
+    }
+    if (k0 + HF_BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
+      const bool has_next = s + 1 < segN;
+      const int64_t sn = has_next ? s + 1 : s;
+      const char* na = (const char*)(uintptr_t)segs[sn].a;
+      const char* nb = (const char*)(uintptr_t)segs[sn].b;
+      const int64_t nlda4 = segs[sn].lda * 4, nldb4 = segs[sn].ldb * 4;
+      const int64_t ka = k0 + kA;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const char* pa = na + gmA[i] * nlda4 + (ka - ke) * 4;
+        sa[i] = ka < ke ? sa[i] : ((has_next && ka < KT) ? pa : zero);
+        const int64_t kb = k0 + rB0 + i;
+        const char* pb = nb + (kb - ke) * nldb4 + gnB * 4;
+        sb[i] = kb < ke ? sb[i] : ((has_next && kb < KT) ? pb : zero);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 256 * i;
-      // A tile: 128 rows x 8 float4 along k
-      const int row = f >> 3, kq = (f & 7) * 4;
-      const int64_t gm = m0 + row, kk = k0 + kq;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (gm < M && kk < KT) {
-        const float* p = (inside || kk < ke) ? a_cur + gm * lda + (kk - ks) : a_n + gm * lda_n + (kk - ke);
-        v = *(const CUBED_G f32x4*)(uintptr_t)p;
-      }
-      ra[i] = F4{v.x, v.y, v.z, v.w};
-      // B tile: 32 k-rows x 32 float4 along n
-      const int kr = f >> 5, nq = (f & 31) * 4;
-      const int64_t kk2 = k0 + kr, gn = n0 + nq;
-      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (kk2 < KT && gn < N) {
-        const float* p = (inside || kk2 < ke) ? b_cur + (kk2 - ks) * ldb + gn : b_n + (kk2 - ke) * ldb_n + gn;
-        u = *(const CUBED_G f32x4*)(uintptr_t)p;
-      }
-      rb[i] = F4{u.x, u.y, u.z, u.w};
-    }
-  };
-  auto advance = [&](int64_t k0next) {
-    if (k0next >= ke && s + 1 < segN) {
+    for (int i = 0; i < 2; ++i) glds16(sa[i], buf + (2 * w + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(sb[i], buf + HF_A + (rB0 + i) * 1024);
+    if (k0 + HF_BK >= ke && s + 1 < segN) {  // the next step starts in the next segment
       ks = ke;
       ++s;
-      a_cur = (const float*)(uintptr_t)segs[s].a;
-      b_cur = (const float*)(uintptr_t)segs[s].b;
-      lda = segs[s].lda;
-      ldb = segs[s].ldb;
+      a_cur = (const char*)(uintptr_t)segs[s].a;
+      b_cur = (const char*)(uintptr_t)segs[s].b;
+      lda4 = segs[s].lda * 4;
+      ldb4 = segs[s].ldb * 4;
       ke = ks + segs[s].k;
     }
   };
-  auto store = [&](int slot) {
-    float (*As)[LDA_S] = As_[slot];
-    float (*Bs)[LDB_S] = Bs_[slot];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int f = tid + 256 * i;
-      const int row = f >> 3, kq = (f & 7) * 4;
-      As[kq + 0][row] = ra[i].x;
-      As[kq + 1][row] = ra[i].y;
-      As[kq + 2][row] = ra[i].z;
-      As[kq + 3][row] = ra[i].w;
-      const int kr = f >> 5, nq = (f & 31) * 4;
-      f32x4 v;
-      v.x = rb[i].x; v.y = rb[i].y; v.z = rb[i].z; v.w = rb[i].w;
-      *(f32x4*)&Bs[kr][nq] = v;
-    }
-  };
 
-  load(0);
-  advance(HF_BK);
-  store(0);
-  __syncthreads();
-  const int hi = lane >> 5, lo = lane & 31;
-  int cur = 0;
-  for (int64_t k0 = 0; k0 < KT; k0 += HF_BK) {
-    const bool more = k0 + HF_BK < KT;
-    if (more) {
-      load(k0 + HF_BK);  // in flight during this tile's MFMAs
-      advance(k0 + 2 * HF_BK);
-    }
-    const float (*As)[LDA_S] = As_[cur];
-    const float (*Bs)[LDB_S] = Bs_[cur];
-#pragma unroll 4
-    for (int kk = 0; kk < HF_BK; kk += 2) {
-      const float a0 = As[kk + hi][wm + lo], a1 = As[kk + hi][wm + 32 + lo];
-      const float b0 = Bs[kk + hi][wn + lo], b1 = Bs[kk + hi][wn + 32 + lo];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if constexpr (DB) {
-      // the other slot was last read in the previous step, before its barrier
-      if (more) store(cur ^ 1);
-      __syncthreads();
-      cur ^= 1;
-    } else {
-      __syncthreads();
-      if (more) {
-        store(0);
-        __syncthreads();
-      }
-    }
-  }
-  CUBED_G float* __restrict__ C = (CUBED_G float*)(uintptr_t)T->c;
-  const bool accum = T->accumulate != 0;
-  // C/D map of a 32x32 accumulator: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  // ---- fragment read offsets (within a slot)
+  const int h = lane >> 5, r32 = lane & 31;
+  // A, row block rb, k group g: row wm + 32 rb + r32, logical chunk 2g + h
+  int offA[2][2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      offA[rb][g] = (wm + 32 * rb + r32) * 64 + 16 * ((2 * g + h) ^ ((r32 >> 2) & 3));
+  // B, k group g, step j: k-row 8g + 4h + j, columns wn + 4 r32 .. +3
+  const int offB = HF_A + 4 * h * 1024 + (wn + 4 * r32) * 4;
+
+  f32x16 acc[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][q][r] = 0.f;
+
+  const int64_t nst = (KT + HF_BK - 1) / HF_BK;
+  constexpr int D = HF_NS - 1;  // steps staged ahead
+  for (int64_t p = 0; p < D && p < nst; ++p) stage(p * HF_BK, lds + p * HF_STAGE);
+  // retire this wave's loads of step q (4 per step; steps up to q + D - 1 issued)
+  auto wait_step = [&](int64_t q) {
+    int64_t younger = nst - 1 - q;
+    if (younger > D - 1) younger = D - 1;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  int rd = 0, wr_slot = D;
+  for (int64_t p = 0; p < nst; ++p) {
+    // this wave's step p landed; then every wave's (barrier), and every wave
+    // finished reading step p-1's slot (restaged below)
+    wait_step(p);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (p + D < nst) stage((p + D) * HF_BK, lds + wr_slot * HF_STAGE);
+    const CUBED_L char* bufc = lds + rd * HF_STAGE;
+    rd = rd + 1 == HF_NS ? 0 : rd + 1;
+    wr_slot = wr_slot + 1 == HF_NS ? 0 : wr_slot + 1;
+    // all 12 fragment reads of the step first (group 0's A and B, then group
+    // 1's): group 1's land while group 0's 32 MFMAs run
+    f32x4 af[2][2], bq[2][4];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) af[g][rb] = *(const CUBED_L f32x4*)(bufc + offA[rb][g]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bq[g][j] = *(const CUBED_L f32x4*)(bufc + offB + (8 * g + j) * 1024);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (counted lgkmcnt waits follow)
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc[rb][q] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g][rb][j], bq[g][j][q], acc[rb][q], 0, 0, 0);
+  }
+
+  // ---- epilogue: accumulator (rb, q) register r = row wm + 32 rb + (r&3) +
+  // 8 (r>>2) + 4h, column wn + 4 r32 + q: one float4 per (rb, r)
+  char* C = (char*)(uintptr_t)T->c;
+  const int64_t ldc = T->ldc;
+  const bool accum = T->accumulate != 0;
+  const int64_t gn = n0 + wn + 4 * r32;
+  if (gn < N) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * hi;
-        const int64_t gm = m0 + wm + 32 * i + row, gn = n0 + wn + 32 * j + lo;
-        if (gm < M && gn < N) {
-          CUBED_G float* c = C + gm * T->ldc + gn;
-          *c = accum ? (*c + acc[i][j][r]) : acc[i][j][r];
+        const int64_t gm = m0 + wm + 32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < M) {
+          CUBED_G f32x4* c = (CUBED_G f32x4*)(uintptr_t)(C + (gm * ldc + gn) * 4);
+          f32x4 v = {acc[rb][0][r], acc[rb][1][r], acc[rb][2][r], acc[rb][3][r]};
+          if (accum) v += *c;
+          *c = v;
         }
       }
+  }
 }
 
 // ------------------------------------------------------------------ any dtype
@@ -679,13 +710,12 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     else
       hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
   } else if (path == CUBED_GEMM_MFMA && in_dtype == CUBED_F32) {
+    if (!d_zero) return fail("the f32 path needs a zero page");
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
     const int64_t blocks = ntasks * tm * tn;
     if (blocks > 0x7fffffff) return fail("grid too large");
-    // single LDS slot: the double-buffered form (one barrier per step, 75 KB
-    // of LDS: 2 instead of 3 waves per SIMD) measured 101 vs 111 TF on config 5
-    hipLaunchKernelGGL((k_gemm_f32_chain<HF_BM + 4, HF_BN + 32>), dim3((unsigned)blocks), dim3(256), 0, st,
-                       d_tasks, d_segs, tm, tn);
+    hipLaunchKernelGGL(k_gemm_f32_chain, dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm, tn,
+                       (const char*)d_zero);
   } else {
     const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
     const int64_t blocks = ntasks * tm * tn;

@@ -5,10 +5,15 @@ through shared Zarr storage (cubed/core/plan.py:44-48).  On one
 MI355X node the executor runs one process per GPU and moves chunks over
 xGMI with RCCL (torch.distributed's "nccl" backend is RCCL on ROCm):
 
-* ``all_to_all`` -- the chunk exchange of rechunk and of any pipeline whose
-  tasks read chunks owned by another rank (one ``all_to_all_single`` of a
-  packed byte buffer, issued on torch's current stream, so it is ordered
-  with the pack/unpack kernels around it);
+* ``exchange`` -- the piece transfers of a rechunk: grouped point-to-point
+  sends / receives (``batch_isend_irecv``, one RCCL group), so pieces land
+  straight in their target chunk slots; started on torch's current stream
+  and waited for by it (``Pending.wait``), so kernels queued in between
+  (the next slice's pack, the local pieces) overlap the transfers;
+* ``all_to_all`` -- whole-chunk fetches of pipelines whose tasks read chunks
+  owned by another rank (one ``all_to_all_single`` of a packed byte buffer,
+  issued on torch's current stream, so it is ordered with the pack kernel
+  before it);
 * ``reduce`` / ``all_reduce`` -- the final combine round of a reduction
   (SUM of f64 totals / i64 counts);
 * ``all_gather`` -- partials whose combine RCCL cannot express with numpy's
@@ -65,6 +70,26 @@ class Comm:
         self.dist.all_to_all_single(r, s, rs, ss, group=self.group)
         self._unstage(r, recv, staged)
 
+    def exchange(self, sends, recvs) -> "Pending":
+        """Start grouped point-to-point transfers: ``sends`` / ``recvs`` are
+        (byte tensor, peer rank) lists; per peer, both ends list their
+        transfers in the same order.  Returns a handle whose ``wait()``
+        orders the current stream (RCCL) or the host (gloo) after them."""
+        dist = self.dist
+        ops, fixups = [], []
+        for t, peer in sends:
+            h, _ = self._stage(t)
+            ops.append(dist.P2POp(dist.isend, h, self._global(peer), group=self.group))
+        for t, peer in recvs:
+            if self.staged and t.device.type != "cpu":
+                h = t.new_empty(t.shape, device="cpu")
+                fixups.append((h, t))
+            else:
+                h = t
+            ops.append(dist.P2POp(dist.irecv, h, self._global(peer), group=self.group))
+        works = dist.batch_isend_irecv(ops) if ops else []
+        return Pending(works, fixups)
+
     def all_reduce_sum(self, t):
         h, staged = self._stage(t)
         self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
@@ -104,6 +129,20 @@ class Comm:
         if self.group is None:
             return r
         return self.dist.get_global_rank(self.group, r)
+
+
+class Pending:
+    """Transfers started by ``Comm.exchange``."""
+
+    def __init__(self, works, fixups):
+        self.works, self.fixups = works, fixups
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        for host, dev in self.fixups:
+            dev.copy_(host)
+        self.works, self.fixups = [], []
 
 
 def default_comm() -> Optional[Comm]:

@@ -8,10 +8,14 @@ which bytes every other rank sends and receives.  Two plans:
 * ``RechunkExchange`` -- ``copy_read_to_write`` (cubed/primitive/rechunk.py
   :187-192) over a whole target array: each target chunk is assembled from
   pieces of source chunks; pieces whose source and target chunks share an
-  owner are copied locally, the rest go through one all-to-all.  Pieces are
-  enumerated in (target chunk, source chunk) C order on every rank, so the
-  packed send layout of rank s for rank d equals the receive layout rank d
-  expects from s.
+  owner are copied locally, the rest move as point-to-point transfers (one
+  send / receive pair per piece, grouped).  A piece whose box is contiguous
+  in its TARGET chunk (e.g. a row band of a column chunk: config 3's
+  (1000 rows x 1000 cols) pieces of a (50000, 1000) target) is received
+  straight into the chunk's slot -- no unpack pass; one contiguous in its
+  SOURCE chunk is sent from the slot -- no pack pass.  Pieces are
+  enumerated in (target chunk, source chunk) C order on every rank, so both
+  ends of every peer pair post their transfers in the same order.
 * ``FetchExchange`` -- whole chunks a pipeline's tasks read but do not own
   (inputs on a different chunk grid, merge regions spanning ranks, matmul
   operand panels).  Each needed (array, chunk, field) is fetched once per
@@ -83,29 +87,66 @@ def rechunk_pieces(src_grid, dst_grid) -> List[Piece]:
     return out
 
 
+def box_contiguous(chunk_extent, start, extent) -> bool:
+    """Whether a box of a C-order chunk is one contiguous byte run: every dim
+    after the first one the box spans (> 1) is taken whole."""
+    nd = len(extent)
+    k = next((d for d in range(nd) if extent[d] > 1), nd - 1)
+    return all(start[d] == 0 and extent[d] == chunk_extent[d] for d in range(k + 1, nd))
+
+
+def box_offset(chunk_extent, start) -> int:
+    """Element offset of a box's first element inside its C-order chunk."""
+    st, o = 1, 0
+    for d in range(len(chunk_extent) - 1, -1, -1):
+        o += start[d] * st
+        st *= chunk_extent[d]
+    return o
+
+
+@dataclass(frozen=True)
+class Xfer:
+    """One point-to-point transfer of a rechunk piece.  ``direct``: the
+    bytes go straight from the source slot (send) or into the target slot
+    (receive); otherwise through the pack (send) or staging (receive)
+    buffer at byte ``offset``.  ``index``: the piece's position in the
+    global piece order (slices of the exchange are index ranges)."""
+    piece: Piece
+    index: int
+    direct: bool
+    offset: int
+    nbytes: int
+
+
 @dataclass
 class RechunkExchange:
     """What one rank does in a distributed rechunk."""
     rank: int
     world: int
     itemsize: int
-    local: List[Piece]                       # src and dst chunk both owned here
-    send: List[List[Tuple[Piece, int]]]      # per dst rank: (piece, byte offset in send buffer)
-    recv: List[List[Tuple[Piece, int]]]      # per src rank: (piece, byte offset in recv buffer)
-    send_splits: List[int]
-    recv_splits: List[int]
-
-    @property
-    def send_bytes(self) -> int:
-        return sum(self.send_splits)
-
-    @property
-    def recv_bytes(self) -> int:
-        return sum(self.recv_splits)
+    npieces: int
+    local: List[Piece]          # src and dst chunk both owned here
+    send: List[List[Xfer]]      # per dst rank, in piece order
+    recv: List[List[Xfer]]      # per src rank, in piece order
+    pack_bytes: int             # pack buffer (sends whose source box is strided)
+    stage_bytes: int            # staging buffer (receives whose target box is strided)
 
     @property
     def exchanges(self) -> bool:
-        return any(self.send_splits) or any(self.recv_splits)
+        return any(self.send) or any(self.recv)
+
+    @property
+    def send_bytes(self) -> int:
+        return sum(x.nbytes for lst in self.send for x in lst)
+
+    @property
+    def recv_bytes(self) -> int:
+        return sum(x.nbytes for lst in self.recv for x in lst)
+
+    def slice_bounds(self, nslices: int) -> List[Tuple[int, int]]:
+        """``nslices`` ranges of piece indices (the same on every rank)."""
+        n = max(1, self.npieces)
+        return [(n * k // nslices, n * (k + 1) // nslices) for k in range(nslices)]
 
 
 def plan_rechunk(src_grid, dst_grid, rank: int, world: int, itemsize: int,
@@ -115,30 +156,28 @@ def plan_rechunk(src_grid, dst_grid, rank: int, world: int, itemsize: int,
     pieces = rechunk_pieces(src_grid, dst_grid) if pieces is None else pieces
     replicated = src_world == 1
     local = []
-    send: List[List[Tuple[Piece, int]]] = [[] for _ in range(world)]
-    recv: List[List[Tuple[Piece, int]]] = [[] for _ in range(world)]
-    sent = [0] * world
-    got = [0] * world
-    for p in pieces:
+    send: List[List[Xfer]] = [[] for _ in range(world)]
+    recv: List[List[Xfer]] = [[] for _ in range(world)]
+    packed = staged = 0
+    for i, p in enumerate(pieces):
         d = owner_of(dst_grid, p.dst, world)
         s = d if replicated else owner_of(src_grid, p.src, world)
         if s == d:
             if s == rank:
                 local.append(p)
             continue
-        nbytes = round_up(p.size * itemsize)
+        nbytes = p.size * itemsize
         if s == rank:
-            send[d].append((p, sent[d]))
-            sent[d] += nbytes
+            direct = box_contiguous(src_grid.chunk_extent(p.src), p.src_start, p.extent)
+            send[d].append(Xfer(p, i, direct, 0 if direct else packed, nbytes))
+            if not direct:
+                packed += round_up(nbytes)
         if d == rank:
-            recv[s].append((p, got[s]))
-            got[s] += nbytes
-    # per-peer offsets -> absolute offsets in the packed buffers
-    soff = prefix(sent)
-    roff = prefix(got)
-    send = [[(p, o + soff[j]) for p, o in lst] for j, lst in enumerate(send)]
-    recv = [[(p, o + roff[j]) for p, o in lst] for j, lst in enumerate(recv)]
-    return RechunkExchange(rank, world, itemsize, local, send, recv, sent, got)
+            direct = box_contiguous(dst_grid.chunk_extent(p.dst), p.dst_start, p.extent)
+            recv[s].append(Xfer(p, i, direct, 0 if direct else staged, nbytes))
+            if not direct:
+                staged += round_up(nbytes)
+    return RechunkExchange(rank, world, itemsize, len(pieces), local, send, recv, packed, staged)
 
 
 def prefix(xs: Sequence[int]) -> List[int]:

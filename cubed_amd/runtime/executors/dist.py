@@ -8,8 +8,11 @@ crosses GPUs only where a task reads a chunk it does not own:
 
 * ``FetchLaunch``   -- whole chunks read by local tasks but owned elsewhere
   (pack -> RCCL all-to-all -> the task views point into the receive buffer);
-* ``RechunkLaunch`` -- rechunk: local pieces copied in place, the rest packed,
-  exchanged with one all-to-all and unpacked into the target chunks;
+* ``RechunkLaunch`` -- rechunk: local pieces copied in place, the rest moved
+  by grouped point-to-point transfers in 1-4 slices (the pack of slice k+1
+  and the local copies overlap the transfers of slice k); pieces contiguous
+  in their target chunk are received straight into its slot, pieces
+  contiguous in their source chunk are sent from it;
 * ``PartialsLaunch``-- a fused reduction chain whose inputs are spread over
   the ranks: every rank reduces its own chunks to per-field partials
   (CUBED_MODE_PARTIALS), RCCL reduces them (SUM fields) or all-gathers them
@@ -30,7 +33,7 @@ import numpy as np
 from ... import _native as nat
 from ...lowering import Box, CopyLaunch
 from ...storage import DeviceArray, c_strides
-from ..exchange import FetchExchange, RechunkExchange
+from ..exchange import FetchExchange, RechunkExchange, box_offset
 
 FETCH_ROW = 4096  # bytes per row of a whole-chunk pack copy (one wave moves 4 KiB)
 
@@ -85,6 +88,10 @@ class FetchLaunch:
         self.ctx.comm.all_to_all(self.recv, self.send, self.plan.recv_splits, self.plan.send_splits)
 
 
+SLICE_BYTES = 256 << 20  # exchanges moving more than this per rank run in slices
+MAX_SLICES = 4
+
+
 class RechunkLaunch:
     """copy_read_to_write over all target chunks owned here."""
 
@@ -94,46 +101,73 @@ class RechunkLaunch:
 
         self.ctx = ctx
         self.plan = plan
-        isz = dst.dtype.itemsize
-        self.send = torch.empty(max(plan.send_bytes, 16), dtype=torch.uint8, device=ctx.device)
-        self.recv = torch.empty(max(plan.recv_bytes, 16), dtype=torch.uint8, device=ctx.device)
-        sbase, rbase = self.send.data_ptr(), self.recv.data_ptr()
+        isz = plan.itemsize
+        self.pack_buf = torch.empty(max(plan.pack_bytes, 16), dtype=torch.uint8, device=ctx.device)
+        self.stage_buf = torch.empty(max(plan.stage_bytes, 16), dtype=torch.uint8, device=ctx.device)
+        pbase, sbase = self.pack_buf.data_ptr(), self.stage_buf.data_ptr()
 
-        def src_box(p):
+        def src_at(p):
             ext = src.chunk_extent(p.src)
-            st = c_strides(ext)
-            return src.chunk_addr(p.src) + sum(a * s for a, s in zip(p.src_start, st)) * isz, list(st)
+            return src.chunk_addr(p.src) + box_offset(ext, p.src_start) * isz, list(c_strides(ext))
 
-        def dst_box(p):
+        def dst_at(p):
             ext = dst.chunk_extent(p.dst)
-            st = c_strides(ext)
-            return dst.chunk_addr(p.dst) + sum(a * s for a, s in zip(p.dst_start, st)) * isz, list(st)
+            return dst.chunk_addr(p.dst) + box_offset(ext, p.dst_start) * isz, list(c_strides(ext))
 
-        local, pack, unpack = [], [], []
+        def slab_view(arr, addr, nbytes):
+            slab = arr.slabs[None]
+            o = addr - slab.data_ptr()
+            return slab[o:o + nbytes]
+
+        local = []
         for p in plan.local:
-            s, ss = src_box(p)
-            d, ds = dst_box(p)
-            local.append(Box(s, d, list(p.extent), ss, ds))
-        for lst in plan.send:
-            for p, off in lst:
-                s, ss = src_box(p)
-                pack.append(Box(s, sbase + off, list(p.extent), ss, list(c_strides(p.extent))))
-        for lst in plan.recv:
-            for p, off in lst:
-                d, ds = dst_box(p)
-                unpack.append(Box(rbase + off, d, list(p.extent), list(c_strides(p.extent)), ds))
+            s_, ss = src_at(p)
+            d_, ds = dst_at(p)
+            local.append(Box(s_, d_, list(p.extent), ss, ds))
         local.sort(key=lambda b: b.src)
-        pack.sort(key=lambda b: b.src)
         self.local = CopyLaunch(local, isz, ctx.device)
-        self.pack = CopyLaunch(pack, isz, ctx.device)
+        moved = plan.send_bytes + plan.recv_bytes
+        nslices = 1 if moved <= SLICE_BYTES else min(MAX_SLICES, -(-moved // SLICE_BYTES))
+        self.slices = []
+        unpack = []
+        for lo, hi in plan.slice_bounds(nslices):
+            pack, sends, recvs = [], [], []
+            for peer, lst in enumerate(plan.send):
+                for x in lst:
+                    if not lo <= x.index < hi:
+                        continue
+                    a, ss = src_at(x.piece)
+                    if x.direct:
+                        sends.append((slab_view(src, a, x.nbytes), peer))
+                    else:
+                        pack.append(Box(a, pbase + x.offset, list(x.piece.extent), ss,
+                                        list(c_strides(x.piece.extent))))
+                        sends.append((self.pack_buf[x.offset:x.offset + x.nbytes], peer))
+            for peer, lst in enumerate(plan.recv):
+                for x in lst:
+                    if not lo <= x.index < hi:
+                        continue
+                    a, ds = dst_at(x.piece)
+                    if x.direct:
+                        recvs.append((slab_view(dst, a, x.nbytes), peer))
+                    else:
+                        recvs.append((self.stage_buf[x.offset:x.offset + x.nbytes], peer))
+                        unpack.append(Box(sbase + x.offset, a, list(x.piece.extent),
+                                          list(c_strides(x.piece.extent)), ds))
+            pack.sort(key=lambda b: b.src)
+            self.slices.append((CopyLaunch(pack, isz, ctx.device), sends, recvs))
         self.unpack = CopyLaunch(unpack, isz, ctx.device)
-        self.exchange = any(plan.send_splits) or any(plan.recv_splits)
+        self.exchange = plan.exchanges
         self.collective = True  # every rank takes part, even with nothing to move
 
     def run(self, stream):
-        self.pack.run(stream)
-        self.ctx.comm.all_to_all(self.recv, self.send, self.plan.recv_splits, self.plan.send_splits)
-        self.local.run(stream)
+        pending = []
+        for pack, sends, recvs in self.slices:
+            pack.run(stream)
+            pending.append(self.ctx.comm.exchange(sends, recvs))
+        self.local.run(stream)  # overlaps the transfers
+        for p in pending:
+            p.wait()
         self.unpack.run(stream)
 
 

@@ -64,8 +64,11 @@ def test_rechunk_is_one_exchange_per_rank(built):
         rl = [l for l in dry.launched if isinstance(l, RechunkLaunch)]
         assert len(rl) == 1
         plan = rl[0].plan
-        # 6 source x 5 target chunks: 10x10 f32 pieces, 400 B padded to 512
-        assert sum(plan.send_splits) == sum(512 for d in range(world) for _ in plan.send[d])
+        # 6 source x 5 target chunks: 10x10 f32 pieces, each a contiguous
+        # row band of its (60, 10) target chunk: received in place, no unpack
+        assert plan.stage_bytes == 0 and rl[0].unpack.nboxes == 0
+        assert plan.pack_bytes == sum(512 for d in range(world) for _ in plan.send[d])
+        assert sum(s[0].nboxes for s in rl[0].slices) == sum(len(l) for l in plan.send)
         assert rl[0].local.nboxes == len(plan.local)
 
 

@@ -16,6 +16,8 @@ import numpy as np
 import pytest
 
 from cubed_amd.runtime.exchange import (
+    box_contiguous,
+    box_offset,
     owner_of,
     plan_fetch,
     plan_rechunk,
@@ -65,16 +67,51 @@ def test_rechunk_plans_agree_between_ranks(case, world):
         for d in range(world):
             sent = plans[s].send[d]
             got = plans[d].recv[s]
-            assert [p for p, _ in sent] == [p for p, _ in got]
-            assert plans[s].send_splits[d] == plans[d].recv_splits[s]
-            assert plans[s].send_splits[d] == sum(round_up(p.size * 4) for p, _ in sent)
-            for p, _ in sent:
+            # both ends post the pair's transfers in the same order and sizes
+            assert [(x.piece, x.index, x.nbytes) for x in sent] == [(x.piece, x.index, x.nbytes) for x in got]
+            assert [x.index for x in sent] == sorted(x.index for x in sent)
+            for x in sent:
+                p = x.piece
                 assert owner_of(src, p.src, world) == s and owner_of(dst, p.dst, world) == d
-            moved += sum(p.size for p, _ in sent)
+                assert x.nbytes == p.size * 4
+                assert x.direct == box_contiguous(src.chunk_extent(p.src), p.src_start, p.extent)
+            for x in got:
+                p = x.piece
+                assert x.direct == box_contiguous(dst.chunk_extent(p.dst), p.dst_start, p.extent)
+            moved += sum(x.piece.size for x in sent)
         moved += sum(p.size for p in plans[s].local)
+        # packed / staged pieces get disjoint 256-B aligned buffer ranges
+        for lst, size in ((plans[s].send, plans[s].pack_bytes), (plans[s].recv, plans[s].stage_bytes)):
+            spans = sorted((x.offset, x.offset + x.nbytes) for l in lst for x in l if not x.direct)
+            assert all(a % 256 == 0 for a, _ in spans)
+            assert all(b1 <= a2 for (_, b1), (a2, _) in zip(spans, spans[1:]))
+            assert all(b <= size for _, b in spans)
     assert moved == total
     if world == 1:
         assert not plans[0].exchanges
+
+
+def test_row_bands_of_column_chunks_land_in_place():
+    """Config 3's shape: every piece (a row band of a source row chunk x the
+    target's columns) is one contiguous run of its target column chunk, so
+    nothing is staged (no unpack pass); the sources are strided (packed)."""
+    src, dst = ChunkGrid((40, 40), np.float32, (5, 40)), ChunkGrid((40, 40), np.float32, (40, 5))
+    for world in (2, 8):
+        for r in range(world):
+            plan = plan_rechunk(src, dst, r, world, 4)
+            assert plan.stage_bytes == 0 and all(x.direct for l in plan.recv for x in l)
+            assert all(not x.direct for l in plan.send for x in l)
+            assert plan.pack_bytes == sum(round_up(x.nbytes) for l in plan.send for x in l)
+
+
+def test_box_contiguity():
+    assert box_contiguous((10, 8), (3, 0), (4, 8))       # whole rows
+    assert box_contiguous((10, 8), (3, 2), (1, 5))       # part of one row
+    assert not box_contiguous((10, 8), (3, 2), (2, 5))   # parts of two rows
+    assert box_contiguous((4, 6, 8), (1, 0, 0), (2, 6, 8))
+    assert box_contiguous((4, 6, 8), (1, 2, 0), (1, 3, 8))
+    assert not box_contiguous((4, 6, 8), (1, 2, 0), (2, 3, 8))
+    assert box_offset((4, 6, 8), (1, 2, 3)) == 1 * 48 + 2 * 8 + 3
 
 
 def test_replicated_source_is_all_local():
@@ -107,7 +144,12 @@ def test_fetch_plan_consistency():
 # ---------------------------------------------------------------- gloo data path
 
 
-def _rechunk_rank(rank, world, case):
+def _rechunk_rank(rank, world, case, nslices):
+    """RechunkLaunch's data path with numpy box copies in place of the pack /
+    unpack / local HIP copies: chunk slots are byte tensors, direct transfers
+    are views of them (the bytes land in the target slot), the rest go
+    through the pack and staging buffers; slices are started in order and
+    waited for at the end, as RechunkLaunch.run does."""
     import torch
 
     from cubed_amd.runtime.comm import Comm
@@ -119,36 +161,63 @@ def _rechunk_rank(rank, world, case):
     def chunk(grid, c):
         return tuple(slice(s, s + e) for s, e in zip(grid.chunk_start(c), grid.chunk_extent(c)))
 
-    mine = {c: full[chunk(src, c)].copy() for c in itertools.product(*map(range, src.numblocks))
-            if owner_of(src, c, world) == rank}
-    out = {c: np.full(dst.chunk_extent(c), -1, np.float32)
+    def box(p_start, extent):
+        return tuple(slice(a, a + e) for a, e in zip(p_start, extent))
+
+    mine = {c: torch.from_numpy(full[chunk(src, c)].copy().reshape(-1).view(np.uint8))
+            for c in itertools.product(*map(range, src.numblocks)) if owner_of(src, c, world) == rank}
+    out = {c: torch.full((math.prod(dst.chunk_extent(c)) * 4,), 255, dtype=torch.uint8)
            for c in itertools.product(*map(range, dst.numblocks)) if owner_of(dst, c, world) == rank}
+
+    def as_array(buf, grid, c):
+        return buf.numpy().view(np.float32).reshape(grid.chunk_extent(c))
+
     plan = plan_rechunk(src, dst, rank, world, 4)
-    send = np.zeros(max(plan.send_bytes, 16), np.uint8)
-    for lst in plan.send:
-        for p, off in lst:
-            box = mine[p.src][tuple(slice(a, a + e) for a, e in zip(p.src_start, p.extent))]
-            send[off:off + box.nbytes] = np.ascontiguousarray(box).view(np.uint8).reshape(-1)
-    recv = torch.zeros(max(plan.recv_bytes, 16), dtype=torch.uint8)
-    comm.all_to_all(recv, torch.from_numpy(send), plan.recv_splits, plan.send_splits)
-    rb = recv.numpy()
+    pack = torch.zeros(max(plan.pack_bytes, 16), dtype=torch.uint8)
+    stage = torch.zeros(max(plan.stage_bytes, 16), dtype=torch.uint8)
+    pending = []
+    for lo, hi in plan.slice_bounds(nslices):
+        sends, recvs = [], []
+        for peer, lst in enumerate(plan.send):
+            for x in (x for x in lst if lo <= x.index < hi):
+                p = x.piece
+                if x.direct:
+                    o = box_offset(src.chunk_extent(p.src), p.src_start) * 4
+                    sends.append((mine[p.src][o:o + x.nbytes], peer))
+                else:
+                    vals = as_array(mine[p.src], src, p.src)[box(p.src_start, p.extent)]
+                    pack[x.offset:x.offset + x.nbytes] = torch.from_numpy(
+                        np.ascontiguousarray(vals).reshape(-1).view(np.uint8))
+                    sends.append((pack[x.offset:x.offset + x.nbytes], peer))
+        for peer, lst in enumerate(plan.recv):
+            for x in (x for x in lst if lo <= x.index < hi):
+                p = x.piece
+                if x.direct:
+                    o = box_offset(dst.chunk_extent(p.dst), p.dst_start) * 4
+                    recvs.append((out[p.dst][o:o + x.nbytes], peer))
+                else:
+                    recvs.append((stage[x.offset:x.offset + x.nbytes], peer))
+        pending.append(comm.exchange(sends, recvs))
     for p in plan.local:
-        out[p.dst][tuple(slice(a, a + e) for a, e in zip(p.dst_start, p.extent))] = \
-            mine[p.src][tuple(slice(a, a + e) for a, e in zip(p.src_start, p.extent))]
+        as_array(out[p.dst], dst, p.dst)[box(p.dst_start, p.extent)] = \
+            as_array(mine[p.src], src, p.src)[box(p.src_start, p.extent)]
+    for h in pending:
+        h.wait()
     for lst in plan.recv:
-        for p, off in lst:
-            n = p.size * 4
-            out[p.dst][tuple(slice(a, a + e) for a, e in zip(p.dst_start, p.extent))] = \
-                rb[off:off + n].view(np.float32).reshape(p.extent)
+        for x in (x for x in lst if not x.direct):
+            p = x.piece
+            as_array(out[p.dst], dst, p.dst)[box(p.dst_start, p.extent)] = \
+                stage[x.offset:x.offset + x.nbytes].numpy().view(np.float32).reshape(p.extent)
     for c, v in out.items():
-        assert np.array_equal(v, full[chunk(dst, c)]), (rank, c)
+        assert np.array_equal(as_array(v, dst, c), full[chunk(dst, c)]), (rank, c)
     return len(out)
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_rechunk_exchange_over_gloo(world):
+@pytest.mark.parametrize("nslices", [1, 3])
+def test_rechunk_exchange_over_gloo(world, nslices):
     for case in CASES[:3]:
-        counts = run_ranks(_rechunk_rank, world, case)
+        counts = run_ranks(_rechunk_rank, world, case, nslices)
         src, dst = grids(case)
         assert sum(counts) == math.prod(dst.numblocks)
 
