@@ -40,6 +40,9 @@ def asarray(obj, /, *, dtype=None, device=None, copy=None, chunks="auto", spec=N
             a = a.astype(dtype)
     if dtype is None:
         dtype = a.dtype
+    from ..ir import check_input_dtype
+
+    check_input_dtype(a.dtype)
     chunksize = to_chunksize(normalize_chunks(chunks, shape=a.shape, dtype=dtype)) if a.ndim else ()
     name = gensym()
     target = virtual_in_memory(a, chunks=chunksize)

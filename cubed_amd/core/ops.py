@@ -57,6 +57,9 @@ def from_array(x, chunks="auto", asarray=None, spec=None) -> "Array":
     HBM by the executor (reference: map_blocks(_from_array), core/ops.py:40-85)."""
     if isinstance(x, CoreArray):
         raise ValueError("Array is already a Cubed array. Use 'asarray' or 'rechunk' instead.")
+    from ..ir import check_input_dtype
+
+    check_input_dtype(x.dtype)
     previous_chunks = getattr(x, "chunks", None)
     outchunks = normalize_chunks(chunks, x.shape, dtype=x.dtype, previous_chunks=previous_chunks)
     host = HostArray(np.asarray(x) if (asarray or asarray is None) else x, to_chunksize(outchunks) if x.ndim else ())

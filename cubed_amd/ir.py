@@ -28,10 +28,23 @@ import numpy as np
 
 # ----------------------------------------------------------------- dtypes
 
-# numpy has no bfloat16: it is carried as a distinct 2-byte void dtype (its
-# bit pattern = the top half of an IEEE f32).  The kernels load/store it as
-# CUBED_BF16; host readback widens it exactly to float32 (bf16_to_numpy).
-bfloat16 = np.dtype("V2")
+# numpy has no bfloat16: it is carried as a 2-byte void dtype tagged with
+# metadata (its bit pattern = the top half of an IEEE f32).  The kernels
+# load/store it as CUBED_BF16; host readback widens it exactly to float32
+# (bf16_to_numpy).  numpy keeps the tag through views, copies and slices;
+# an UNtagged 2-byte void array handed to from_array / asarray is refused
+# (check_input_dtype) instead of being read as bf16.
+bfloat16 = np.dtype("V2", metadata={"cubed_bf16": True})
+
+
+def check_input_dtype(dt):
+    """Refuse raw void dtypes at the API boundary: only the tagged bfloat16
+    carrier (and structured dtypes) may enter as 'V'."""
+    dt = np.dtype(dt)
+    if dt.kind == "V" and not dt.names and not (dt.metadata or {}).get("cubed_bf16"):
+        raise TypeError(f"raw void dtype {dt} is not an array dtype here (bfloat16 data: "
+                        "use cubed_amd.array_api.bfloat16 / ir.numpy_to_bf16)")
+    return dt
 
 DTYPE_CODES = {
     bfloat16: 12,

@@ -496,6 +496,7 @@ class Codegen:
             self.code.append((ir_op("CAST"), r, 0, 0, ir.dtype_code(e.dtype), ir.dtype_code(e.dtype)))
         k = self.skey(e)
         if self.uses.get(k, 0) > 1:
+            self._last_use(k)  # the computing visit is one of the uses
             self.cache[k] = r
             return r, False
         return r, True

@@ -91,3 +91,23 @@ def test_codegen_matches_numpy_on_random_programs():
             for e, r in zip(outs, regs_out):
                 assert np.array_equal(regs[r], evaluate(e, vals), equal_nan=True), (trial, e)
     assert tried > 500
+
+
+def test_common_subexpression_handed_over_at_last_use():
+    """t = exp(x0) is used twice: first as the left operand of t * x1 (it
+    stays cached, so that use copies it), last as the left operand of
+    t - x2: handed over in place, no second MOV."""
+    x = [ir.Arg(i, F8, (0,)) for i in range(3)]
+    t = ir.Unary("exp", x[0], F8)
+    out = ir.Binary("add", ir.Binary("multiply", t, x[1], F8), ir.Binary("subtract", t, x[2], F8), F8)
+    cg = Codegen(V_F64, {id(a): a.index for a in x})
+    cg.count_uses([out])
+    r, _ = cg.gen(out)
+    movs = [c for c in cg.code if c[0] == _OPCODES["MOV"]]
+    assert len(movs) == 1, cg.code
+    vals = [np.linspace(-1, 1, 8) * (i + 1) for i in range(3)]
+    regs = {i: vals[i].copy() for i in range(3)}
+    for i in range(3, 6):
+        regs[i] = np.full(8, np.nan)
+    run(cg.code, regs)
+    assert np.array_equal(regs[r], np.exp(vals[0]) * vals[1] + (np.exp(vals[0]) - vals[2]))

@@ -449,6 +449,21 @@ def test_matmul_without_k_sum_fusion_is_per_chunk(built, dry):
     assert g.n == 2 * 3 * 2 and all(int(t["nseg"]) == 1 for t in g.tasks)
 
 
+def test_raw_void_arrays_are_refused():
+    """A 2-byte void array is not taken for bf16 data: only the
+    tagged carrier enters; its tag survives numpy views and copies."""
+    from cubed_amd import ir
+
+    raw = np.zeros((4, 4), dtype="V2")
+    with pytest.raises(TypeError, match="raw void"):
+        cubed.from_array(raw, chunks=2)
+    with pytest.raises(TypeError, match="raw void"):
+        xp.asarray(raw)
+    ok = ir.numpy_to_bf16(np.ones((4, 4), np.float32))
+    assert ir.is_bf16(ok.dtype) and ok[1:].copy().dtype.metadata == {"cubed_bf16": True}
+    assert cubed.from_array(ok, chunks=2).dtype == xp.bfloat16
+
+
 def test_bfloat16_promotion():
     assert xp.result_type(xp.bfloat16, xp.bfloat16) == xp.bfloat16
     assert xp.result_type(xp.bfloat16, xp.float32) == xp.float32
