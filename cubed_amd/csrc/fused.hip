@@ -186,7 +186,13 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     if (L.bpt < 1) L.bpt = 1;
     if (L.bpt > 65536) L.bpt = 65536;
     const int64_t base = ntasks * L.bpt;
-    if (P->nfields > 0 && base < (256 * 9) / 10 && max_red >= 64)
+    // bytes of loads one workgroup keeps in flight: U rows x leaves x W
+    // groups x 4 elements per lane; below ~96 KiB per CU the grid cannot
+    // cover HBM latency (the per-rank share of the elided rechunk + mean:
+    // 350 one-leaf f32 workgroups = 44 KiB per CU, 2.9 TB/s unsplit)
+    const int isz = P->vtype == CUBED_V_F32 ? 4 : 8;
+    const int64_t inflight = (int64_t)kBlock * stream_unroll(isz, P->nleaves) * P->nleaves * W * 4 * isz;
+    if (P->nfields > 0 && base * inflight < (int64_t)256 * 96 * 1024 && max_red >= 64)
       L.nsplit = (int32_t)choose_split(base, max_red / 16, kStreamTarget);
     L.blocks = ntasks * L.nsplit * L.bpt;
   } else if (L.kernel == 0) {

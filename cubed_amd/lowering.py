@@ -1637,7 +1637,8 @@ def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
     W gives each lane about 256 B of loads in flight (U rows x leaves x W
     groups x 4 elements), e.g. W = 2 for quad-means' two f32 leaves -- but
     only when the W-wide grid still fills the CUs without a time split
-    (>= 230 workgroups; config 1's split grid ran 2.7x slower with W = 2)
+    (>= 96 KiB of loads in flight per CU; config 1's split grid ran 2.7x
+    slower with W = 2)
     and a task's kept extent fills at least 8 workgroups of 1024 W elements
     (the elided rechunk+mean's 1000-wide pieces left half of every
     workgroup idle with W = 2: 2.7x slower; profiles/r02_stream_ab.log)."""
@@ -1649,7 +1650,10 @@ def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
         w = 256 // (_stream_unroll(isz, nl) * nl * 4 * isz)
         w = 4 if w >= 4 else 2 if w >= 2 else 1
         slots = -(-max_kept // (256 * w)) * 64
-        if w > 1 and (ntasks * -(-slots // 256) < 230 or max_kept < 8 * 1024 * w):
+        # the W-wide grid must hold >= 96 KiB of loads in flight per CU
+        # unsplit (fused.hip plan_launch splits below that)
+        inflight = 256 * _stream_unroll(isz, nl) * nl * w * 4 * isz
+        if w > 1 and (ntasks * -(-slots // 256) * inflight < 256 * 96 * 1024 or max_kept < 8 * 1024 * w):
             w = 1
     return MODE_STREAM_W4 if w == 4 else MODE_STREAM_W2 if w == 2 else 0
 

@@ -41,6 +41,7 @@ __device__ __forceinline__ long xcd_remap(long b, long nblk) {
 // of row chunk i.
 template <bool IMAJOR, bool REMAP, bool NT, int U, int PPW>
 __global__ __launch_bounds__(256) void k_pieces(const float* __restrict__ x, double* __restrict__ part) {
+  static_assert(RC % U == 0, "rows in flight must divide the row chunk (no reads past the array)");
   long g = blockIdx.x;
   if (REMAP) g = xcd_remap(g, gridDim.x);
   const int tid = threadIdx.x;
@@ -141,12 +142,12 @@ int main(int argc, char** argv) {
   run("i-major plain cached U8", k_pieces<true, false, false, 8, 1>, 1, false);
   run("i-major xcd-remap nt U8", k_pieces<true, true, true, 8, 1>, 1, false);
   run("i-major xcd-remap cached U8", k_pieces<true, true, false, 8, 1>, 1, false);
-  run("i-major xcd-remap cached U16", k_pieces<true, true, false, 16, 1>, 1, false);
+  run("i-major xcd-remap cached U10", k_pieces<true, true, false, 10, 1>, 1, false);
   run("i-major xcd-remap cached U4", k_pieces<true, true, false, 4, 1>, 1, false);
   run("i-major plain cached U8, 2 pieces/WG", k_pieces<true, false, false, 8, 2>, 2, false);
   run("i-major xcd-remap cached U8, 2 pieces/WG", k_pieces<true, true, false, 8, 2>, 2, false);
   run("i-major xcd-remap nt U8, 2 pieces/WG", k_pieces<true, true, true, 8, 2>, 2, false);
-  run("i-major xcd-remap cached U16, 2 pieces/WG", k_pieces<true, true, false, 16, 2>, 2, false);
+  run("i-major xcd-remap cached U20, 2 pieces/WG", k_pieces<true, true, false, 20, 2>, 2, false);
   run("j-major plain nt U8 (again)", k_pieces<false, false, true, 8, 1>, 1, false);
   return 0;
 }
