@@ -390,16 +390,28 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 // LDS slot: A [256 rows][16 k] (64-B rows, 16-B chunk c of row r at
 // position c ^ ((r >> 2) & 3): conflict-free b128 reads) + B [16 k][256 n]
 // (1 KiB rows, as in HBM).
-constexpr int HF_BM = 256, HF_BN = 256, HF_BK = 16, HF_NS = 4;
-constexpr int HF_A = HF_BM * HF_BK * 4;  // 16 KiB
-constexpr int HF_B = HF_BK * HF_BN * 4;  // 16 KiB
-constexpr int HF_STAGE = HF_A + HF_B;
+constexpr int HF_BM = 256, HF_BN = 256;
 
+// BK: K depth of one ring slot (16 or 32); NS: ring slots.  A slot holds A
+// [256 rows][BK k] (BK*4-byte rows, CPR = BK/4 16-B chunks, chunk c of row
+// r at position c ^ swz(r): conflict-free b128 reads) + B [BK k][256 n]
+// (1 KiB rows, as in HBM).
+template <int BK, int NS>
 __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
                                                         int64_t tiles_m, int64_t tiles_n,
                                                         const char* __restrict__ zero) {
-  __shared__ __attribute__((aligned(1024))) char lds_[HF_NS * HF_STAGE];
+  static_assert(BK == 16 || BK == 32, "K step of 16 or 32");
+  constexpr int SA = HF_BM * BK * 4, SB = BK * HF_BN * 4, STAGE = SA + SB;
+  constexpr int CPR = BK / 4;            // 16-B chunks per A row
+  constexpr int RPI = 1024 / (BK * 4);   // A rows per wave instruction (1 KiB)
+  constexpr int NA = HF_BM / RPI / 8;    // A loads per wave per step
+  constexpr int NB = BK / 8;             // B loads per wave per step
+  constexpr int LPS = NA + NB;           // vmcnt per step
+  constexpr int SWS = BK == 16 ? 2 : 1;  // swz(r) = (r >> SWS) & (CPR - 1)
+  constexpr int G = BK / 8;              // 8-deep k groups per step
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char lds_[NS * STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
   tile_of<HF_BM, HF_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
@@ -413,17 +425,18 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
   const int wm = (w >> 1) * 64, wn = (w & 1) * 128;
 
   // ---- staging geometry (constant over the K loop)
-  // A: wave w instruction i stages rows 16*(2w+i) + lane>>2; LDS position
-  // lane&3 of the row holds global chunk (lane&3) ^ ((lane>>4)&3)
-  int64_t gmA[2];
+  // A: wave w instruction i stages rows RPI*(NA*w + i) + lane/CPR; LDS
+  // position lane%CPR of the row holds global chunk (lane%CPR) ^ swz(row)
+  int64_t gmA[NA];
+  int kA[NA];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int64_t r = 16 * (2 * w + i) + (lane >> 2);
+  for (int i = 0; i < NA; ++i) {
+    const int r = RPI * (NA * w + i) + lane / CPR;
     gmA[i] = (m0 + r < M ? m0 + r : M - 1);
+    kA[i] = 4 * ((lane % CPR) ^ ((r >> SWS) & (CPR - 1)));
   }
-  const int kA = 4 * ((lane & 3) ^ ((lane >> 4) & 3));  // k offset of this lane's chunk
-  // B: wave w instruction i stages k-row 2w+i, columns n0 + 4*lane .. +3
-  const int rB0 = 2 * w;
+  // B: wave w instruction i stages k-row NB*w + i, columns n0 + 4*lane .. +3
+  const int rB0 = NB * w;
   const int64_t gnB = (n0 + 4 * lane + 4 <= N ? n0 + 4 * lane : N - 4);
 
   int64_t s = seg0, ks = 0;
@@ -433,34 +446,36 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
   int64_t ke = segs[s].k;
 
   auto stage = [&](int64_t k0, CUBED_L char* buf) {
-    const char* sa[2];
-    const char* sb[2];
+    const char* sa[NA];
+    const char* sb[NB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      sa[i] = a_cur + gmA[i] * lda4 + (k0 - ks + kA) * 4;
-      sb[i] = b_cur + (k0 - ks + rB0 + i) * ldb4 + gnB * 4;
-    }
-    if (k0 + HF_BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
+    for (int i = 0; i < NA; ++i) sa[i] = a_cur + gmA[i] * lda4 + (k0 - ks + kA[i]) * 4;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) sb[i] = b_cur + (k0 - ks + rB0 + i) * ldb4 + gnB * 4;
+    if (k0 + BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
       const bool has_next = s + 1 < segN;
       const int64_t sn = has_next ? s + 1 : s;
       const char* na = (const char*)(uintptr_t)segs[sn].a;
       const char* nb = (const char*)(uintptr_t)segs[sn].b;
       const int64_t nlda4 = segs[sn].lda * 4, nldb4 = segs[sn].ldb * 4;
-      const int64_t ka = k0 + kA;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NA; ++i) {
+        const int64_t ka = k0 + kA[i];
         const char* pa = na + gmA[i] * nlda4 + (ka - ke) * 4;
         sa[i] = ka < ke ? sa[i] : ((has_next && ka < KT) ? pa : zero);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
         const int64_t kb = k0 + rB0 + i;
         const char* pb = nb + (kb - ke) * nldb4 + gnB * 4;
         sb[i] = kb < ke ? sb[i] : ((has_next && kb < KT) ? pb : zero);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(sa[i], buf + (2 * w + i) * 1024);
+    for (int i = 0; i < NA; ++i) glds16(sa[i], buf + (NA * w + i) * 1024);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(sb[i], buf + HF_A + (rB0 + i) * 1024);
-    if (k0 + HF_BK >= ke && s + 1 < segN) {  // the next step starts in the next segment
+    for (int i = 0; i < NB; ++i) glds16(sb[i], buf + SA + (rB0 + i) * 1024);
+    if (k0 + BK >= ke && s + 1 < segN) {  // the next step starts in the next segment
       ks = ke;
       ++s;
       a_cur = (const char*)(uintptr_t)segs[s].a;
@@ -474,14 +489,14 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
   // ---- fragment read offsets (within a slot)
   const int h = lane >> 5, r32 = lane & 31;
   // A, row block rb, k group g: row wm + 32 rb + r32, logical chunk 2g + h
-  int offA[2][2];
+  int offA[2][G];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
-      offA[rb][g] = (wm + 32 * rb + r32) * 64 + 16 * ((2 * g + h) ^ ((r32 >> 2) & 3));
+    for (int g = 0; g < G; ++g)
+      offA[rb][g] = (wm + 32 * rb + r32) * (BK * 4) + 16 * ((2 * g + h) ^ ((r32 >> SWS) & (CPR - 1)));
   // B, k group g, step j: k-row 8g + 4h + j, columns wn + 4 r32 .. +3
-  const int offB = HF_A + 4 * h * 1024 + (wn + 4 * r32) * 4;
+  const int offB = SA + 4 * h * 1024 + (wn + 4 * r32) * 4;
 
   f32x16 acc[2][4];
 #pragma unroll
@@ -491,18 +506,18 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][q][r] = 0.f;
 
-  const int64_t nst = (KT + HF_BK - 1) / HF_BK;
-  constexpr int D = HF_NS - 1;  // steps staged ahead
-  for (int64_t p = 0; p < D && p < nst; ++p) stage(p * HF_BK, lds + p * HF_STAGE);
-  // retire this wave's loads of step q (4 per step; steps up to q + D - 1 issued)
+  const int64_t nst = (KT + BK - 1) / BK;
+  constexpr int D = NS - 1;  // steps staged ahead
+  for (int64_t p = 0; p < D && p < nst; ++p) stage(p * BK, lds + p * STAGE);
+  // retire this wave's loads of step q (LPS per step; steps up to q + D - 1 issued)
   auto wait_step = [&](int64_t q) {
     int64_t younger = nst - 1 - q;
     if (younger > D - 1) younger = D - 1;
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * LPS) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(LPS) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  int rd = 0, wr_slot = D;
+  int rd = 0, wr_slot = D % NS;
   for (int64_t p = 0; p < nst; ++p) {
     // this wave's step p landed; then every wave's (barrier), and every wave
     // finished reading step p-1's slot (restaged below)
@@ -510,23 +525,23 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (p + D < nst) stage((p + D) * HF_BK, lds + wr_slot * HF_STAGE);
-    const CUBED_L char* bufc = lds + rd * HF_STAGE;
-    rd = rd + 1 == HF_NS ? 0 : rd + 1;
-    wr_slot = wr_slot + 1 == HF_NS ? 0 : wr_slot + 1;
-    // all 12 fragment reads of the step first (group 0's A and B, then group
-    // 1's): group 1's land while group 0's 32 MFMAs run
-    f32x4 af[2][2], bq[2][4];
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    if (p + D < nst) stage((p + D) * BK, lds + wr_slot * STAGE);
+    const CUBED_L char* bufc = lds + rd * STAGE;
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
+    // fragments of group g+1 are read while group g's 32 MFMAs run
+    f32x4 af[G][2], bq[G][4];
+    auto read_group = [&](int g) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) af[g][rb] = *(const CUBED_L f32x4*)(bufc + offA[rb][g]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bq[g][j] = *(const CUBED_L f32x4*)(bufc + offB + (8 * g + j) * 1024);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (counted lgkmcnt waits follow)
+    };
+    read_group(0);
+    if constexpr (G > 1) read_group(1);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -534,6 +549,12 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             acc[rb][q] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g][rb][j], bq[g][j][q], acc[rb][q], 0, 0, 0);
+      if (g + 2 < G) {
+        __builtin_amdgcn_sched_barrier(0);
+        read_group(g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   }
 
   // ---- epilogue: accumulator (rb, q) register r = row wm + 32 rb + (r&3) +
@@ -714,8 +735,8 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
     const int64_t blocks = ntasks * tm * tn;
     if (blocks > 0x7fffffff) return fail("grid too large");
-    hipLaunchKernelGGL(k_gemm_f32_chain, dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm, tn,
-                       (const char*)d_zero);
+    hipLaunchKernelGGL((k_gemm_f32_chain<16, 4>), dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm,
+                       tn, (const char*)d_zero);
   } else {
     const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
     const int64_t blocks = ntasks * tm * tn;

@@ -15,6 +15,7 @@ thread_local char g_err[512];
 }
 #include "../cubed_amd/csrc/gemm_chain.hip"
 #include "gemm_bf16_experiments.h"
+#include "gemm_bf16_bt.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -61,6 +62,23 @@ int main(int argc, char** argv) {
         segs[t * nb + k] = {(int64_t)(uintptr_t)(A + (i * nb + k) * slot_in),
                             (int64_t)(uintptr_t)(B + (k * nb + j) * slot_in), Cc, Cc, Cc, 0};
     }
+  // B^T chunks (n x k, pitch k) for the transposed-B variants
+  char* BT;
+  CHECK(hipMalloc(&BT, slot_in * nb * nb));
+  {
+    const int64_t per = ((Cc + 63) / 64) * ((Cc + 63) / 64);
+    k_transpose_bf16<<<(unsigned)(per * nb * nb), 256>>>((const uint16_t*)B, (uint16_t*)BT, Cc, Cc, slot_in,
+                                                        nb * nb);
+    CHECK(hipDeviceSynchronize());
+  }
+  std::vector<cubed_gemm_seg_t> segs_bt(segs);
+  for (int64_t i = 0; i < nb; ++i)
+    for (int64_t j = 0; j < nb; ++j)
+      for (int64_t k = 0; k < nb; ++k)
+        segs_bt[(i * nb + j) * nb + k].b = (int64_t)(uintptr_t)(BT + (k * nb + j) * slot_in);
+  cubed_gemm_seg_t* dsbt;
+  CHECK(hipMalloc(&dsbt, sizeof(cubed_gemm_seg_t) * segs.size()));
+  CHECK(hipMemcpy(dsbt, segs_bt.data(), sizeof(cubed_gemm_seg_t) * segs.size(), hipMemcpyHostToDevice));
   cubed_gemm_chain_t *dt0, *dt1;
   cubed_gemm_seg_t* ds;
   CHECK(hipMalloc(&dt0, sizeof(cubed_gemm_chain_t) * tasks.size()));
@@ -80,17 +98,13 @@ int main(int argc, char** argv) {
   float* dmax;
   CHECK(hipMalloc(&dmax, 4));
 
-  struct V { const char* name; kfn f; bool check; int threads = 0; };
+  struct V { const char* name; kfn f; bool check; int threads = 0; bool bt = false; };
   V vs[] = {
       {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, true>, false},
-      {"pp abl: no vmcnt wait", k_gemm_bf16_chain<false, 16, true>, false},
-      {"pp abl: L2-resident staging", k_gemm_bf16_chain<false, 32, true>, false},
-      {"pp abl: no staging", k_gemm_bf16_chain<false, 1 | 16, true>, false},
-      {"pp abl: L2-res + no wait", k_gemm_bf16_chain<false, 32 | 16, true>, false},
-      {"ping-pong NS4 (reference)", k_gemm_bf16_chain<false, 0, true>, false},
-      {"q4 (4-phase BK64)", k_gemm_bf16_q4<false, 4>, true},
-      {"w4 (1 wave/SIMD, 128x128)", k_gemm_bf16_w4<false, 4>, true, 256},
+      {"ping-pong, A in 128-B lines", k_gemm_bf16_a64<false>, true},
+      {"ping-pong, B^T b128 reads", k_gemm_bf16_bt<false>, true, 0, true},
       {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, true>, true},
+      {"ping-pong, A in 128-B lines (again)", k_gemm_bf16_a64<false>, true},
   };
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
   for (const V& v : vs) {
@@ -98,7 +112,8 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(v.f, grid, v.threads ? dim3(v.threads) : blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z);
+      hipLaunchKernelGGL(v.f, grid, v.threads ? dim3(v.threads) : blk, 0, 0, v.check ? dt1 : dt0, v.bt ? dsbt : ds,
+                         tm, tn, (const char*)Z);
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
@@ -106,7 +121,7 @@ int main(int argc, char** argv) {
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       if (r > 0 && ms < best) best = ms;
     }
-    printf("%-28s %9.3f ms %7.1f TF\n", v.name, best, flop / best / 1e9);
+    printf("%-36s %9.3f ms %7.1f TF\n", v.name, best, flop / best / 1e9);
     if (v.check) {
       CHECK(hipMemset(dmax, 0, 4));
       k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
