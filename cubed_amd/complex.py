@@ -15,8 +15,10 @@ complex output becomes the structured output {real, imag}, and a complex
 reduction field becomes one field per part.  Layout copies (rechunk, index,
 concat) move each part slab.
 
-Ops with no real-pair form here (complex powers, trigonometric functions,
-ordering comparisons, prod over complex values) raise LoweringError.
+Powers (exp(w log z)), sin / cos / tan and their hyperbolic forms (the
+FreeBSD / npymath formulas numpy uses for finite values) are rewritten too.
+Ops with no real-pair form here (inverse trigonometric functions, ordering
+comparisons, prod over complex values) raise LoweringError.
 """
 
 from __future__ import annotations
@@ -202,6 +204,14 @@ class _Splitter:
             return ("c", _un("log", _bin("hypot", re, im, p), p), _bin("atan2", im, re, p))
         if op == "sqrt":
             return self._sqrt(re, im, p)
+        if op in ("sinh", "cosh", "sin", "cos"):
+            return self._hyp(op, re, im, p)
+        if op in ("tanh", "tan"):
+            if op == "tanh":
+                return self._tanh(re, im, p)
+            # tan z = -i tanh(i z), i z = (-im, re)
+            _, a, b = self._tanh(_un("negative", im, p), re, p)
+            return ("c", b, _un("negative", a, p))
         if op == "sign":
             # numpy 2: z / |z|, 0 at 0
             a = _bin("hypot", re, im, p)
@@ -209,6 +219,71 @@ class _Splitter:
             return ("c", ir.Where(z, _const(0, p), _bin("divide", re, a, p), p),
                     ir.Where(z, _const(0, p), _bin("divide", im, a, p), p))
         raise _err(f"complex {op} is not lowered on the MI355X executor")
+
+    def _hyp(self, op, re, im, p) -> Val:
+        # npy_csinh / npy_ccosh for finite values (FreeBSD s_csinh.c):
+        #   sinh z = (sinh x cos y, cosh x sin y), cosh z = (cosh x cos y, sinh x sin y),
+        # y = 0 exact: sinh(x + 0i) = (sinh x, y), cosh(x + 0i) = (cosh x, x y);
+        # sin z = -i sinh(i z) = (sin x cosh y, cos x sinh y),
+        # cos z = cosh(i z) = (cos x cosh y, -sin x sinh y)
+        if op in ("sin", "cos"):
+            x, y = _un("negative", im, p), re  # i z
+        else:
+            x, y = re, im
+        shx, chx = _un("sinh", x, p), _un("cosh", x, p)
+        cy, sy = _un("cos", y, p), _un("sin", y, p)
+        zero = _bin("equal", y, _const(0, p), np.bool_)
+        if op in ("sinh", "sin"):
+            a = ir.Where(zero, shx, _bin("multiply", shx, cy, p), p)
+            b = ir.Where(zero, y, _bin("multiply", chx, sy, p), p)
+        else:
+            a = ir.Where(zero, chx, _bin("multiply", chx, cy, p), p)
+            b = ir.Where(zero, _bin("multiply", x, y, p), _bin("multiply", shx, sy, p), p)
+        if op == "sin":   # -i (a + i b) = (b, -a)
+            return ("c", b, _un("negative", a, p))
+        return ("c", a, b)
+
+    def _tanh(self, re, im, p) -> Val:
+        # npy_ctanh (FreeBSD s_ctanh.c, Kahan's algorithm) for finite values:
+        #   |x| >= 22: (copysign(1, x), 4 sin y cos y exp(-2|x|))
+        #   else t = tan y, beta = 1 + t^2, s = sinh x, rho = sqrt(1 + s^2),
+        #        denom = 1 + beta s^2: (beta rho s / denom, t / denom)
+        x, y = re, im
+        one = _const(1, p)
+        t = _un("tan", y, p)
+        beta = _bin("add", one, _bin("multiply", t, t, p), p)
+        sx = _un("sinh", x, p)
+        s2 = _bin("multiply", sx, sx, p)
+        rho = _un("sqrt", _bin("add", one, s2, p), p)
+        denom = _bin("add", one, _bin("multiply", beta, s2, p), p)
+        a = _bin("divide", _bin("multiply", _bin("multiply", beta, rho, p), sx, p), denom, p)
+        b = _bin("divide", t, denom, p)
+        big = _bin("greater_equal", _un("abs", x, p), _const(22, p), np.bool_)
+        e = _un("exp", _bin("multiply", _const(-2, p), _un("abs", x, p), p), p)
+        bb = _bin("multiply", _bin("multiply", _const(4, p), _bin("multiply", _un("sin", y, p),
+                                                                  _un("cos", y, p), p), p), e, p)
+        return ("c", ir.Where(big, _bin("copysign", one, x, p), a, p), ir.Where(big, bb, b, p))
+
+    def _pow(self, ar, ai, br, bi, p) -> Val:
+        # z ** w = exp(w log z) (npy_cpow's general branch); w = 0 -> 1 + 0i,
+        # z = 0 with real w > 0 -> 0 + 0i.  numpy multiplies small integer
+        # powers out instead: the results agree to a few ulps (tested bound)
+        lr = _un("log", _bin("hypot", ar, ai, p), p)
+        li = _bin("atan2", ai, ar, p)
+        _, er, ei = self._mul(br, bi, lr, li, p)
+        r = _un("exp", er, p)
+        cr = _bin("multiply", r, _un("cos", ei, p), p)
+        ci = _bin("multiply", r, _un("sin", ei, p), p)
+        zero_w = _bin("logical_and", _bin("equal", br, _const(0, p), np.bool_),
+                      _bin("equal", bi, _const(0, p), np.bool_), np.bool_)
+        zero_z = _bin("logical_and",
+                      _bin("logical_and", _bin("equal", ar, _const(0, p), np.bool_),
+                           _bin("equal", ai, _const(0, p), np.bool_), np.bool_),
+                      _bin("logical_and", _bin("greater", br, _const(0, p), np.bool_),
+                           _bin("equal", bi, _const(0, p), np.bool_), np.bool_), np.bool_)
+        re = ir.Where(zero_w, _const(1, p), ir.Where(zero_z, _const(0, p), cr, p), p)
+        im = ir.Where(zero_w, _const(0, p), ir.Where(zero_z, _const(0, p), ci, p), p)
+        return ("c", re, im)
 
     def _sqrt(self, re, im, p) -> Val:
         # npy_csqrt (principal branch): t = sqrt((|re| + |z|) / 2);
@@ -272,6 +347,8 @@ class _Splitter:
             return self._mul(ar, ai, br, bi, p)
         if op == "divide":
             return self._div(ar, ai, br, bi, p)
+        if op == "pow":
+            return self._pow(ar, ai, br, bi, p)
         if op == "equal":
             return ("r", _bin("logical_and", _bin("equal", ar, br, np.bool_), _bin("equal", ai, bi, np.bool_),
                               np.bool_))

@@ -54,7 +54,11 @@ class GemmChain:
 def _is_ksum(p, src_leaf_ok) -> Optional[ir.ReduceField]:
     """The program if it is ``sum over the k axis`` of one input (the
     ``_chunk_sum`` of linear_algebra_functions.py:77-78, with or without a
-    merge region and a squeeze), else None."""
+    merge region and a squeeze), else None.  A complex k-sum split into its
+    parts (rewrites.split_complex: fields ``v#re`` / ``v#im`` over the
+    input's real / imag slabs, output {real, imag}) counts too."""
+    if isinstance(p, ir.ExprProgram) and p.reduce is not None and p.structured:
+        return _is_split_complex_ksum(p, src_leaf_ok)
     if not isinstance(p, ir.ExprProgram) or p.reduce is None or p.structured:
         return None
     if tuple(p.reduce.axes) != (K_AXIS,) or p.ndim != 3 or len(p.reduce.fields) != 1:
@@ -67,6 +71,26 @@ def _is_ksum(p, src_leaf_ok) -> Optional[ir.ReduceField]:
     if np.dtype(p.outputs.dtype) != np.dtype(f.dtype) or np.dtype(f.expr.dtype) != np.dtype(f.dtype):
         return None
     return f
+
+
+def _is_split_complex_ksum(p, src_leaf_ok):
+    if tuple(p.reduce.axes) != (K_AXIS,) or p.ndim != 3 or len(p.reduce.fields) != 2:
+        return None
+    re, im = p.reduce.fields
+    if not (re.name.endswith("#re") and im.name == re.name[:-3] + "#im"):
+        return None
+    for f, part in ((re, "real"), (im, "imag")):
+        if f.rop != "sum" or not src_leaf_ok(f.expr) or getattr(f.expr, "field", None) != part:
+            return None
+        if np.dtype(f.expr.dtype) != np.dtype(f.dtype):
+            return None
+    outs = dict(p.outputs)
+    if set(outs) != {"real", "imag"}:
+        return None
+    if not all(isinstance(outs[k], ir.Field) and outs[k].name == f.name
+               for k, f in (("real", re), ("imag", im))):
+        return None
+    return re
 
 
 def find_gemm_chains(dag, array_names) -> Dict[str, GemmChain]:
@@ -167,3 +191,91 @@ def chain_tables(ex, chain: GemmChain, keys):
             ktot += ak
         tasks[t] = (F.chunk_addr(key), m, n, n, t * nk, nk, ktot, 0)
     return tasks, segs[:si], in_dt, F.dtype
+
+
+def complex_chain_tables(ex, chain: GemmChain, keys):
+    """Complex matmul as real chained GEMMs over the part slabs
+    (cubed_amd/complex.py's SoA layout): for every output chunk two tasks,
+
+        C.real = sum_k Ar_k Br_k + sum_k Ai_k (-Bi_k)
+        C.imag = sum_k Ar_k Bi_k + sum_k Ai_k Br_k
+
+    each one K loop over 2 nk segments, so the four real products of
+    numpy's complex dot (linear_algebra_functions.py:62-64 on complex
+    chunks) run on the f32 MFMA kernel (complex64) or the f64 element kernel
+    (complex128).  -Bi is one negated copy of B's imaginary slab per chunk
+    (a map launch, returned in ``pre``).  Returns (pre launches, tasks,
+    segs, part dtype, part dtype)."""
+    from types import SimpleNamespace
+
+    from . import _native as nat
+    from .complex import is_complex, part_dtype
+    from .lowering import LoweringError
+    from .primitive.types import CubedArrayProxy
+
+    F = chain.final_target
+    G = chain.gemm_target
+    nk = G.numblocks[K_AXIS]
+    pdt = part_dtype(F.dtype)
+    negs = {}
+    pre = []
+
+    def neg_imag(B):
+        """Device array holding -B.imag (same chunk grid), made once."""
+        if id(B) in negs:
+            return negs[id(B)]
+        T = DeviceArray(B.shape, part_dtype(B.dtype), B.chunks, name=f"{B.name}-negimag")
+        ex.own(T)
+        ex.allocate(T)
+        axes = tuple(range(B.ndim))
+        prog = ir.ExprProgram(ndim=B.ndim, nargs=1,
+                              outputs=ir.Unary("negative", ir.Arg(0, np.dtype(T.dtype), axes, "imag"),
+                                               np.dtype(T.dtype)),
+                              out_axes=axes, name="neg_imag")
+        cfg = SimpleNamespace(block_function=lambda out_key, _n=B.name: [(_n,) + tuple(out_key[1:])],
+                              reads_map={B.name: CubedArrayProxy(B, B.chunks)})
+        import itertools
+
+        tkeys = list(itertools.product(*[range(n) for n in B.numblocks]))
+        from .runtime.executors.gpu import _with_gathers
+
+        pre.extend(_with_gathers(ex.lowerer.lower_expr_pipeline(prog, cfg, T, tkeys), ex.device))
+        negs[id(B)] = T
+        return T
+
+    tasks = np.zeros(2 * len(keys), dtype=nat.CHAIN_DTYPE)
+    segs = np.zeros(2 * len(keys) * 2 * nk, dtype=nat.SEG_DTYPE)
+    si = 0
+    for t, key in enumerate(keys):
+        i, j = key[0], key[-1]
+        m, n = F.chunk_extent(key)[0], F.chunk_extent(key)[-1]
+        pairs = []
+        for k in range(nk):
+            args = chain.gemm_spec.block_function(("out", i, k, j))
+            a_key, b_key = args[0], args[1]
+            A = ex.device_source(chain.gemm_spec.reads_map[a_key[0]].array)
+            B = ex.device_source(chain.gemm_spec.reads_map[b_key[0]].array)
+            if A.ndim != 2 or B.ndim != 2:
+                raise LoweringError("chained GEMM needs 2-d operands")
+            if not (is_complex(A.dtype) and is_complex(B.dtype) and A.dtype == B.dtype == F.dtype):
+                raise LoweringError(f"matmul of {A.dtype} x {B.dtype} -> {F.dtype} is not lowered "
+                                    "(complex operands of the output's dtype)")
+            am, ak = A.chunk_extent(a_key[1:])
+            bk, bn = B.chunk_extent(b_key[1:])
+            if ak != bk or am != m or bn != n:
+                raise LoweringError("operand chunks do not match the output chunk")
+            pairs.append((A, a_key[1:], B, b_key[1:], ak))
+        for part in ("real", "imag"):
+            seg0, ktot = si, 0
+            for A, ac, B, bc, kk in pairs:  # Ar x (Br | Bi)
+                b = B.chunk_addr(bc, "real" if part == "real" else "imag")
+                segs[si] = (A.chunk_addr(ac, "real"), b, kk, kk, B.chunk_extent(bc)[1], 0)
+                si += 1
+                ktot += kk
+            for A, ac, B, bc, kk in pairs:  # Ai x (-Bi | Br)
+                b = neg_imag(B).chunk_addr(bc) if part == "real" else B.chunk_addr(bc, "real")
+                segs[si] = (A.chunk_addr(ac, "imag"), b, kk, kk, B.chunk_extent(bc)[1], 0)
+                si += 1
+                ktot += kk
+            tasks[2 * t + (part == "imag")] = (F.chunk_addr(key, part), m, n, n, seg0, 2 * nk, ktot, 0)
+    return pre, tasks, segs[:si], pdt, pdt

@@ -773,6 +773,14 @@ class GpuDagExecutor(DagExecutor):
         self.allocate(F)
         keys = self._task_keys(F)
         out = []
+        if F.dtype.kind == "c":
+            from ...gemm_chains import complex_chain_tables
+
+            if self.world > 1:
+                raise LoweringError("complex matmul runs on one GPU")
+            pre, tasks, segs, in_dt, out_dt = complex_chain_tables(self, chain, keys)
+            return pre + [GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
+                                     self.zero_page())]
         if self.world > 1:
             def reads(k):
                 G = chain.gemm_target

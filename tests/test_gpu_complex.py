@@ -146,6 +146,50 @@ def test_sum_and_nansum(ex, dtype):
     assert np.allclose(got, exp, rtol=1e-6 if dtype == "complex64" else 1e-12, equal_nan=True)
 
 
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_complex_matmul(ex, dtype):
+    """Complex matmul as chained real GEMMs over the part slabs
+    (gemm_chains.complex_chain_tables; complex64 on the f32 MFMA kernel,
+    complex128 on the f64 element kernel), ragged chunks, against numpy's
+    complex128 product; bound 8 sqrt(2K) eps sum|x||y| per part."""
+    X = cdata((150, 128), dtype, 9, specials=False)
+    Y = cdata((128, 172), dtype, 10, specials=False)
+    spec = mkspec(ex)
+    got = xp.matmul(cubed.from_array(X, chunks=(64, 48), spec=spec),
+                    cubed.from_array(Y, chunks=(48, 80), spec=spec)).compute()
+    assert got.dtype == np.dtype(dtype)
+    exp = X.astype(np.complex128) @ Y.astype(np.complex128)
+    scale = np.abs(X).astype(np.float64) @ np.abs(Y).astype(np.float64)
+    bound = 8 * np.sqrt(2 * 128) * np.finfo(np.dtype(dtype)).eps * scale
+    assert np.all(np.abs(got.real - exp.real) <= bound)
+    assert np.all(np.abs(got.imag - exp.imag) <= bound)
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_trigonometric_hyperbolic_and_pow(ex, dtype):
+    """sin/cos/tan/sinh/cosh/tanh of complex values (npymath's finite-value
+    formulas) and complex powers (exp(w log z)) against numpy, finite
+    inputs incl. a zero imaginary part and |re| > 22 for tanh; bound: 64 ulps
+    of the modulus of the inputs' magnitudes (pow: of |z ** w|)."""
+    Z = cdata((6, 7), dtype, 11, specials=False) * 2
+    Z.reshape(-1)[0] = complex(1.5, 0)
+    Z.reshape(-1)[1] = complex(-30, 0.7)
+    Z.reshape(-1)[2] = complex(25, -1.2)
+    W = cdata((6, 7), dtype, 12, specials=False) * 0.5
+    W.reshape(-1)[3] = 0
+    spec = mkspec(ex)
+    z = cubed.from_array(Z, chunks=(3, 4), spec=spec)
+    w = cubed.from_array(W, chunks=(3, 4), spec=spec)
+    with np.errstate(all="ignore"):
+        for name in ("sin", "cos", "tan", "sinh", "cosh", "tanh"):
+            got = getattr(xp, name)(z).compute()
+            exp = getattr(np, name)(Z)
+            close(got, exp, dtype, ulps=64, scale=np.maximum(np.abs(exp), 1.0))
+        got = xp.pow(z, w).compute()
+        exp = np.power(Z, W)
+        close(got, exp, dtype, ulps=64, scale=np.maximum(np.abs(exp), 1e-30))
+
+
 def test_unsupported_complex_ops_raise(ex):
     Z = cdata((4, 4), "complex128", 8, specials=False)
     spec = mkspec(ex)
@@ -153,4 +197,4 @@ def test_unsupported_complex_ops_raise(ex):
     from cubed_amd.lowering import LoweringError
 
     with pytest.raises(LoweringError, match="complex"):
-        xp.sin(z).compute()
+        xp.asin(z).compute()

@@ -586,3 +586,43 @@ def test_two_random_streams_split(built, dry):
     assert all(k.count(philox) <= 1 for k in kinds), kinds
     # a map launch whose only leaf is a random stream (the materialised part)
     assert any(l.prog.nfields == 0 and k == [philox] for l, k in zip(fused, kinds))
+
+
+def test_complex_matmul_is_two_real_chains_per_output_chunk(built, dry):
+    """complex64 matmul: one negation launch (-B.imag) and ONE chained GEMM
+    launch whose tasks are (real, imag) pairs per output chunk, each a K loop
+    over 2 nk segments on the f32 part slabs (gemm_chains.complex_chain_tables)."""
+    from cubed_amd.lowering import GemmLaunch
+
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    x = (np.arange(64 * 48).reshape(64, 48) % 7 + 1j).astype(np.complex64)
+    a = cubed.from_array(x, chunks=(32, 16), spec=spec)
+    b = cubed.from_array(x.T.copy(), chunks=(16, 32), spec=spec)
+    arrays_to_plan(a, b).execute(executor=dry, array_names=[a.name, b.name])
+    m = xp.matmul(a, b)
+    dry.launched.clear()
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    fused = _fused(dry)
+    gl = [l for l in dry.launched if isinstance(l, GemmLaunch)]
+    assert len(gl) == 1 and len(fused) == 1
+    assert fused[0].prog.nfields == 0  # the -B.imag map
+    L = gl[0]
+    assert L.in_code == L.out_code == 9  # f32 parts
+    M = m.zarray
+    assert L.n == 2 * M.nchunks
+    A, B = a.zarray, b.zarray
+    nk = A.numblocks[1]
+    for t in range(M.nchunks):
+        re, im = L.tasks[2 * t], L.tasks[2 * t + 1]
+        assert re["nseg"] == im["nseg"] == 2 * nk and re["ktot"] == im["ktot"] == 2 * 48
+        key = (t // M.numblocks[1], t % M.numblocks[1])
+        assert re["c"] == M.chunk_addr(key, "real") and im["c"] == M.chunk_addr(key, "imag")
+        sr = L.segs[re["seg0"]:re["seg0"] + 2 * nk]
+        si = L.segs[im["seg0"]:im["seg0"] + 2 * nk]
+        for k in range(nk):
+            assert sr[k]["a"] == A.chunk_addr((key[0], k), "real") == si[k]["a"]
+            assert sr[k]["b"] == B.chunk_addr((k, key[1]), "real")
+            assert si[k]["b"] == B.chunk_addr((k, key[1]), "imag")
+            assert sr[nk + k]["a"] == A.chunk_addr((key[0], k), "imag") == si[nk + k]["a"]
+            assert si[nk + k]["b"] == B.chunk_addr((k, key[1]), "real")
+            assert sr[nk + k]["b"] not in (B.chunk_addr((k, key[1]), "real"), B.chunk_addr((k, key[1]), "imag"))
