@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 9  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 10  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -167,6 +167,9 @@ def lib():
     L.cubed_blosc_max_compressed.restype = c_int64
     L.cubed_blosc_compress.argtypes = [c_void_p, c_int64, c_int, c_int, c_void_p, c_int64]
     L.cubed_blosc_compress.restype = c_int64
+    for fn in (L.cubed_zstd_decompress, L.cubed_lz4_chunk_decompress):
+        fn.argtypes = [c_void_p, c_int64, c_void_p, c_int64]
+        fn.restype = c_int
     L.cubed_abi_version.restype = c_int
     L.cubed_last_error.restype = c_char_p
     L.cubed_device_count.restype = c_int
@@ -189,7 +192,7 @@ EXPORTED_SYMBOLS = (
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
     "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
-    "cubed_blosc_compress", "cubed_gemm_chain", "cubed_gemm_chain_path",
+    "cubed_blosc_compress", "cubed_zstd_decompress", "cubed_lz4_chunk_decompress", "cubed_gemm_chain", "cubed_gemm_chain_path",
 )
 
 

@@ -18,15 +18,22 @@
 //   Byte shuffle transposes each block as a (blocksize/typesize, typesize)
 //   byte matrix; the trailing blocksize % typesize bytes stay in place.
 //
-// Decoding supports lz4 and zlib streams with byte or no shuffle (what
-// zarr's defaults and the zlib codec write); the encoder writes lz4 with
-// byte shuffle and unsplit blocks (flag 0x10), which every Blosc >= 1.x
-// decoder reads.  Plain C ABI (include/cubed_amd.h); no GPU code.
+// Decoding supports lz4, zlib and zstd streams with byte or no shuffle
+// (what zarr's defaults, the zlib codec and Blosc(cname="zstd") write); zstd
+// streams go to the system's libzstd (dlopen'ed on first use: it is the
+// reference implementation of the zstd format, only the Blosc container is
+// restated here).  blosclz / snappy streams and bit shuffle are refused.
+// The encoder writes lz4 with byte shuffle and unsplit blocks (flag 0x10),
+// which every Blosc >= 1.x decoder reads.  Also the standalone numcodecs
+// "zstd" (one zstd frame) and "lz4" (a 4-byte size + one LZ4 block) chunks.
+// Plain C ABI (include/cubed_amd.h); no GPU code.
 
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include "cubed_amd.h"
@@ -179,6 +186,32 @@ void lz4_encode(const uint8_t* src, int64_t n, std::vector<uint8_t>& out) {
     put_seq(out, src + anchor, n - anchor, 0, 0);
 }
 
+// ---------------------------------------------------------------- zstd (libzstd)
+
+typedef size_t (*zstd_decompress_fn)(void*, size_t, const void*, size_t);
+typedef unsigned (*zstd_is_error_fn)(size_t);
+zstd_decompress_fn g_zstd_decompress = nullptr;
+zstd_is_error_fn g_zstd_is_error = nullptr;
+
+bool load_zstd() {
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        g_zstd_decompress = (zstd_decompress_fn)dlsym(h, "ZSTD_decompress");
+        g_zstd_is_error = (zstd_is_error_fn)dlsym(h, "ZSTD_isError");
+        if (!g_zstd_decompress || !g_zstd_is_error) g_zstd_decompress = nullptr;
+    });
+    return g_zstd_decompress != nullptr;
+}
+
+int zstd_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t size) {
+    if (!load_zstd()) return CUBED_E_UNSUPPORTED;
+    const size_t r = g_zstd_decompress(dst, size_t(size), src, size_t(n));
+    if (g_zstd_is_error(r) || int64_t(r) != size) return CUBED_E_CODEC;
+    return 0;
+}
+
 // ---------------------------------------------------------------- Blosc frame
 
 int decode_stream(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, int64_t size) {
@@ -192,6 +225,7 @@ int decode_stream(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, in
         if (uncompress(dst, &got, src, uLong(csize)) != Z_OK || int64_t(got) != size) return CUBED_E_CODEC;
         return 0;
     }
+    if (codec == 4) return zstd_decode(src, csize, dst, size);
     return CUBED_E_UNSUPPORTED;
 }
 
@@ -251,6 +285,19 @@ int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t d
         if (shuffled) byte_unshuffle(tmp.data(), d + b * blocksize, bsize, ts);
     }
     return 0;
+}
+
+int cubed_zstd_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen) {
+    if (!src || !dst || srclen < 0 || dstlen < 0) return CUBED_E_ARG;
+    return zstd_decode(static_cast<const uint8_t*>(src), srclen, static_cast<uint8_t*>(dst), dstlen);
+}
+
+int cubed_lz4_chunk_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen) {
+    // numcodecs LZ4: little-endian int32 uncompressed size, then one LZ4 block
+    if (!src || !dst || srclen < 4 || dstlen < 0) return CUBED_E_ARG;
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    if (int64_t(rd32(s)) != dstlen) return CUBED_E_CODEC;
+    return lz4_decode(s + 4, srclen - 4, static_cast<uint8_t*>(dst), dstlen) == dstlen ? 0 : CUBED_E_CODEC;
 }
 
 int64_t cubed_blosc_max_compressed(int64_t nbytes) { return nbytes + kHeader + 64; }

@@ -396,7 +396,7 @@ constexpr int HF_BM = 256, HF_BN = 256;
 // [256 rows][BK k] (BK*4-byte rows, CPR = BK/4 16-B chunks, chunk c of row
 // r at position c ^ swz(r): conflict-free b128 reads) + B [BK k][256 n]
 // (1 KiB rows, as in HBM).
-template <int BK, int NS>
+template <int BK, int NS, bool PP = false>
 __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
                                                         int64_t tiles_m, int64_t tiles_n,
@@ -518,6 +518,51 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
   int rd = 0, wr_slot = D % NS;
+  if constexpr (PP) {
+    // Ping-pong (the bf16 kernel's schedule): wave rows 0-1 (w < 4) and 2-3
+    // run one barrier apart, alternating a memory slot M(p) -- step p's 12
+    // fragment reads into registers, step p+D's staging loads, the wait for
+    // step p+1 -- and a compute slot C(p) of 64 MFMAs, so on every SIMD one
+    // wave's MFMAs cover the other's LDS reads.  RAW / WAR as in
+    // k_gemm_bf16_chain (same ring).
+    const int half = w >> 2;
+    if (nst > 0) wait_step(0);
+    __builtin_amdgcn_s_barrier();
+    if (half == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 af[G][2], bq[G][4];
+    for (int64_t p = 0; p < nst; ++p) {
+      const CUBED_L char* bufc = lds + rd * STAGE;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) af[g][rb] = *(const CUBED_L f32x4*)(bufc + offA[rb][g]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[g][j] = *(const CUBED_L f32x4*)(bufc + offB + (8 * g + j) * 1024);
+      }
+      if (p + D < nst) stage((p + D) * BK, lds + wr_slot * STAGE);
+      rd = rd + 1 == NS ? 0 : rd + 1;
+      wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (p + 1 < nst) wait_step(p + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              acc[rb][q] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g][rb][j], bq[g][j][q], acc[rb][q], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (half == 0) __builtin_amdgcn_s_barrier();  // same barrier count in both halves
+  } else
   for (int64_t p = 0; p < nst; ++p) {
     // this wave's step p landed; then every wave's (barrier), and every wave
     // finished reading step p-1's slot (restaged below)

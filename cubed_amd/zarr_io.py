@@ -8,8 +8,10 @@ this module restates the Zarr v2 directory-store format itself: ``.zarray``
 JSON metadata, one file per chunk named ``"i.j.k"`` (or ``"i/j/k"``), every
 chunk stored at the full chunk shape (edge chunks padded with the fill
 value), missing chunks read as the fill value.  Chunk codecs: none, ``zlib``
-and ``gzip`` (Python's zlib), ``blosc`` (native, cubed_amd/csrc/codec.cpp:
-lz4/zlib streams, byte or no shuffle).
+and ``gzip`` (Python's zlib), ``lzma`` and ``bz2`` (Python's), ``blosc``
+(native, cubed_amd/csrc/codec.cpp: lz4 / zlib / zstd streams, byte or no
+shuffle), ``zstd`` and ``lz4`` (native; zstd through the system libzstd).
+Writes use blosc-lz4 (or zlib / gzip when asked for).
 
 Data path: intermediates never touch Zarr (they stay in HBM); a Zarr source
 is decoded on host threads into pinned staging buffers and copied into the
@@ -32,6 +34,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 DEFAULT_COMPRESSOR = {"id": "blosc", "cname": "lz4", "clevel": 5, "shuffle": 1, "blocksize": 0}
+DECODABLE = ("blosc", "zlib", "gzip", "zstd", "lz4", "lzma", "bz2")
 _IO_THREADS = min(16, os.cpu_count() or 4)
 
 
@@ -92,7 +95,7 @@ class ZarrV2Array:
             raise ValueError(f"{path}: only Zarr format 2 is supported")
         if meta.get("filters"):
             raise NotImplementedError(f"{path}: Zarr filters {meta['filters']} are not supported")
-        if self.compressor is not None and self.compressor.get("id") not in ("blosc", "zlib", "gzip"):
+        if self.compressor is not None and self.compressor.get("id") not in DECODABLE:
             raise NotImplementedError(f"{path}: compressor {self.compressor.get('id')!r} is not supported")
 
     # -- construction ------------------------------------------------------------
@@ -112,6 +115,9 @@ class ZarrV2Array:
         chunks = tuple(int(c) for c in chunks) if shape else ()
         if compressor == "default":
             compressor = dict(DEFAULT_COMPRESSOR)
+        if compressor is not None and compressor.get("id") not in ("blosc", "zlib", "gzip"):
+            raise NotImplementedError(f"writing {compressor.get('id')!r} chunks (this build writes "
+                                      "blosc-lz4, zlib, gzip; it reads zstd, lz4, lzma, bz2 too)")
         if compressor is not None and compressor.get("id") == "blosc":
             # the native encoder writes lz4 streams (byte shuffle unless 0)
             compressor = dict(DEFAULT_COMPRESSOR, shuffle=1 if compressor.get("shuffle", 1) else 0)
@@ -194,6 +200,17 @@ class ZarrV2Array:
             _blosc_decompress(data, flat)
         elif comp["id"] == "zlib":
             raw = np.frombuffer(zlib.decompress(data), dtype=np.uint8)
+        elif comp["id"] in ("zstd", "lz4"):
+            raw = None
+            _native_decompress(comp["id"], data, flat)
+        elif comp["id"] == "lzma":
+            import lzma
+
+            raw = np.frombuffer(lzma.decompress(data), dtype=np.uint8)
+        elif comp["id"] == "bz2":
+            import bz2
+
+            raw = np.frombuffer(bz2.decompress(data), dtype=np.uint8)
         else:
             raw = np.frombuffer(gzip.decompress(data), dtype=np.uint8)
         if raw is not None:
@@ -223,7 +240,9 @@ class ZarrV2Array:
             return _blosc_compress(buf, self.dtype.itemsize, comp.get("shuffle", 1))
         if comp["id"] == "zlib":
             return zlib.compress(buf.tobytes(), comp.get("level", 1))
-        return gzip.compress(buf.tobytes(), comp.get("level", 1), mtime=0)
+        if comp["id"] == "gzip":
+            return gzip.compress(buf.tobytes(), comp.get("level", 1), mtime=0)
+        raise NotImplementedError(f"writing {comp['id']!r} chunks (this build writes blosc-lz4, zlib, gzip)")
 
     def write_chunk(self, coords, value: np.ndarray):
         """Write one chunk (its in-array extent; edge chunks are padded to the
@@ -295,9 +314,21 @@ def _blosc_decompress(data: bytes, out_u8: np.ndarray):
     L = nat.lib()
     rc = L.cubed_blosc_decompress(data, len(data), out_u8.ctypes.data, out_u8.size)
     if rc != 0:
-        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec/shuffle (only lz4/zlib, byte shuffle)",
+        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec/shuffle (lz4/zlib/zstd with byte or no shuffle; "
+                                                 "blosclz, snappy and bit shuffle are not decoded)",
                 -1: "size mismatch"}.get(rc, f"error {rc}")
         raise ValueError(f"blosc decode failed: {what}")
+
+
+def _native_decompress(kind: str, data: bytes, out_u8: np.ndarray):
+    from . import _native as nat
+
+    L = nat.lib()
+    fn = L.cubed_zstd_decompress if kind == "zstd" else L.cubed_lz4_chunk_decompress
+    rc = fn(data, len(data), out_u8.ctypes.data, out_u8.size)
+    if rc != 0:
+        what = {-6: "malformed or wrong-size chunk", -7: "libzstd.so.1 is not available"}.get(rc, f"error {rc}")
+        raise ValueError(f"{kind} decode failed: {what}")
 
 
 def _blosc_compress(buf_u8: np.ndarray, typesize: int, shuffle: int) -> bytes:

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 9
+#define CUBED_ABI_VERSION 10
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -373,6 +373,12 @@ int cubed_blosc_header(const void* src, int64_t srclen, int64_t* nbytes, int64_t
                        int* typesize, int* flags);
 int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen);
 int64_t cubed_blosc_max_compressed(int64_t nbytes);
+/* Standalone numcodecs chunk codecs (zarr compressor ids "zstd" and "lz4"):
+ * one zstd frame (decoded by the system libzstd, loaded on first use;
+ * CUBED_E_UNSUPPORTED when it is absent) / a little-endian int32 size + one
+ * LZ4 block.  dst must hold exactly the decoded size. */
+int cubed_zstd_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen);
+int cubed_lz4_chunk_decompress(const void* src, int64_t srclen, void* dst, int64_t dstlen);
 int64_t cubed_blosc_compress(const void* src, int64_t nbytes, int typesize, int shuffle, void* dst,
                              int64_t dstcap);
 

@@ -276,10 +276,73 @@ def test_zarr_metadata_and_missing_chunks(tmp_path, built):
 def test_zarr_refuses_what_it_cannot_decode(tmp_path, built):
     os.makedirs(tmp_path / "q.zarr")
     meta = {"zarr_format": 2, "shape": [4], "chunks": [4], "dtype": "<f8", "fill_value": 0.0,
-            "order": "C", "filters": None, "compressor": {"id": "zstd", "level": 1}}
+            "order": "C", "filters": None, "compressor": {"id": "snappy"}}
     json.dump(meta, open(tmp_path / "q.zarr" / ".zarray", "w"))
-    with pytest.raises(NotImplementedError, match="zstd"):
+    with pytest.raises(NotImplementedError, match="snappy"):
         Z.open_array(str(tmp_path / "q.zarr"))
+    # blosclz streams inside a blosc frame: refused with a clear error
+    data = patterned(4096)
+    fr = bytearray(frame(data, 4, 4096, 3, True, True, lambda b: zlib.compress(b, 5)))
+    fr[2] = (fr[2] & 0x1F) | (0 << 5)  # codec 0 = blosclz (the streams are compressed)
+    with pytest.raises(ValueError, match="blosclz"):
+        native_decode(bytes(fr), len(data))
+
+
+def _zstd():
+    import ctypes
+
+    try:
+        z = ctypes.CDLL("libzstd.so.1")
+    except OSError:
+        pytest.skip("libzstd.so.1 not available")
+    z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+
+    def compress(b: bytes, level=3) -> bytes:
+        cap = z.ZSTD_compressBound(len(b))
+        out = ctypes.create_string_buffer(cap)
+        n = z.ZSTD_compress(out, cap, b, len(b), level)
+        assert n < cap
+        return out.raw[:n]
+    return compress
+
+
+@pytest.mark.parametrize("ts, bsize, shuf, dont_split", [(4, 4096, True, False), (8, 2048, False, True)])
+def test_decoder_reads_zstd_blosc_frames(built, ts, bsize, shuf, dont_split):
+    """Blosc(cname="zstd"): codec 4 streams, decoded by the system libzstd
+    (zstd frames here are written by the same library's ZSTD_compress)."""
+    zc = _zstd()
+    data = patterned(4 * 2500 + 3)
+    fr = frame(data, ts, bsize, 4, shuf, dont_split, zc)
+    assert native_decode(fr, len(data)) == data
+
+
+def test_zarr_reads_zstd_lz4_lzma_bz2_chunks(tmp_path, built):
+    """Standalone numcodecs compressors: "zstd" (one zstd frame), "lz4" (int32
+    size + one LZ4 block), "lzma" and "bz2" (Python's codecs)."""
+    import bz2
+    import lzma
+
+    zc = _zstd()
+    x = np.arange(24, dtype=np.float64).reshape(4, 6) * 1.5
+    encs = {"zstd": zc, "lz4": lambda b: struct.pack("<i", len(b)) + lz4_literals(b),
+            "lzma": lzma.compress, "bz2": bz2.compress}
+    for cid, enc in encs.items():
+        d = tmp_path / f"{cid}.zarr"
+        os.makedirs(d)
+        meta = {"zarr_format": 2, "shape": [4, 6], "chunks": [2, 3], "dtype": "<f8", "fill_value": 0.0,
+                "order": "C", "filters": None, "compressor": {"id": cid}}
+        json.dump(meta, open(d / ".zarray", "w"))
+        for i in range(2):
+            for j in range(2):
+                blk = np.ascontiguousarray(x[2 * i:2 * i + 2, 3 * j:3 * j + 3])
+                open(d / f"{i}.{j}", "wb").write(enc(blk.tobytes()))
+        a = Z.open_array(str(d))
+        assert np.array_equal(a[...], x), cid
+        with pytest.raises(NotImplementedError, match="writing"):
+            Z.ZarrV2Array.create(str(tmp_path / f"w{cid}.zarr"), (4,), np.float64, (2,), compressor={"id": cid})
 
 
 def test_zarr_overwrite_removes_nested_chunks(tmp_path, built):

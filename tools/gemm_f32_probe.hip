@@ -79,10 +79,10 @@ int main(int argc, char** argv) {
   struct V { const char* name; kfn f; bool check; };
   V vs[] = {
       {"BK16 NS4 (library)", k_gemm_f32_chain<16, 4>, false},
-      {"BK32 NS2", k_gemm_f32_chain<32, 2>, true},
-      {"BK16 NS3", k_gemm_f32_chain<16, 3>, true},
+      {"BK16 NS4 ping-pong", k_gemm_f32_chain<16, 4, true>, true},
+      {"BK16 NS3 ping-pong", k_gemm_f32_chain<16, 3, true>, true},
       {"BK16 NS4 (again)", k_gemm_f32_chain<16, 4>, true},
-      {"BK32 NS2 (again)", k_gemm_f32_chain<32, 2>, true},
+      {"BK16 NS4 ping-pong (again)", k_gemm_f32_chain<16, 4, true>, true},
   };
   for (const V& v : vs) {
     float best = 1e30f;
