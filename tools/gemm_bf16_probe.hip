@@ -100,11 +100,10 @@ int main(int argc, char** argv) {
 
   struct V { const char* name; kfn f; bool check; int threads = 0; bool bt = false; };
   V vs[] = {
-      {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, true>, false},
-      {"ping-pong, A in 128-B lines", k_gemm_bf16_a64<false>, true},
-      {"ping-pong, B^T b128 reads", k_gemm_bf16_bt<false>, true, 0, true},
-      {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, true>, true},
-      {"ping-pong, A in 128-B lines (again)", k_gemm_bf16_a64<false>, true},
+      {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, 1>, false},
+      {"ping-pong, staging in C slot", k_gemm_bf16_chain<false, 0, 2>, true},
+      {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, 1>, true},
+      {"ping-pong, staging in C (again)", k_gemm_bf16_chain<false, 0, 2>, true},
   };
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
   for (const V& v : vs) {
