@@ -1,19 +1,27 @@
-"""Reference point for the chunk GEMM (development tool): torch.bmm fp32
-(hipBLASLt / rocBLAS inside torch) on the shape of tools/gemm_probe.py,
-8 x 5000^3 f32 products, TF32 off."""
+"""Vendor reference point for the chained GEMM (development tool):
+torch.matmul (hipBLASLt / rocBLAS inside PyTorch) on BASELINE config 5's
+operands as ONE unchunked 40000^2 x 40000^2 product, f32 (TF32 off; gfx950
+has no xf32 anyway) and bf16, uniform [-1, 1) data, best of 3 after a
+warm-up.  The chained kernel does the same flops on 5000^2 chunk slots
+(64 output chunks x 8 segments); this times the library on a plain
+contiguous problem of the same size."""
 import torch
 
-n, T = 5000, 8
-A = torch.rand(T, n, n, device="cuda") - 0.5
-B = torch.rand(T, n, n, device="cuda") - 0.5
+n = 40000
 torch.backends.cuda.matmul.allow_tf32 = False
-C = torch.bmm(A, B)
-torch.cuda.synchronize()
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(3):
-    C = torch.bmm(A, B)
-e1.record()
-torch.cuda.synchronize()
-ms = e0.elapsed_time(e1) / 3
-print(f"torch.bmm fp32: {ms:.2f} ms {2 * T * n ** 3 / ms / 1e9:.1f} TF")
+for dt in (torch.float32, torch.bfloat16):
+    A = (torch.rand(n, n, device="cuda", dtype=torch.float32) * 2 - 1).to(dt)
+    B = (torch.rand(n, n, device="cuda", dtype=torch.float32) * 2 - 1).to(dt)
+    C = torch.matmul(A, B)
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        C = torch.matmul(A, B)
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1))
+    print(f"torch.matmul {str(dt).split('.')[-1]} {n}^3: {best:.2f} ms {2 * n ** 3 / best / 1e9:.1f} TF", flush=True)
+    del A, B, C
+    torch.cuda.empty_cache()
