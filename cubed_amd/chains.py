@@ -53,6 +53,8 @@ COMPOSE = {
     ("max", "max"): "max", ("min", "min"): "min", ("prod", "prod"): "prod",
     ("nanmax", "nanmax"): "nanmax", ("nanmin", "nanmin"): "nanmin",
     ("nanprod", "nanprod"): "nanprod", ("any", "any"): "any", ("all", "all"): "all",
+    ("argmax", "argmax"): "argmax", ("argmin", "argmin"): "argmin", ("cprod", "cprod"): "cprod",
+    ("pair_index", "pair_index"): "pair_index", ("pair_imag", "pair_imag"): "pair_imag",
 }
 
 

@@ -141,6 +141,36 @@ _mean_aggregate = _MeanAggregate()
 _nanmean_aggregate = _MeanAggregate()
 
 
+class ArgReduction(ChunkReduction):
+    """``_arg_func`` + ``_arg_combine`` (core/ops.py:1124-1145): the reference
+    keeps {i, v} per block and picks, with argmax/argmin, the pair whose value
+    wins.  Here the {v, i} pairs are reduced by the pair op ``argmax`` /
+    ``argmin`` (first NaN, else the larger / smaller value, ties to the
+    smaller index -- numpy's choice, independent of the combine order), so the
+    per-chunk pass and every combine round are the same program."""
+
+    structured = True
+
+    def __init__(self, arg_func: str):
+        self.rop = arg_func
+        self.name = f"_arg_combine[{arg_func}]"
+
+    def fields(self, in_dtype, kwargs):
+        return [("v", self.rop, in_dtype["v"], "v"), ("i", "pair_index", np.dtype(np.int64), "i")]
+
+
+class _ArgAggregate(ChunkMap):
+    name = "_arg_aggregate"
+
+    def program(self, ndim, in_dtype, out_dtype=None):
+        axes = tuple(range(ndim))
+        return ir.ExprProgram(ndim=ndim, nargs=1, outputs=ir.Arg(0, np.dtype(np.int64), axes, field="i"),
+                              out_axes=axes, name=self.name)
+
+
+_arg_aggregate = _ArgAggregate()
+
+
 def as_chunk_reduction(func) -> Optional[ChunkReduction]:
     """Map a user-supplied reduction callable to a ChunkReduction."""
     if isinstance(func, functools.partial):

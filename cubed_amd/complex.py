@@ -12,13 +12,14 @@ over real expressions (``split_program``): a complex leaf becomes its two
 part leaves, complex arithmetic becomes the real formulas numpy evaluates
 (npymath's nc_sum/nc_diff/nc_prod and Smith's division, hypot for abs), a
 complex output becomes the structured output {real, imag}, and a complex
-reduction field becomes one field per part.  Layout copies (rechunk, index,
-concat) move each part slab.
+reduction field becomes one field per part (a sum: two independent sums; a
+product: the pair reduction cprod, whose {re, im} accumulators multiply as
+complex numbers).  Layout copies (rechunk, index, concat) move each part slab.
 
 Powers (exp(w log z)), sin / cos / tan and their hyperbolic forms (the
 FreeBSD / npymath formulas numpy uses for finite values) are rewritten too.
 Ops with no real-pair form here (inverse trigonometric functions, ordering
-comparisons, prod over complex values) raise LoweringError.
+comparisons) raise LoweringError.
 """
 
 from __future__ import annotations
@@ -392,16 +393,26 @@ def split_program(p: ir.ExprProgram) -> ir.ExprProgram:
                     raise _err(f"a complex value reduced into the real field {f.name}")
                 fields.append(dataclasses.replace(f, expr=v[1]))
                 continue
-            if f.rop not in ("sum", "nansum"):
-                raise _err(f"{f.rop} of complex values is not lowered (sum/nansum are)")
+            if f.rop not in ("sum", "nansum", "prod", "nanprod"):
+                raise _err(f"{f.rop} of complex values is not lowered (sum/nansum/prod/nanprod are)")
             pt = part_dtype(f.dtype)
             re, im = s.pair(f.expr, pt)
             rop = f.rop
-            if rop == "nansum":
-                # numpy's nansum drops an element whose real OR imaginary part is NaN
+            if rop in ("nansum", "nanprod"):
+                # numpy's nan-reductions replace an element whose real OR
+                # imaginary part is NaN by the identity (0 / 1 + 0j)
                 nan = _bin("logical_or", _un("isnan", re, np.bool_), _un("isnan", im, np.bool_), np.bool_)
-                re, im = ir.Where(nan, _const(0, pt), re, pt), ir.Where(nan, _const(0, pt), im, pt)
-                rop = "sum"
+                one = 0 if rop == "nansum" else 1
+                re, im = ir.Where(nan, _const(one, pt), re, pt), ir.Where(nan, _const(0, pt), im, pt)
+                rop = "sum" if rop == "nansum" else "prod"
+            if rop == "prod":
+                # one pair reduction: the {re, im} accumulators multiply as
+                # complex numbers (cubed_rop CPROD / PAIR_IMAG)
+                if len(reduce.fields) != 1:
+                    raise _err("a complex product shares its reduction with another field")
+                fields.append(ir.ReduceField(f.name + "#re", "cprod", re, pt))
+                fields.append(ir.ReduceField(f.name + "#im", "pair_imag", im, pt))
+                continue
             fields.append(ir.ReduceField(f.name + "#re", rop, re, pt))
             fields.append(ir.ReduceField(f.name + "#im", rop, im, pt))
         reduce = dataclasses.replace(reduce, fields=tuple(fields))

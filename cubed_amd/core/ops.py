@@ -829,22 +829,35 @@ def squeeze(x, /, axis):
 
 
 def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
-    """argmax / argmin along one axis (core/ops.py:1093-1153).
+    """argmax / argmin along one axis or over the whole array
+    (core/ops.py:1093-1153).
 
-    The reference maps every block to a structured {i, v} pair with
-    take_along_axis and reduces the pairs.  The VM's accumulators are one
-    8-byte value per field, so the same result is produced as two fused
-    reductions over x: the max (min) along the axis, then the smallest index
-    whose element equals it -- where(x == m, index, INT64_MAX) reduced with
-    min.  NaN follows numpy: a NaN anywhere makes m NaN and the first NaN's
-    index is returned (isnan(x) & isnan(m) counts as equal).  Ties give the
-    first index, as numpy's argmax/argmin."""
+    The reference's first map (_arg_map_func) turns each block into {i, v}
+    with the block-offset index, then ``reduction`` combines the pairs with
+    _arg_combine.  Here every ELEMENT is a {v, i} pair -- its value key and
+    its global index (the flat C-order index when axis is None, which the
+    reference gets from reshape) -- built inside the reduce kernel's program
+    and reduced in one fused pass with the pair op argmax / argmin
+    (chunkfuncs.ArgReduction): the first NaN wins, else the larger (smaller)
+    value, ties to the smaller index, as numpy.  Value keys: floats as f64
+    (exact), bool / ints as int64, uint64 with the sign bit flipped
+    (order-preserving)."""
     from ..array_api import creation_functions as cf
-    from ..array_api import elementwise_functions as ef
     from ..array_api import manipulation_functions as mf
-    from ..array_api import searching_functions as sf
-    from ..array_api import statistical_functions as stf
-    from ..array_api.data_type_functions import astype
+    from ..array_api import elementwise_functions as ef
+    from ..chunkfuncs import ArgReduction, _arg_aggregate
+
+    if x.ndim == 0:
+        x = mf.expand_dims(x, axis=0)
+        axis, keepdims = 0, False
+    if axis is not None:
+        axis = validate_axis(axis, x.ndim)
+        if isinstance(axis, tuple):
+            if len(axis) != 1:
+                raise ValueError("argmax/argmin take a single axis")
+            axis = axis[0]
+    if (x.size if axis is None else x.shape[axis]) == 0:
+        raise ValueError(f"attempt to get {arg_func} of an empty sequence")
 
     def index_along(d):
         """The index along dim d, broadcastable against x."""
@@ -854,77 +867,37 @@ def arg_reduction(x, /, arg_func, axis=None, *, keepdims=False):
                 idx = mf.expand_dims(idx, axis=e)
         return idx
 
-    def flat_index():
-        flat = None
+    if axis is None and x.ndim > 1:
+        idx = None
         for d in range(x.ndim):
             stride = int(np.prod(x.shape[d + 1:], dtype=np.int64))
             term = ef.multiply(index_along(d), cf.asarray(np.int64(stride), spec=x.spec))
-            flat = term if flat is None else ef.add(flat, term)
-        return flat
-
-    if axis is not None:
-        axis = validate_axis(axis, x.ndim)
-        if isinstance(axis, tuple):
-            if len(axis) != 1:
-                raise ValueError("argmax/argmin take a single axis")
-            axis = axis[0]
-    vbits = _packed_key_bits(x.dtype)
-    n_index = x.size if axis is None else x.shape[axis]
-    if vbits is not None and x.ndim > 0 and n_index <= (1 << (53 - vbits)):
-        # one pass over x: max of (value key << ibits | reversed index), exact
-        # in f64 / int64 (< 2^53); ties keep the smallest index, NaN wins
-        ibits = 53 - vbits
-        if axis is None and x.ndim > 1:
-            target_axis, idx = None, flat_index()
-        else:
-            target_axis, idx = (0 if axis is None else axis), index_along(0 if axis is None else axis)
-        if x.dtype.kind == "f" or x.dtype == ir.bfloat16:
-            key = elemwise("ordkey_max" if arg_func == "argmax" else "ordkey_min", x, dtype=np.float64)
-            low = cf.asarray(np.float64((1 << ibits) - 1), spec=x.spec)
-            scale = cf.asarray(np.float64(1 << ibits), spec=x.spec)
-            idx = astype(idx, np.float64)  # exact: < 2^53
-        else:
-            key = astype(x, np.int64)
-            if x.dtype.kind == "i":
-                key = ef.add(key, cf.asarray(np.int64(1 << (vbits - 1)), spec=x.spec))
-            if arg_func == "argmin":
-                key = ef.subtract(cf.asarray(np.int64((1 << vbits) - 1), spec=x.spec), key)
-            low = cf.asarray(np.int64((1 << ibits) - 1), spec=x.spec)
-            scale = cf.asarray(np.int64(1 << ibits), spec=x.spec)
-        packed = ef.add(ef.multiply(key, scale), ef.subtract(low, idx))
-        m = stf.max(packed, axis=target_axis, keepdims=keepdims)
-        return astype(ef.subtract(low, ef.remainder(m, scale)), np.int64)
-
-    reduce_max = stf.max if arg_func == "argmax" else stf.min
-    if axis is None and x.ndim > 1:
-        # the reference flattens with reshape (argmax(x) on an n-d array);
-        # here the flat C-order index is built from the per-dim indexes
-        m = reduce_max(x, keepdims=True)
-        target_axis, idx = None, flat_index()
+            idx = term if idx is None else ef.add(idx, term)
+        red_axis = None
     else:
-        if axis is None:
-            axis = 0
-        m = reduce_max(x, axis=axis, keepdims=True)
-        target_axis, idx = axis, index_along(axis)
-    eq = ef.equal(x, m)
-    if x.dtype.kind == "f":
-        eq = ef.logical_or(eq, ef.logical_and(ef.isnan(x), ef.isnan(m)))
-    big = cf.asarray(np.int64(np.iinfo(np.int64).max), spec=x.spec)
-    cand = sf.where(eq, idx, big)
-    return stf.min(cand, axis=target_axis, keepdims=keepdims)
+        red_axis = 0 if axis is None else axis
+        idx = index_along(red_axis)
 
-
-def _packed_key_bits(dtype):
-    """Bits of the order-preserving value key of ``dtype`` for the one-pass
-    argmax/argmin (None: no packed form; 64-bit values take two passes)."""
-    dt = np.dtype(dtype)
-    if dt.kind == "b":
-        return 1
-    if dt.kind in "iu" and dt.itemsize <= 4:
-        return 8 * dt.itemsize
-    if dt in (np.dtype(np.float32), np.dtype(np.float16), ir.bfloat16):
-        return 32  # keyed through the value's f32 bit pattern
-    return None
+    dt = np.dtype(x.dtype)
+    n = x.ndim
+    v = ir.Arg(0, dt, tuple(range(n)))
+    if ir.is_float(dt):
+        vdt = np.dtype(np.float64)
+        key = ir.cast(v, vdt)
+    else:
+        vdt = np.dtype(np.int64)
+        key = ir.cast(v, vdt)
+        if dt == np.uint64:
+            key = ir.Binary("bitwise_xor", key, ir.Const(np.int64(np.iinfo(np.int64).min), vdt), vdt)
+    intermediate = [("v", vdt), ("i", np.int64)]
+    prog = ir.ExprProgram(ndim=n, nargs=2,
+                          outputs=(("v", key), ("i", ir.Arg(1, np.dtype(np.int64), tuple(range(n))))),
+                          out_axes=tuple(range(n)), name=f"{arg_func}_pairs")
+    inds = tuple(range(n))[::-1]
+    pairs = blockwise(prog, inds, x, inds, idx, inds, dtype=intermediate)
+    r = ArgReduction(arg_func)
+    return reduction(pairs, r, combine_func=r, aggegrate_func=_arg_aggregate, axis=red_axis,
+                     intermediate_dtype=intermediate, dtype=np.int64, keepdims=keepdims)
 
 
 def unify_chunks(*args: "Array", **kwargs):

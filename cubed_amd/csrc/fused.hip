@@ -256,6 +256,17 @@ int check_program(const cubed_program_t& P) {
     set_err("cubed_fused_chunks: program header out of range");
     return CUBED_E_ARG;
   }
+  for (int f = 0; f < P.nfields; ++f) {
+    const int rop = P.field_rop[f];
+    const bool partner = rop == CUBED_R_PAIR_INDEX || rop == CUBED_R_PAIR_IMAG;
+    const bool pair_ok = f == 0 ? (!pair_rop(rop) || (P.nfields == 2 &&
+                                   P.field_rop[1] == (rop == CUBED_R_CPROD ? CUBED_R_PAIR_IMAG : CUBED_R_PAIR_INDEX)))
+                                : (partner == pair_rop(P.field_rop[0]));
+    if (rop < CUBED_R_SUM || rop > CUBED_R_PAIR_IMAG || (f == 0 && partner) || !pair_ok) {
+      set_err("cubed_fused_chunks: bad reduction op (pair ops need their partner as field 1)");
+      return CUBED_E_ARG;
+    }
+  }
   if ((P.mode & CUBED_MODE_PARTIALS) && P.nfields == 0) { set_err("cubed_fused_chunks: partials mode needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & 3) == 1 && P.nfields == 0) { set_err("cubed_fused_chunks: kernel B needs a reduction"); return CUBED_E_ARG; }
   if ((P.mode & CUBED_MODE_STREAM) &&

@@ -27,16 +27,11 @@ CUBED_DEV void divmod64(int64_t a, int64_t b, int64_t& q, int64_t& r) {
 template <typename V, int VEC>
 CUBED_DEV void accumulate(Acc (&acc)[CUBED_MAX_FIELDS][VEC], Regs<V, VEC>& regs,
                           const cubed_program_t& P) {
+  V src[CUBED_MAX_FIELDS][VEC];
 #pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    if (f < P.nfields) {
-      V src[VEC];
-      fetch(regs, P.field_src[f], src);
-      const int rop = P.field_rop[f], ai = P.field_acc[f];
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
-    }
-  }
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    if (f < P.nfields) fetch(regs, P.field_src[f], src[f]);
+  fields_add<V, VEC>(acc, src, P);
 }
 
 // Epilogue + store of VEC reduced elements.

@@ -286,13 +286,20 @@ CUBED_DEV void fused_b_body(
   // combine VEC lanes, then the 64-wide wave, then the 4 waves
   Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    a[f] = acc[f][0];
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc[f][0];
 #pragma unroll
-    for (int j = 1; j < VEC; ++j) a[f] = acc_combine(a[f], acc[f][j], P.field_rop[f], P.field_acc[f]);
+  for (int j = 1; j < VEC; ++j) {
+    Acc b[CUBED_MAX_FIELDS];
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) b[f] = acc[f][j];
+    fields_combine(a, b, P);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    Acc b[CUBED_MAX_FIELDS];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) b[f] = shfl_xor_acc(a[f], m);
+    fields_combine(a, b, P);
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
@@ -301,14 +308,14 @@ CUBED_DEV void fused_b_body(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    Acc x[CUBED_MAX_FIELDS];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) x[f] = red[0][f];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) fields_combine(x, red[w], P);
     Acc fin[CUBED_MAX_FIELDS][1];
 #pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-      Acc x = red[0][f];
-#pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
-      fin[f][0] = x;
-    }
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) fin[f][0] = x[f];
     if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
       finish<1>(P, T, fin, ooff);
     } else {
@@ -317,6 +324,15 @@ CUBED_DEV void fused_b_body(
       for (int f = 0; f < CUBED_MAX_FIELDS; ++f) if (f < P.nfields) w[f] = fin[f][0];
     }
   }
+}
+
+// The fields of element i of a SoA partial block (field stride n); fields
+// past P.nfields hold the identity.
+CUBED_DEV void soa_load(const cubed_program_t& P, const Acc* __restrict__ soa, int64_t n, int64_t i,
+                        Acc (&x)[CUBED_MAX_FIELDS]) {
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    x[f] = f < P.nfields ? soa[f * n + i] : acc_init(P.field_rop[f], P.field_acc[f]);
 }
 
 // ---------------------------------------------------------------- finalize
@@ -342,15 +358,15 @@ CUBED_DEV void fold_splits_of(const cubed_program_t& P, const Acc* __restrict__ 
       for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
         if (f < nf) v[u][f] = p[(int64_t)(s + u) * sstride + f];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-        if (f < nf) x[f] = acc_combine(x[f], v[u][f], P.field_rop[f], P.field_acc[f]);
+    for (int u = 0; u < 8; ++u) fields_combine(x, v[u], P);
   }
-  for (; s < nsplit; ++s)
+  for (; s < nsplit; ++s) {
+    Acc v[CUBED_MAX_FIELDS];
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-      if (f < nf) x[f] = acc_combine(x[f], p[(int64_t)s * sstride + f], P.field_rop[f], P.field_acc[f]);
+      if (f < nf) v[f] = p[(int64_t)s * sstride + f];
+    fields_combine(x, v, P);
+  }
 }
 
 CUBED_DEV void finalize_body(
@@ -453,14 +469,16 @@ CUBED_DEV void finish_groups_body(
     for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] += c * T->out_stride[o][d];
   }
   const int64_t n = ntasks * max_kept;
-  Acc fin[CUBED_MAX_FIELDS][1];
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    if (f >= P.nfields) { fin[f][0] = acc_init(CUBED_R_NONE, 0); continue; }
-    Acc x = soa[f * n + t0 * max_kept + k];
-    for (int64_t t = t0 + 1; t < t1; ++t)
-      x = acc_combine(x, soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
-    fin[f][0] = x;
+  Acc x[CUBED_MAX_FIELDS];
+  soa_load(P, soa, n, t0 * max_kept + k, x);
+  for (int64_t t = t0 + 1; t < t1; ++t) {
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, soa, n, t * max_kept + k, y);
+    fields_combine(x, y, P);
   }
+  Acc fin[CUBED_MAX_FIELDS][1];
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) fin[f][0] = x[f];
   finish<1>(P, T, fin, ooff);
 }
 
@@ -480,15 +498,19 @@ CUBED_DEV void combine_groups_body(
   int64_t nk = 1;
   for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
   const int64_t n = ntasks * max_kept, no = ngroups * max_kept_out;
-  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-    Acc x = acc_init(P.field_rop[f], P.field_acc[f]);
-    if (k < nk) {
-      x = soa[f * n + t0 * max_kept + k];
-      for (int64_t t = t0 + 1; t < t1; ++t)
-        x = acc_combine(x, soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+  Acc x[CUBED_MAX_FIELDS];
+  if (k < nk) {
+    soa_load(P, soa, n, t0 * max_kept + k, x);
+    for (int64_t t = t0 + 1; t < t1; ++t) {
+      Acc y[CUBED_MAX_FIELDS];
+      soa_load(P, soa, n, t * max_kept + k, y);
+      fields_combine(x, y, P);
     }
-    out[f * no + i] = x;
+  } else {
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) x[f] = acc_init(P.field_rop[f], P.field_acc[f]);
   }
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * no + i] = x[f];
 }
 
 // Workgroup fold of per-thread accumulators (64-wide shuffle tree, then the
@@ -497,10 +519,12 @@ CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIE
                                 Acc (&red)[kBlock / 64][CUBED_MAX_FIELDS], Acc* __restrict__ out,
                                 int64_t stride, int64_t idx) {
 #pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+  for (int m = 32; m >= 1; m >>= 1) {
+    Acc b[CUBED_MAX_FIELDS];
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-      a[f] = acc_combine(a[f], shfl_xor_acc(a[f], m), P.field_rop[f], P.field_acc[f]);
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) b[f] = shfl_xor_acc(a[f], m);
+    fields_combine(a, b, P);
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
 #pragma unroll
@@ -508,11 +532,11 @@ CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIE
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-      Acc x = red[0][f];
-      for (int w = 1; w < kBlock / 64; ++w) x = acc_combine(x, red[w][f], P.field_rop[f], P.field_acc[f]);
-      out[f * stride + idx] = x;
-    }
+    Acc x[CUBED_MAX_FIELDS];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) x[f] = red[0][f];
+    for (int w = 1; w < kBlock / 64; ++w) fields_combine(x, red[w], P);
+    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * stride + idx] = x[f];
   }
 }
 
@@ -537,10 +561,9 @@ CUBED_DEV void fold_groups_body(
     int64_t nk = 1;
     for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
     for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-        if (f < P.nfields)
-          a[f] = acc_combine(a[f], soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+      Acc y[CUBED_MAX_FIELDS];
+      soa_load(P, soa, n, t * max_kept + k, y);
+      fields_combine(a, y, P);
     }
   }
   block_fold_store(P, a, red, out, ngroups, g);
@@ -567,10 +590,9 @@ CUBED_DEV void fold_groups_split_body(
     int64_t nk = 1;
     for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
     for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-        if (f < P.nfields)
-          a[f] = acc_combine(a[f], soa[f * n + t * max_kept + k], P.field_rop[f], P.field_acc[f]);
+      Acc y[CUBED_MAX_FIELDS];
+      soa_load(P, soa, n, t * max_kept + k, y);
+      fields_combine(a, y, P);
     }
   }
   block_fold_store(P, a, red, out_split, ngroups * nsplit, b);
@@ -586,10 +608,9 @@ CUBED_DEV void fold_splits_body(const cubed_program_t& P, const Acc* __restrict_
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
   for (int64_t s = threadIdx.x; s < nsplit; s += kBlock) {
-#pragma unroll
-    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-      if (f < P.nfields)
-        a[f] = acc_combine(a[f], in_split[f * ns + g * nsplit + s], P.field_rop[f], P.field_acc[f]);
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, in_split, ns, g * nsplit + s, y);
+    fields_combine(a, y, P);
   }
   block_fold_store(P, a, red, out, ngroups, g);
 }
@@ -602,12 +623,14 @@ CUBED_DEV void combine_parts_body(const cubed_program_t& P, const Acc* __restric
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const int64_t block = (int64_t)P.nfields * n;
-  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) {
-    Acc x = parts[f * n + i];
-    for (int r = 1; r < nparts; ++r)
-      x = acc_combine(x, parts[r * block + f * n + i], P.field_rop[f], P.field_acc[f]);
-    out[f * n + i] = x;
+  Acc x[CUBED_MAX_FIELDS];
+  soa_load(P, parts, n, i, x);
+  for (int r = 1; r < nparts; ++r) {
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, parts + r * block, n, i, y);
+    fields_combine(x, y, P);
   }
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * n + i] = x[f];
 }
 
 // ---------------------------------------------------------------- streaming fast path
@@ -686,16 +709,11 @@ CUBED_DEV void set_leaves(Regs<V, 4>& regs, const V (&b)[NL][4]) {
 template <typename V>
 CUBED_DEV void accumulate_nocount(Acc (&acc)[CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
                                   const cubed_program_t& P) {
+  V src[CUBED_MAX_FIELDS][4];
 #pragma unroll
-  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-    if (f < P.nfields && P.field_rop[f] != CUBED_R_COUNT) {
-      V src[4];
-      fetch(regs, P.field_src[f], src);
-      const int rop = P.field_rop[f], ai = P.field_acc[f];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc_add<V>(acc[f][j], rop, ai, src[j]);
-    }
-  }
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    if (f < P.nfields) fetch(regs, P.field_src[f], src[f]);
+  fields_add<V, 4, true>(acc, src, P);
 }
 
 // Rows [lo, hi) of W kept VEC groups (group j at element offset go[j], pair

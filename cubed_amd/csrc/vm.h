@@ -77,18 +77,6 @@ CUBED_DEV V cast_val(V x, int t, int s) {
   }
 }
 
-// Order-preserving key of an f32 value in [0, 2^32 - 1]: larger value ->
-// larger key (reversed when `rev`), -0 and +0 equal, every NaN the largest
-// key in both orders (numpy's argmax/argmin return the first NaN).
-CUBED_DEV uint32_t ordkey32(float f, bool rev) {
-  if (f != f) return 0xffffffffu;
-  if (f == 0.f) f = 0.f;
-  uint32_t b = __float_as_uint(f);
-  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-  // non-NaN keys are <= 0xff800000 (+inf), so the reversed order stays below NaN's
-  return rev ? 0xfffffffeu - b : b;
-}
-
 template <typename V, int VEC>
 CUBED_DEV void unary(int op, V (&X)[VEC]) {
   if constexpr (is_same_v<V, int64_t>) {
@@ -140,8 +128,6 @@ CUBED_DEV void unary(int op, V (&X)[VEC]) {
       case CUBED_OP_ATANH: CUBED_EACH(atanh(x)); break;
       case CUBED_OP_EXP2: CUBED_EACH(exp2(x)); break;
       case CUBED_OP_SIGNBIT: CUBED_EACH((V)(signbit(x) ? 1 : 0)); break;
-      case CUBED_OP_ORDKEY_MAX: CUBED_EACH((V)ordkey32((float)x, false)); break;
-      case CUBED_OP_ORDKEY_MIN: CUBED_EACH((V)ordkey32((float)x, true)); break;
       default: break;
     }
   }
@@ -313,9 +299,54 @@ CUBED_DEV Acc acc_init(int rop, int acc_i) {
     case CUBED_R_PROD: case CUBED_R_NANPROD: if (acc_i) a.i = 1; else a.f = 1.0; break;
     case CUBED_R_ALL: a.i = 1; break;
     case CUBED_R_SUM: case CUBED_R_NANSUM: if (acc_i) a.i = 0; else a.f = -0.0; break;
+    // pairs: {value, index} starts at the weakest value with no index, so
+    // any element (even -inf / INT64_MIN) takes its place; {re, im} at 1 + 0j
+    case CUBED_R_ARGMAX: if (acc_i) a.i = INT64_MIN; else a.f = -__builtin_inf(); break;
+    case CUBED_R_ARGMIN: if (acc_i) a.i = INT64_MAX; else a.f = __builtin_inf(); break;
+    case CUBED_R_PAIR_INDEX: a.i = INT64_MAX; break;
+    case CUBED_R_CPROD: a.f = 1.0; break;
+    case CUBED_R_PAIR_IMAG: a.f = 0.0; break;
     default: a.i = 0; break;
   }
   return a;
+}
+
+// ---- pair reductions: field 0 leads, field 1 is its partner
+// argmax/argmin {value, index}: numpy's rule -- the first NaN wins, else the
+// larger (smaller) value, ties to the smaller index (an order-free choice,
+// so every combine tree gives the same pair).  cprod {re, im}: the complex
+// product (ar*br - ai*bi, ar*bi + ai*br), unfused like npymath's nc_prod.
+__host__ __device__ inline bool pair_rop(int rop) { return rop == CUBED_R_ARGMAX || rop == CUBED_R_ARGMIN || rop == CUBED_R_CPROD; }
+
+CUBED_DEV void pair_combine(Acc& a0, Acc& a1, Acc b0, Acc b1, int rop, int acc_i) {
+  if (rop == CUBED_R_CPROD) {
+#pragma clang fp contract(off)
+    const double re = a0.f * b0.f - a1.f * b1.f;
+    const double im = a0.f * b1.f + a1.f * b0.f;
+    a0.f = re; a1.f = im;
+    return;
+  }
+  const bool mx = rop == CUBED_R_ARGMAX;
+  bool take;
+  if (acc_i) {
+    take = (mx ? b0.i > a0.i : b0.i < a0.i) || (b0.i == a0.i && b1.i < a1.i);
+  } else {
+    const bool an = a0.f != a0.f, bn = b0.f != b0.f;
+    take = an ? (bn && b1.i < a1.i)
+              : (bn || (mx ? b0.f > a0.f : b0.f < a0.f) || (b0.f == a0.f && b1.i < a1.i));
+  }
+  if (take) { a0 = b0; a1 = b1; }
+}
+
+template <typename V>
+CUBED_DEV void pair_add(Acc& a0, Acc& a1, int rop, int acc_i, V v0, V v1) {
+  Acc b0, b1;
+  if (rop == CUBED_R_CPROD) { b0.f = (double)v0; b1.f = (double)v1; }
+  else {
+    if (acc_i) b0.i = to_i64(v0); else b0.f = (double)v0;
+    b1.i = to_i64(v1);
+  }
+  pair_combine(a0, a1, b0, b1, rop, acc_i);
 }
 
 // fold one value into an accumulator
@@ -376,6 +407,40 @@ CUBED_DEV Acc shfl_xor_acc(Acc a, int m) {
   Acc r;
   r.i = __shfl_xor((long long)a.i, m, 64);
   return r;
+}
+
+// x (+)= y over all fields of P (a pair program combines its two fields as
+// one; its partner rop leaves acc_combine a no-op)
+CUBED_DEV void fields_combine(Acc (&x)[CUBED_MAX_FIELDS], const Acc (&y)[CUBED_MAX_FIELDS],
+                              const cubed_program_t& P) {
+  if (pair_rop(P.field_rop[0])) {
+    pair_combine(x[0], x[1], y[0], y[1], P.field_rop[0], P.field_acc[0]);
+    return;
+  }
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+    if (f < P.nfields) x[f] = acc_combine(x[f], y[f], P.field_rop[f], P.field_acc[f]);
+}
+
+// fold the field values src[f][j] of VEC elements into acc[f][j]; SKIP_COUNT:
+// the streaming kernel adds CUBED_R_COUNT fields once per run instead
+template <typename V, int VEC, bool SKIP_COUNT = false>
+CUBED_DEV void fields_add(Acc (&acc)[CUBED_MAX_FIELDS][VEC], const V (&src)[CUBED_MAX_FIELDS][VEC],
+                          const cubed_program_t& P) {
+  if (pair_rop(P.field_rop[0])) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j)
+      pair_add<V>(acc[0][j], acc[1][j], P.field_rop[0], P.field_acc[0], src[0][j], src[1][j]);
+    return;
+  }
+#pragma unroll
+  for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+    if (f < P.nfields && !(SKIP_COUNT && P.field_rop[f] == CUBED_R_COUNT)) {
+      const int rop = P.field_rop[f], ai = P.field_acc[f];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc_add<V>(acc[f][j], rop, ai, src[f][j]);
+    }
+  }
 }
 
 }  // namespace cubed

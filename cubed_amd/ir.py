@@ -105,8 +105,6 @@ UNARY_OPS = {
     "log1p": 37, "expm1": 38, "log2": 39, "log10": 40, "sinh": 41, "cosh": 42,
     "asin": 43, "acos": 44, "atan": 45, "asinh": 46, "acosh": 47, "atanh": 48,
     "exp2": 49, "signbit": 50, "positive": None,
-    # internal (argmax/argmin packed keys): f64 result, float inputs only
-    "ordkey_max": 51, "ordkey_min": 52,
 }
 BINARY_OPS = {
     "add": 64, "subtract": 65, "multiply": 66, "divide": 67, "floor_divide": 68,
@@ -126,7 +124,11 @@ COMPLEX_PARTS_OPS = {"conj", "real", "imag"}
 
 # reduction ops (enum cubed_rop)
 ROPS = {"sum": 1, "nansum": 2, "count": 3, "count_nonnan": 4, "max": 5, "min": 6,
-        "prod": 7, "nanmax": 8, "nanmin": 9, "any": 10, "all": 11, "nanprod": 12}
+        "prod": 7, "nanmax": 8, "nanmin": 9, "any": 10, "all": 11, "nanprod": 12,
+        # pair reductions: field 0 = the lead, field 1 = its partner
+        # (include/cubed_amd.h cubed_rop)
+        "argmax": 13, "argmin": 14, "cprod": 15, "pair_index": 16, "pair_imag": 17}
+PAIR_PARTNER = {"argmax": "pair_index", "argmin": "pair_index", "cprod": "pair_imag"}
 
 
 # ----------------------------------------------------------------- expressions
@@ -762,8 +764,10 @@ def reduction_result_dtype(rop: str, dtype, requested=None) -> np.dtype:
 
 def acc_is_int(rop: str, dtype) -> bool:
     dtype = np.dtype(dtype)
-    if rop in ("count", "count_nonnan", "any", "all"):
+    if rop in ("count", "count_nonnan", "any", "all", "pair_index"):
         return True
+    if rop in ("cprod", "pair_imag"):
+        return False
     return dtype.kind in "iub"
 
 

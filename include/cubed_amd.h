@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 10
+#define CUBED_ABI_VERSION 11
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -91,11 +91,17 @@ enum cubed_leaf_kind {
                          /* global index along an axis (arange/eye/tril)    */
 };
 
-/* reduction ops of a field; accumulators are f64 or i64 (acc_type) */
+/* reduction ops of a field; accumulators are f64 or i64 (acc_type).  The
+ * pair ops couple field 0 (the lead, one of ARGMAX/ARGMIN/CPROD) with field 1
+ * (its partner, PAIR_INDEX / PAIR_IMAG): argmax/argmin reduce {value, index}
+ * pairs (core/ops.py:1093-1153 _arg_func/_arg_combine), cprod the {re, im}
+ * parts of a complex product (np.prod of complex chunks).  A program holding
+ * a pair has exactly these two fields. */
 enum cubed_rop {
   CUBED_R_NONE = 0, CUBED_R_SUM, CUBED_R_NANSUM, CUBED_R_COUNT,
   CUBED_R_COUNT_NONNAN, CUBED_R_MAX, CUBED_R_MIN, CUBED_R_PROD,
-  CUBED_R_NANMAX, CUBED_R_NANMIN, CUBED_R_ANY, CUBED_R_ALL, CUBED_R_NANPROD
+  CUBED_R_NANMAX, CUBED_R_NANMIN, CUBED_R_ANY, CUBED_R_ALL, CUBED_R_NANPROD,
+  CUBED_R_ARGMAX, CUBED_R_ARGMIN, CUBED_R_CPROD, CUBED_R_PAIR_INDEX, CUBED_R_PAIR_IMAG
 };
 
 /* VM opcodes (two-address: r[a] = op(r[a], r[b]); where: r[a] = r[c] ? r[a] : r[b]) */
@@ -114,10 +120,6 @@ enum cubed_op {
   CUBED_OP_LOG2, CUBED_OP_LOG10, CUBED_OP_SINH, CUBED_OP_COSH, CUBED_OP_ASIN,
   CUBED_OP_ACOS, CUBED_OP_ATAN, CUBED_OP_ASINH, CUBED_OP_ACOSH,
   CUBED_OP_ATANH, CUBED_OP_EXP2, CUBED_OP_SIGNBIT,
-  /* order-preserving 32-bit key of the value rounded to f32 (argmax/argmin
-     packed keys, core/ops.py:1093-1153): NaN above +inf, -0 == +0; the
-     _MIN form reverses the order of non-NaN values */
-  CUBED_OP_ORDKEY_MAX, CUBED_OP_ORDKEY_MIN,
   /* binary */
   CUBED_OP_ADD = 64, CUBED_OP_SUB, CUBED_OP_MUL, CUBED_OP_DIV,
   CUBED_OP_FLOORDIV, CUBED_OP_MOD, CUBED_OP_POW, CUBED_OP_MAX, CUBED_OP_MIN,

@@ -147,6 +147,38 @@ def test_sum_and_nansum(ex, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_prod_and_nanprod(ex, dtype):
+    """prod / nanprod of complex chunks: one pair reduction whose {re, im}
+    accumulators multiply as complex numbers (cubed_rop CPROD), through the
+    merge + combine rounds, against numpy's complex128 product.  np.nanprod
+    through core ``reduction`` treats an element with a NaN part as 1
+    (numpy's _replace_nan)."""
+    from cubed_amd.core.ops import reduction
+
+    rng = np.random.default_rng(31)
+    Z = (rng.uniform(0.9, 1.1, (40, 30)) * np.exp(1j * rng.uniform(-np.pi, np.pi, (40, 30)))).astype(dtype)
+    Z[3, 4] = complex(np.nan, 1)
+    Z[10, 2] = complex(2, np.nan)
+    spec = mkspec(ex)
+    z = cubed.from_array(Z, chunks=(7, 9), spec=spec)
+    for axis in (0, 1, None):
+        got = xp.prod(z, axis=axis).compute()
+        exp = np.prod(Z, axis=axis, dtype=np.complex128)
+        assert got.dtype == np.complex128
+        assert np.allclose(got, exp, rtol=1e-12, atol=0, equal_nan=True), axis
+        got = reduction(z, np.nanprod, axis=axis, dtype=np.complex128,
+                        extra_func_kwargs=dict(dtype=np.complex128)).compute()
+        exp = np.nanprod(Z, axis=axis, dtype=np.complex128)
+        assert np.allclose(got, exp, rtol=1e-12, atol=0, equal_nan=True), axis
+    # many merge + combine rounds of the pair accumulators
+    small = cubed.Spec(allowed_mem=20000, executor=ex)
+    W = Z[:, :3].copy()
+    W[np.isnan(W)] = 1
+    got = xp.prod(cubed.from_array(W, chunks=(2, 3), spec=small), axis=0).compute()
+    assert np.allclose(got, np.prod(W, axis=0, dtype=np.complex128), rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
 def test_complex_matmul(ex, dtype):
     """Complex matmul as chained real GEMMs over the part slabs
     (gemm_chains.complex_chain_tables; complex64 on the f32 MFMA kernel,

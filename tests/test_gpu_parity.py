@@ -536,13 +536,14 @@ def test_arg_reductions_ties_and_nans(ex, fn):
         assert np.array_equal(got, getattr(x, fn)(axis=axis)), axis
 
 
-@pytest.mark.parametrize("dtype", ["float32", "float16", "int32", "int16", "uint32", "uint8", "bool"])
+@pytest.mark.parametrize("dtype", ["float64", "float32", "float16", "int64", "uint64", "int32", "int16",
+                                   "uint32", "uint8", "bool"])
 @pytest.mark.parametrize("fn", ["argmax", "argmin"])
-def test_arg_reductions_packed_keys(ex, fn, dtype):
-    """One-pass argmax/argmin over packed (value key, reversed index) keys for
-    <= 32-bit dtypes: bit-exact indexes vs numpy, ties -> first index, NaN ->
-    first NaN, -0 == +0, +-inf and the dtype's extreme values, over axis 0, 1,
-    None and keepdims."""
+def test_arg_reductions_pairs(ex, fn, dtype):
+    """One-pass argmax/argmin over {value, index} pairs for every dtype
+    (64-bit values included): bit-exact indexes vs numpy, ties -> first
+    index, NaN -> first NaN, -0 == +0, +-inf and the dtype's extreme values,
+    over axis 0, 1, None and keepdims."""
     rng = np.random.default_rng(23)
     dt = np.dtype(dtype)
     if dt.kind == "f":
@@ -562,6 +563,10 @@ def test_arg_reductions_packed_keys(ex, fn, dtype):
         x = rng.integers(max(info.min, -5), min(info.max, 5) + 1, (45, 39)).astype(dt)
         x[1, 2], x[44, 2] = info.max, info.min
         x[6, 9] = x[8, 9] = info.max
+        x[10, 12] = x[20, 12] = info.min
+        if dt.itemsize == 8:  # values that no f64 holds exactly
+            x[30, 14], x[31, 14] = info.max - 1, info.max
+            x[32, 15], x[33, 15] = info.min + 1, info.min
     spec = mkspec(ex)
     a = cubed.from_array(x, chunks=(7, 10), spec=spec)
     for axis in (0, 1, None):
@@ -569,6 +574,24 @@ def test_arg_reductions_packed_keys(ex, fn, dtype):
             got = np.asarray(getattr(xp, fn)(a, axis=axis, keepdims=keepdims).compute())
             exp = getattr(np, fn)(x, axis=axis, keepdims=keepdims)
             assert got.dtype == np.int64 and np.array_equal(got, exp), (axis, keepdims)
+
+
+@pytest.mark.parametrize("fn", ["argmax", "argmin"])
+def test_arg_reductions_merge_rounds_and_0d(ex, fn):
+    """Many chunks along the reduced axis under a small allowed_mem: the
+    pairs go through several merge + combine rounds (core/ops.py:849-889);
+    a 0-d array gives index 0; an empty axis raises as numpy does."""
+    rng = np.random.default_rng(5)
+    x = np.round(rng.standard_normal((400, 6)) * 3)
+    x[123, 2] = x[301, 2] = np.nan
+    spec = cubed.Spec(allowed_mem=20000, executor=ex)
+    a = cubed.from_array(x, chunks=(3, 6), spec=spec)
+    for axis in (0, None):
+        assert np.array_equal(getattr(xp, fn)(a, axis=axis).compute(), getattr(np, fn)(x, axis=axis))
+    z = xp.asarray(np.float64(4.0), spec=mkspec(ex))
+    assert int(getattr(xp, fn)(z).compute()) == 0
+    with pytest.raises(ValueError):
+        getattr(xp, fn)(xp.asarray(np.zeros((0, 3)), spec=mkspec(ex)), axis=0)
 
 
 # ----------------------------------------------------------- callbacks / resume

@@ -15,6 +15,7 @@ import cubed_amd as cubed
 import cubed_amd.array_api as xp
 import cubed_amd.random as crandom
 from cubed_amd import _native as nat
+from cubed_amd import ir
 from cubed_amd.core.plan import arrays_to_plan
 from cubed_amd.lowering import MODE_STREAM, CopyLaunch, FusedLaunch
 
@@ -626,3 +627,37 @@ def test_complex_matmul_is_two_real_chains_per_output_chunk(built, dry):
             assert sr[nk + k]["a"] == A.chunk_addr((key[0], k), "imag") == si[nk + k]["a"]
             assert si[nk + k]["b"] == B.chunk_addr((k, key[1]), "real")
             assert sr[nk + k]["b"] not in (B.chunk_addr((k, key[1]), "real"), B.chunk_addr((k, key[1]), "imag"))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int64, np.uint64, np.float32])
+def test_argmax_is_one_pair_reduction(built, dry, dtype):
+    """argmax over every dtype: ONE fused reduce launch whose program holds
+    the pair {v: argmax, i: pair_index} over x and the global index (Iota
+    leaves), value accumulator f64 for floats, i64 for ints."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    a = cubed.from_array(np.arange(60, dtype=dtype).reshape(6, 10), chunks=(2, 10), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    r = xp.argmax(a, axis=0)
+    dry.launched.clear()
+    arrays_to_plan(r).execute(executor=dry, resume=True, array_names=[r.name])
+    fused = _fused(dry)
+    assert len(fused) == 1
+    P = fused[0].prog
+    assert P.nfields == 2
+    assert (P.field_rop[0], P.field_rop[1]) == (ir.ROPS["argmax"], ir.ROPS["pair_index"])
+    assert P.field_acc[1] == 1 and P.field_acc[0] == (0 if np.dtype(dtype).kind == "f" else 1)
+
+
+def test_complex_prod_is_one_pair_reduction(built, dry):
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    z = cubed.from_array((np.arange(40) + 1j).astype(np.complex64).reshape(4, 10), chunks=(2, 5), spec=spec)
+    arrays_to_plan(z).execute(executor=dry, array_names=[z.name])
+    r = xp.prod(z, axis=0)
+    dry.launched.clear()
+    arrays_to_plan(r).execute(executor=dry, resume=True, array_names=[r.name])
+    fused = _fused(dry)
+    assert len(fused) == 1
+    P = fused[0].prog
+    assert P.nfields == 2
+    assert (P.field_rop[0], P.field_rop[1]) == (ir.ROPS["cprod"], ir.ROPS["pair_imag"])
+    assert P.field_acc[0] == P.field_acc[1] == 0

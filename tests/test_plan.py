@@ -190,15 +190,13 @@ def test_random_is_deterministic_per_seed():
     assert seed_of(a) == seed_of(b) == 0xbdd640fb06671ad11c80317fa3b1799d
 
 
-@pytest.mark.parametrize("dtype, passes", [(np.float32, 1), (np.int16, 1), (np.bool_, 1),
-                                           (np.float64, 2), (np.int64, 2)])
-def test_arg_reduction_reads_x_once_when_packed(spec, dtype, passes):
-    """argmax of a <= 32-bit dtype is one reduction over packed (value key,
-    reversed index) keys, so x has one consumer; 64-bit values keep the
-    max-then-index form, which reads x twice (core/ops.py:1093-1153 reads it
-    once through {i, v} pairs)."""
+@pytest.mark.parametrize("dtype", [np.float32, np.int16, np.bool_, np.float64, np.int64, np.uint64])
+def test_arg_reduction_reads_x_once(spec, dtype):
+    """argmax / argmin of every dtype is one pair reduction over {value key,
+    index}, so x has one consumer (core/ops.py:1093-1153 reads it once
+    through its {i, v} pairs too)."""
     a = xp.asarray(np.zeros((6, 5), dtype=dtype), chunks=(2, 5), spec=spec)
     for r in (xp.argmax(a, axis=0), xp.argmin(a), xp.argmax(a, axis=1, keepdims=True)):
         n = len(set(r.plan.dag.successors(a.name)))
-        assert n == 1 if passes == 1 else n >= 2
+        assert n == 1
         assert r.dtype == np.int64
