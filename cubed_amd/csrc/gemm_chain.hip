@@ -120,7 +120,8 @@ __device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
 // 8 = no K-loop barrier; ping-pong only: 16 = no vmcnt wait in the K loop,
 // 32 = every K step staged from step 0's addresses (L2-resident), 1 = no
 // K-loop staging.  Any nonzero value computes wrong results.
-// PP: ping-pong schedule (see the K loop).
+// PP: 0 = one barrier per step, 1 = ping-pong (the library's), 2 = ping-pong
+// with register staging (see the K loop).
 // NS: ring slots (each step p+NS-1 is staged while step p is consumed);
 // GM: tile rows per XCD tile group.
 template <bool OUT_BF16, int ABL = 0, int PP = 0, int NS = HB_NS, int GM = 4>
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
                                                          const cubed_gemm_seg_t* __restrict__ segs,
                                                          int64_t tiles_m, int64_t tiles_n,
                                                          const char* __restrict__ zero) {
-  __shared__ __attribute__((aligned(1024))) char lds_[NS * HB_STAGE];
+  __shared__ __attribute__((aligned(1024))) char lds_[(PP == 2 ? 2 : NS) * HB_STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
   tile_of<HB_BM, HB_BN, GM>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
@@ -251,8 +252,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 
   const int64_t nst = (KT + HB_BK - 1) / HB_BK;
   constexpr int D = NS - 1;  // steps staged ahead
-  // prologue: steps 0 .. D-1 in flight
-  for (int64_t p = 0; p < D && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
+  // prologue: steps 0 .. D-1 in flight (LDS-DMA schedules)
+  if constexpr (PP != 2)
+    for (int64_t p = 0; p < D && p < nst; ++p) stage(p * HB_BK, lds + p * HB_STAGE);
   // retire this wave's loads of step q (4 per step; steps up to q + D - 1 issued)
   auto wait_step = [&](int64_t q) {
     int64_t younger = nst - 1 - q;
@@ -262,61 +264,79 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
     else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  static_assert(NS >= 3 && NS <= 5, "ring of 3..5 slots");
+  static_assert(PP == 2 ? (NS >= 2 && NS <= 4) : (NS >= 3 && NS <= 5), "ring of 3..5 slots (PP 2: 2..4 register sets)");
   int rd = 0, wr_slot = D % NS;  // ring slots of steps p and p + D
   if constexpr (PP == 2) {
-    // Ping-pong with the staging loads in the COMPUTE slot: C(p) issues step
-    // p+3's four global_load_lds between its MFMAs (one per 8), where an
-    // LDS-DMA issue costs ~60 cycles instead of 100-185 beside the fragment
-    // reads (MI355X_MICROARCH.md, per-instruction constants), and M(p) only
-    // reads fragments.  WAR as PP == 1 (C(p) runs after M(p)); RAW: step
-    // p+1's loads (issued in C(p-2)) are retired at the end of M(p) with
-    // step p+2's (C(p-1)) still in flight.
-    if (nst > 0) wait_step(0);
+    // Ping-pong with REGISTER staging: global_load_dwordx4 into VGPRs, then
+    // ds_write_b128, instead of LDS-DMA (an LDS-DMA instruction costs its
+    // wave 60-185 issue cycles, MI355X_MICROARCH.md per-instruction
+    // constants).  LDS holds two slots: M(p) reads step p from slot p&1,
+    // writes step p+1 (loaded NS-1 memory slots earlier) into slot (p+1)&1
+    // and issues step p+NS's loads into the register set step p vacated.
+    // RAW: M(p)'s ds_writes retire (lgkmcnt(0)) before the barrier ending its
+    //   slot; step p+1 is read in M(p+1), which in both rows starts after
+    //   both rows' M(p) ended.
+    // WAR: slot (p+1)&1 last held step p-1, read in M(p-1), which ended in
+    //   both rows before either row's M(p) started.
+    constexpr int RD = NS;  // register sets: loads of RD steps in flight
+    u32x4 rs[RD][4];
+    int wdst[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      wdst[i] = (2 * w + i) * 1024 + lane * 16;
+      wdst[2 + i] = HB_A + (2 * w + i) * 1024 + lane * 16;
+    }
+    auto gload = [&](int64_t k0, u32x4 (&dst)[4]) {
+      stage_addrs(k0, lds);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dst[i] = *(const CUBED_G u32x4*)(uintptr_t)st_src[i];
+    };
+    auto swrite = [&](CUBED_L char* buf, const u32x4 (&src)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(CUBED_L u32x4*)(buf + wdst[i]) = src[i];
+    };
+#pragma unroll
+    for (int r = 0; r < RD; ++r)
+      if (r < nst) gload(r * HB_BK, rs[r]);
+    if (nst > 0) swrite(lds, rs[0]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (wr == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     bf16x8 af[8];
-    for (int64_t p = 0; p < nst; ++p) {
-      // ---- M(p)
-      const CUBED_L char* bufc = lds + rd * HB_STAGE;
+    for (int64_t p0 = 0; p0 < nst; p0 += RD) {
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
-        s16x4 lo, hi;
-        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(pb));
-        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(pb));
-        bf[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+      for (int r = 0; r < RD; ++r) {
+        const int64_t p = p0 + r;
+        if (p >= nst) break;
+        // ---- M(p)
+        const CUBED_L char* bufc = lds + (p & 1) * HB_STAGE;
 #pragma unroll
-      for (int mb = 0; mb < 8; ++mb) af[mb] = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
-      const bool st = p + D < nst;
-      if (st) stage_addrs((p + D) * HB_BK, lds + wr_slot * HB_STAGE);
-      rd = rd + 1 == NS ? 0 : rd + 1;
-      wr_slot = wr_slot + 1 == NS ? 0 : wr_slot + 1;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (p + 1 < nst) {
-        if (p + 2 < nst) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- C(p), with step p+3's loads between the MFMAs
-#pragma unroll
-      for (int mb = 0; mb < 8; ++mb) {
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb], bf[nb], acc[mb][nb], 0, 0, 0);
-        if (mb & 1) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (st) glds16(st_src[mb >> 1], st_dst[mb >> 1]);
-          __builtin_amdgcn_sched_barrier(0);
+        for (int nb = 0; nb < 4; ++nb) {
+          const uint32_t pb = (uint32_t)(uintptr_t)(bufc + offB[nb]);
+          s16x4 lo, hi;
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(pb));
+          asm volatile("ds_read_b64_tr_b16 %0, %1 offset:2048" : "=v"(hi) : "v"(pb));
+          bf[nb] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) af[mb] = *(const CUBED_L bf16x8*)(bufc + offA + mb * 1024);
+        if (p + 1 < nst) swrite(lds + ((p + 1) & 1) * HB_STAGE, rs[(r + 1) % RD]);
+        if (p + RD < nst) gload((p + RD) * HB_BK, rs[r]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- C(p)
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb)
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb], bf[nb], acc[mb][nb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
     }
     if (wr == 0) __builtin_amdgcn_s_barrier();  // same barrier count in both rows
   } else if constexpr (PP == 1) {

@@ -101,9 +101,11 @@ int main(int argc, char** argv) {
   struct V { const char* name; kfn f; bool check; int threads = 0; bool bt = false; };
   V vs[] = {
       {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, 1>, false},
-      {"ping-pong, staging in C slot", k_gemm_bf16_chain<false, 0, 2>, true},
+      {"ping-pong, register staging 2 sets", k_gemm_bf16_chain<false, 0, 2, 2>, true},
+      {"ping-pong, register staging 3 sets", k_gemm_bf16_chain<false, 0, 2, 3>, true},
       {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, 1>, true},
-      {"ping-pong, staging in C (again)", k_gemm_bf16_chain<false, 0, 2>, true},
+      {"ping-pong, register staging 2 sets (again)", k_gemm_bf16_chain<false, 0, 2, 2>, true},
+      {"ping-pong, register staging 3 sets (again)", k_gemm_bf16_chain<false, 0, 2, 3>, true},
   };
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
   for (const V& v : vs) {
