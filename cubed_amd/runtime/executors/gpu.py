@@ -30,6 +30,7 @@ import time
 import weakref
 from typing import Dict, List, Optional
 
+import networkx as nx
 import numpy as np
 
 from ... import _native as nat
@@ -40,6 +41,7 @@ from ...lowering import (
     ArrView,
     Box,
     CopyLaunch,
+    FusedLaunch,
     GemmLaunch,
     LoweringError,
     Lowerer,
@@ -872,7 +874,16 @@ class GpuDagExecutor(DagExecutor):
         weakref.finalize(dag, _drop_entry, weakref.ref(self), "_exec_dags", key)
         return new
 
-    def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None, **kwargs):
+    def execute_dag(self, dag, callbacks=None, array_names=None, resume=None, spec=None,
+                    compute_arrays_in_parallel=None, **kwargs):
+        """``compute_arrays_in_parallel`` (the async executors' flag,
+        ``runtime/executors/python_async.py:86-114``): the pipelines of one
+        topological generation are independent, so each runs on its own HIP
+        stream (up to ``PARALLEL_STREAMS``), joined back into the executor's
+        stream before the next generation.  Single GPU only: with several
+        ranks every collective must be issued in one order on one stream, so
+        the flag is accepted and the walk stays sequential."""
+        parallel = bool(compute_arrays_in_parallel) and self.world == 1
         if self.world > 1 and self._stream is not None and self.device.type == "cuda":
             # collectives are issued on torch's current stream: make it the
             # executor's, so the pack / exchange / unpack sequence of a
@@ -882,13 +893,13 @@ class GpuDagExecutor(DagExecutor):
             st = self._stream if isinstance(self._stream, torch.cuda.Stream) else \
                 torch.cuda.ExternalStream(int(self._stream), device=self.device)
             with torch.cuda.stream(st):
-                return self._execute_dag(dag, callbacks, array_names, resume)
-        return self._execute_dag(dag, callbacks, array_names, resume)
+                return self._execute_dag(dag, callbacks, array_names, resume, parallel)
+        return self._execute_dag(dag, callbacks, array_names, resume, parallel)
 
-    def _execute_dag(self, dag, callbacks, array_names, resume):
+    def _execute_dag(self, dag, callbacks, array_names, resume, parallel=False):
         stream = self.stream
         key = (id(dag), tuple(array_names or ()), bool(resume), self.elide_rechunks, self.fuse_producers,
-               self.fuse_reductions, self.fuse_gemm_sums)
+               self.fuse_reductions, self.fuse_gemm_sums, parallel)
         book = self._schedules.get(key)
         if book is not None and book.dag_ref() is dag:
             sched = book.lookup()
@@ -903,8 +914,14 @@ class GpuDagExecutor(DagExecutor):
             self._check_hbm(dag)
         targets = [d["target"] for _, d in dag.nodes(data=True) if isinstance(d.get("target"), DeviceArray)]
         state = tuple(t.written for t in targets)
+        gen_of = {}
+        if parallel:
+            for g, names in enumerate(nx.topological_generations(dag)):
+                for n in names:
+                    gen_of[n] = g
         steps = []
         for name, node in visit_nodes(dag, resume=resume):
+            gen = gen_of.get(name, 0)
             if name in members:
                 launches = []  # ran as part of its chain's fused launch
             elif name in chains:
@@ -938,6 +955,10 @@ class GpuDagExecutor(DagExecutor):
                         for t in getattr(ch, "extra_targets", ()):
                             self.elided.discard(id(t))
                         launches = self.compiled(name, node)
+                    else:
+                        # the fused launch reads every member's inputs: in a
+                        # generation walk it runs with the chain's last member
+                        gen = max(gen_of.get(m, 0) for m in ch.nodes)
             else:
                 launches = self.compiled(name, node)
             marks = []
@@ -946,8 +967,9 @@ class GpuDagExecutor(DagExecutor):
                          if isinstance(nodes[out].get("target"), DeviceArray)]
             op = node.get("primitive_op")
             events = list(node.get("fused_from", ())) + [(name, op.num_tasks if op is not None else 1)]
-            steps.append((name, tuple(launches), tuple(marks), tuple(events)))
-        sched = _Schedule(steps)
+            steps.append((name, tuple(launches), tuple(marks), tuple(events), gen))
+        sched = _Schedule(steps, parallel)
+        self.last_schedule = sched
         self._run_schedule(sched, stream, callbacks)
         # later calls with the same plan, names, resume flag and written
         # state replay the launch list without re-walking the DAG
@@ -956,52 +978,124 @@ class GpuDagExecutor(DagExecutor):
             weakref.finalize(plan_dag, _drop_entry, weakref.ref(self), "_schedules", key)
         book.add(state, sched)
 
+    PARALLEL_STREAMS = 4  # GPU_MAX_HW_QUEUES on the box: one hardware queue each
+
+    def _side_streams(self):
+        import torch
+
+        if getattr(self, "_sides", None) is None:
+            self._sides = [torch.cuda.Stream(device=self.device) for _ in range(self.PARALLEL_STREAMS - 1)]
+        return [s.cuda_stream for s in self._sides]
+
     def _run_schedule(self, sched, stream, callbacks):
+        """Run a recorded schedule.  Sequential: every launch on ``stream``.
+        Parallel: per generation, the ops whose launches are all native
+        kernel launches fork onto the side streams (each waits for the
+        generation's start on ``stream``), everything else runs on
+        ``stream`` first, and ``stream`` waits for every side stream before
+        the next generation -- the only dependencies a generation has are on
+        earlier generations."""
         timing = self.timing
         gpu_events = callbacks is not None and self.device.type == "cuda"
-        marks_ev = []
-        if gpu_events:
+        fork_ok = sched.parallel and self.device.type == "cuda"
+        use_events = gpu_events or fork_ok
+        if use_events:
             import torch
 
-            ext = torch.cuda.ExternalStream(stream, device=self.device)
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(ext)
-            marks_ev.append(ev)
+            ext_cache = {}
+
+            def ext(h):
+                e = ext_cache.get(h)
+                if e is None:
+                    e = ext_cache[h] = torch.cuda.ExternalStream(h, device=self.device)
+                return e
+
+            def record(h):
+                ev = torch.cuda.Event(enable_timing=gpu_events)
+                ev.record(ext(h))
+                return ev
+        nsteps = len(sched.steps)
+        start_ev = [None] * nsteps
+        end_ev = [None] * nsteps
         host = [time.time()]
-        for name, launches, marks, _ in sched.steps:
+        t0_ev = record(stream) if gpu_events else None
+
+        def run_step(i, h):
+            name, launches, marks, _, _ = sched.steps[i]
             if timing is None:
                 for launch in launches:
-                    launch.run(stream)
+                    launch.run(h)
             else:
-                for i, launch in enumerate(launches):
+                for j, launch in enumerate(launches):
                     ev0, ev1 = timing.events()
-                    ev0.record()
-                    launch.run(stream)
-                    ev1.record()
-                    timing.add((name, i, type(launch).__name__), ev0, ev1)
+                    if use_events:
+                        ev0.record(ext(h))
+                    else:
+                        ev0.record()
+                    launch.run(h)
+                    if use_events:
+                        ev1.record(ext(h))
+                    else:
+                        ev1.record()
+                    timing.add((name, j, type(launch).__name__), ev0, ev1)
             for t in marks:
                 t.written = True
-            if gpu_events:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record(ext)
-                marks_ev.append(ev)
-            elif callbacks is not None:
-                host.append(time.time())
+
+        for group in sched.groups:
+            if len(group) == 1 or not fork_ok:
+                for i in group:
+                    start_ev[i] = end_ev[i - 1] if i > 0 else t0_ev
+                    run_step(i, stream)
+                    if gpu_events:
+                        end_ev[i] = record(stream)
+                    elif callbacks is not None:
+                        host.append(time.time())
+                continue
+            # host-side steps (allocations, uploads) and single-launch
+            # generations stay on the executor's stream
+            forked = [i for i in group if sched.forkable[i]]
+            for i in group:
+                if i not in forked:
+                    start_ev[i] = t0_ev if gpu_events else None
+                    run_step(i, stream)
+                    if gpu_events:
+                        end_ev[i] = record(stream)
+            fork = record(stream)
+            sides = self._side_streams()
+            used = set()
+            for k, i in enumerate(forked):
+                h = stream if k == 0 else sides[(k - 1) % len(sides)]
+                if h != stream and h not in used:
+                    ext(h).wait_event(fork)
+                    used.add(h)
+                start_ev[i] = fork if gpu_events else None
+                run_step(i, h)
+                if gpu_events:
+                    end_ev[i] = record(h)
+            for h in used:
+                ext(stream).wait_event(record(h))
+            self.parallel_forks = getattr(self, "parallel_forks", 0) + 1
         if callbacks is None:
             return
         if gpu_events:
             # TaskEndEvents carry completion times: each op's end is its
-            # stream event, placed on the host clock from the last one
-            marks_ev[-1].synchronize()
+            # stream event, placed on the host clock from one final event
+            last = record(stream)
+            last.synchronize()
             t_end = time.time()
-            times = [t_end - ev.elapsed_time(marks_ev[-1]) * 1e-3 for ev in marks_ev]
+
+            def at(ev):
+                return t_end - ev.elapsed_time(last) * 1e-3
+
+            starts = [at(e if e is not None else t0_ev) for e in start_ev]
+            ends = [at(e if e is not None else last) for e in end_ev]
         else:
-            times = host
-        for i, (_, _, _, events) in enumerate(sched.steps):
+            starts, ends = host[:-1], host[1:]
+        for i, (_, _, _, events, _) in enumerate(sched.steps):
             for aname, ntasks in events:
-                ev = TaskEndEvent(array_name=aname, num_tasks=ntasks, function_start_tstamp=times[i],
-                                  function_end_tstamp=times[i + 1])
-                ev.task_result_tstamp = times[i + 1]
+                ev = TaskEndEvent(array_name=aname, num_tasks=ntasks, function_start_tstamp=starts[i],
+                                  function_end_tstamp=ends[i])
+                ev.task_result_tstamp = ends[i]
                 for cb in callbacks:
                     cb.on_task_end(ev)
 
@@ -1026,12 +1120,28 @@ class GpuDagExecutor(DagExecutor):
 
 class _Schedule:
     """One recorded execute_dag: per op, its launches, the targets it marks
-    written and the TaskEndEvents it emits."""
+    written, the TaskEndEvents it emits and its topological generation
+    (``groups``: consecutive runs of steps, one per generation when the
+    schedule runs generations in parallel)."""
 
-    def __init__(self, steps):
+    def __init__(self, steps, parallel=False):
         from ...storage import alloc_epoch
 
+        self.parallel = parallel
+        if parallel:
+            # a stable sort by generation: a chain's fused launch moved to
+            # its last member's generation keeps its place among that
+            # generation's ops
+            steps = sorted(steps, key=lambda st: st[4])
+            groups = {}
+            for i, st in enumerate(steps):
+                groups.setdefault(st[4], []).append(i)
+            self.groups = list(groups.values())
+        else:
+            self.groups = [[i] for i in range(len(steps))]
         self.steps = steps
+        self.forkable = [bool(st[1]) and all(isinstance(l, (CopyLaunch, FusedLaunch, GemmLaunch)) for l in st[1])
+                         for st in steps]
         self.epoch = alloc_epoch()
 
 

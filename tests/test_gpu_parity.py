@@ -189,7 +189,10 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     s1, s2 = seeds(4, 2)
     U = R.random_array(shape, chunks, s1).astype(np.float32)
     V = R.random_array(shape, chunks, s2).astype(np.float32)
-    got = xp.mean(u * v, axis=0).compute(resume=True)
+    seen = []
+    keep = [xp.mean(u * v, axis=0)]  # alive: the cache entries die with their plans
+    got = keep[-1].compute(resume=True)
+    seen += _fused_launches(e)
     exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
     assert np.allclose(got, exp, rtol=1e-6, atol=0)
 
@@ -198,11 +201,15 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     arrays_to_plan(a).execute(executor=e, array_names=[a.name])  # an array leaf, not a Philox leaf
     (s,) = seeds(8, 1)
     x = R.random_array((200, 1000), (50, 1000), s)
-    got = xp.mean((a + 1) * 2, axis=0).compute(resume=True)
+    keep.append(xp.mean((a + 1) * 2, axis=0))
+    got = keep[-1].compute(resume=True)
+    seen += _fused_launches(e)
     exp = R.mean((x + 1) * 2, (50, 1000), 0, allowed_mem=2_000_000_000)
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
     # the streaming map branch (no reduction): one IEEE op per element, bit-exact
-    np.testing.assert_array_equal(((a + 1) * 2).compute(resume=True), (x + 1) * 2)
+    keep.append((a + 1) * 2)
+    np.testing.assert_array_equal(keep[-1].compute(resume=True), (x + 1) * 2)
+    seen += _fused_launches(e)
     # a full reduction runs "lifted" in partials mode (per-element SoA
     # partials, then a fold): the W-group partial writes
     random.seed(9)
@@ -210,12 +217,14 @@ def test_stream_groups_per_thread(gpu_executor, monkeypatch, w):
     arrays_to_plan(b).execute(executor=e, array_names=[b.name])
     (sb,) = seeds(9, 1)
     y = R.random_array((200, 20000), (50, 20000), sb)
-    got = xp.mean(b * 3).compute(resume=True)
+    keep.append(xp.mean(b * 3))
+    got = keep[-1].compute(resume=True)
     assert np.allclose(got, np.mean(y * 3), rtol=1e-12, atol=0)
-    assert any(l.prog.mode & L.MODE_PARTIALS and l.prog.mode & L.MODE_STREAM for l in _fused_launches(e))
+    seen += _fused_launches(e)
+    assert any(l.prog.mode & L.MODE_PARTIALS and l.prog.mode & L.MODE_STREAM for l in seen)
 
     bits = {1: 0, 2: L.MODE_STREAM_W2, 4: L.MODE_STREAM_W4}[int(w)]
-    streams = [l for l in _fused_launches(e) if l.prog.mode & L.MODE_STREAM]
+    streams = list({id(l): l for l in seen if l.prog.mode & L.MODE_STREAM}.values())
     assert len(streams) >= 2
     assert all(l.prog.mode & (L.MODE_STREAM_W2 | L.MODE_STREAM_W4) == bits for l in streams)
 

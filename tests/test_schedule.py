@@ -159,3 +159,63 @@ def test_task_end_events_per_op_with_times(built, dry):
             if name in tasks and "primitive_op" in d:
                 assert tasks[name] == d["primitive_op"].num_tasks
     assert np.isfinite(ends[-1])
+
+
+def test_compute_arrays_in_parallel_groups_generations(built, dry):
+    """``compute_arrays_in_parallel`` (python_async.py:86-114): the schedule
+    is grouped by topological generation -- the two independent random
+    arrays' ops share one group (each on its own stream on a GPU), a later
+    op sits in a later group -- and the launches are the sequential walk's."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(12)
+    a = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    b = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    plan = arrays_to_plan(a, b)
+    dag = plan._finalize_dag()
+    op_a = next(iter(dag.predecessors(a.name)))
+    op_b = next(iter(dag.predecessors(b.name)))
+
+    dry.launched.clear()
+    plan.execute(executor=dry, compute_arrays_in_parallel=True, array_names=[a.name, b.name])
+    sched = dry.last_schedule
+    assert sched.parallel
+    groups = [[sched.steps[i][0] for i in g] for g in sched.groups]
+    (both,) = [g for g in groups if op_a in g]
+    assert op_b in both
+    i_a = [st[0] for st in sched.steps].index(op_a)
+    i_b = [st[0] for st in sched.steps].index(op_b)
+    assert sched.forkable[i_a] and sched.forkable[i_b]
+    par = [type(l).__name__ for l in dry.launched]
+
+    for t in (a.zarray, b.zarray):
+        t.written = False
+    dry.launched.clear()
+    plan.execute(executor=dry, array_names=[a.name, b.name])
+    assert not dry.last_schedule.parallel
+    assert all(len(g) == 1 for g in dry.last_schedule.groups)
+    assert sorted(par) == sorted(type(l).__name__ for l in dry.launched)
+
+
+def test_parallel_chain_runs_with_its_last_member(built, dry):
+    """A fused reduction chain's one launch reads what every member reads,
+    so in a generation walk it is placed in its last member's generation."""
+    spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+    random.seed(13)
+    a = crandom.random((40, 40), chunks=(10, 10), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    m = xp.mean(a * 2, axis=0)
+    s = xp.sum(a + 1, axis=1)
+    plan = arrays_to_plan(m, s)
+    plan.execute(executor=dry, compute_arrays_in_parallel=True, resume=True, array_names=[m.name, s.name])
+    sched = dry.last_schedule
+    gens = [st[4] for st in sched.steps]
+    assert gens == sorted(gens)
+    chains, _ = dry.chains_of(dry.exec_dag(plan._finalize_dag(), [m.name, s.name]), [m.name, s.name])
+    assert chains
+    import networkx as nx
+
+    exec_dag = dry.exec_dag(plan._finalize_dag(), [m.name, s.name])
+    gen_of = {n: g for g, names in enumerate(nx.topological_generations(exec_dag)) for n in names}
+    for head, ch in chains.items():
+        (st,) = [st for st in sched.steps if st[0] == head]
+        assert st[4] == max(gen_of[n] for n in ch.nodes)
