@@ -16,6 +16,8 @@ thread_local char g_err[512];
 #include "../cubed_amd/csrc/gemm_chain.hip"
 #include "gemm_bf16_experiments.h"
 #include "gemm_bf16_bt.h"
+#include "gemm_bf16_8ph.h"
+#include "gemm_bf16_stamp.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -101,13 +103,49 @@ int main(int argc, char** argv) {
   struct V { const char* name; kfn f; bool check; int threads = 0; bool bt = false; };
   V vs[] = {
       {"ping-pong NS4 (default)", k_gemm_bf16_chain<false, 0, 1>, false},
-      {"ping-pong, register staging 2 sets", k_gemm_bf16_chain<false, 0, 2, 2>, true},
-      {"ping-pong, register staging 3 sets", k_gemm_bf16_chain<false, 0, 2, 3>, true},
+      {"8-phase, B^T", k_gemm_bf16_8ph<false, 4, true>, true, 0, true},
+      {"8-phase, B^T, no setprio", k_gemm_bf16_8ph<false, 4, false>, true, 0, true},
       {"ping-pong NS4 (again)", k_gemm_bf16_chain<false, 0, 1>, true},
-      {"ping-pong, register staging 2 sets (again)", k_gemm_bf16_chain<false, 0, 2, 2>, true},
-      {"ping-pong, register staging 3 sets (again)", k_gemm_bf16_chain<false, 0, 2, 3>, true},
   };
   const int only = argc > 2 ? atoi(argv[2]) : -1;  // run one variant (PMC passes)
+  if (only == 99 || only == 98) {  // stamped diagnostic builds: per-segment cycle shares
+    unsigned long long* dbg;
+    const size_t nd = (size_t)grid.x * 8 * 8;
+    CHECK(hipMalloc(&dbg, nd * 8));
+    std::vector<unsigned long long> h(nd);
+    for (int r = 0; r < 3; ++r) {
+      CHECK(hipMemset(dbg, 0, nd * 8));
+      CHECK(hipEventRecord(e0));
+      if (only == 99)
+        hipLaunchKernelGGL((k_gemm_bf16_stamp<false>), grid, blk, 0, 0, dbg, dt1, ds, tm, tn, (const char*)Z);
+      else
+        hipLaunchKernelGGL((k_gemm_bf16_stamp_cs<false>), grid, blk, 0, 0, dbg, dt1, ds, tm, tn, (const char*)Z);
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      CHECK(hipMemcpy(h.data(), dbg, nd * 8, hipMemcpyDeviceToHost));
+      const char* names[6] = {"M: fragment reads (+lgkm wait)", only == 99 ? "M: staging issue" : "M: staging addresses", "M: vmcnt wait",
+                              "barrier into C", "C: 32 MFMA issue", "barrier out of C + loop"};
+      double tot[2][6] = {{0}}, cnt[2] = {0, 0};
+      for (size_t b = 0; b < grid.x; ++b)
+        for (int w = 0; w < 8; ++w) {
+          const unsigned long long* o = &h[(b * 8 + w) * 8];
+          unsigned long long s = 0;
+          for (int i = 0; i < 6; ++i) s += o[i];
+          if (!s) continue;
+          for (int i = 0; i < 6; ++i) tot[w >> 2][i] += (double)o[i];
+          cnt[w >> 2] += 1;
+        }
+      const double steps = (double)((N + 31) / 32);
+      printf("stamped run %d: %.3f ms (%.1f TF, diagnostic build)\n", r, ms, flop / ms / 1e9);
+      for (int i = 0; i < 6; ++i)
+        printf("  %-34s row0 %8.1f  row1 %8.1f cyc/step\n", names[i], tot[0][i] / cnt[0] / steps,
+               tot[1][i] / cnt[1] / steps);
+    }
+    return 0;
+  }
   for (const V& v : vs) {
     if (only >= 0 && &v - vs != only) continue;
     float best = 1e30f;
