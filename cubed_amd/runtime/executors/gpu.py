@@ -883,6 +883,14 @@ class GpuDagExecutor(DagExecutor):
         stream before the next generation.  Single GPU only: with several
         ranks every collective must be issued in one order on one stream, so
         the flag is accepted and the walk stays sequential."""
+        from ..reference_dag import execute_reference_dag, is_reference_dag
+
+        if is_reference_dag(dag):
+            # a plan built by the reference cubed: converted (targets to HBM,
+            # chunk functions traced), run, outputs written to their Zarr stores
+            execute_reference_dag(self, dag, callbacks=callbacks, array_names=array_names, resume=resume,
+                                  spec=spec, compute_arrays_in_parallel=compute_arrays_in_parallel, **kwargs)
+            return
         parallel = bool(compute_arrays_in_parallel) and self.world == 1
         if self.world > 1 and self._stream is not None and self.device.type == "cuda":
             # collectives are issued on torch's current stream: make it the

@@ -1,0 +1,398 @@
+"""Plans built by the reference cubed, run on the MI355X executor.
+
+The reference's executor plug-in contract is "any DAG" (``DagExecutor.
+execute_dag``, cubed/runtime/types.py:9-14): op nodes carry a
+``CubedPipeline(function, name, mappable, config)`` whose stage function is
+``apply_blockwise`` (config ``BlockwiseSpec(block_function, function,
+function_nargs, reads_map, write)``, primitive/blockwise.py:34-103),
+``copy_read_to_write`` (config ``CubedCopySpec(read, write)``,
+primitive/rechunk.py:187-192) or ``create_zarr_array`` (core/plan.py:430-
+456); array nodes carry ``target`` = a ``LazyZarrArray`` (intermediates,
+storage/zarr.py:8-103), a ``zarr.Array`` (sources) or a virtual array
+(storage/virtual.py:14-182).  ``GpuDagExecutor.execute_dag`` recognises such
+a DAG (stage functions from the ``cubed`` package) and hands it here:
+
+* every target becomes an HBM ``DeviceArray`` with the same shape, dtype and
+  chunks (virtual arrays their ``cubed_amd.storage`` counterparts, Zarr
+  sources an upload op reading the store with ``cubed_amd.zarr_io``);
+* every chunk function is lowered by tracing it on proxies
+  (``cubed_amd.tracing``): elementwise numpy / ``array_api_compat`` calls
+  and Python operators, through the reference's ``fuse``/``fuse_multiple``
+  closures, ``functools.partial`` keyword binding and ``astype``; the
+  reference's ``random`` (``map_blocks(_random, ...)`` wrapped by
+  ``func_with_block_id``, cubed/random.py:13-36, core/ops.py:531-560) is
+  recognised and becomes the bit-exact Philox leaf;
+* rechunk copies keep their read / write chunking and become copy launches.
+
+The converted DAG keeps the reference's op names, task counts and array
+names, so callbacks see the same TaskEndEvents and ``resume`` works.  After
+the run, the requested arrays are written into their Zarr stores (the
+paths of their ``LazyZarrArray``s, Zarr v2 via ``cubed_amd.zarr_io``) where
+the reference's ``compute()`` reads them back.
+
+What is not lowered raises ``LoweringError`` naming the op: chunk functions
+that are not elementwise (the reference's reduction rounds -- ``_mean_func``
+returns a dict of fields, ``merge_chunks``/``index`` read side inputs through
+``map_direct`` --, contractions with nested block keys, functions taking
+``block_id`` other than ``random``).  The reference cannot be imported in
+this image, so the tests build DAGs of the reference's shape from stand-ins
+with the same class names and attributes (tests/test_reference_dag.py).
+"""
+
+from __future__ import annotations
+
+import functools
+import weakref
+from typing import Dict
+
+import networkx as nx
+import numpy as np
+
+from .. import ir, tracing
+from ..core.ops import UploadSpec, upload_stage
+from ..core.plan import create_arrays_op
+from ..lowering import LoweringError
+from ..primitive.blockwise import BlockwiseSpec, apply_blockwise
+from ..primitive.rechunk import copy_read_to_write
+from ..primitive.types import CubedArrayProxy, CubedCopySpec, PrimitiveOperation
+from ..storage import (
+    DeviceArray,
+    VirtualEmptyArray,
+    VirtualFullArray,
+    VirtualInMemoryArray,
+    VirtualOffsetsArray,
+)
+from ..utils import normalize_chunks
+from .types import CubedPipeline
+
+
+def _module_of(f) -> str:
+    return getattr(f, "__module__", "") or ""
+
+
+def is_reference_dag(dag) -> bool:
+    """True when the DAG's stage functions come from the reference package
+    (``cubed.*``), not from this one."""
+    for _, d in dag.nodes(data=True):
+        p = d.get("pipeline")
+        if p is not None:
+            mod = _module_of(p.function)
+            return mod == "cubed" or mod.startswith("cubed.")
+    return False
+
+
+class ConvertedDag:
+    """The executor-side DAG of a reference DAG and where its outputs go."""
+
+    def __init__(self, dag, targets: Dict[str, DeviceArray], sinks: Dict[str, object]):
+        self.dag = dag
+        self.targets = targets  # array name -> DeviceArray
+        self.sinks = sinks      # array name -> reference target (LazyZarrArray / zarr.Array)
+
+
+def _store_path(t):
+    """Filesystem path of a reference Zarr target (a LazyZarrArray's store is
+    the path string new_temp_path made; a zarr.Array's a DirectoryStore)."""
+    store = getattr(t, "store", None)
+    if isinstance(store, str):
+        base = store
+    elif store is not None and isinstance(getattr(store, "path", None), str):
+        base = store.path
+    else:
+        raise LoweringError(f"Zarr target {t!r}: only local directory stores are supported")
+    sub = getattr(t, "path", "") if type(t).__name__ != "LazyZarrArray" else ""
+    import os
+
+    return os.path.join(base, sub) if sub else base
+
+
+class _Converter:
+    def __init__(self, dag):
+        self.ref = dag
+        self.arrays: Dict[int, object] = {}
+        self.sources = []  # (node name, ZarrV2Array, DeviceArray): uploads to add
+
+    # -- arrays ----------------------------------------------------------------
+    def array(self, t, name):
+        key = id(t)
+        if key in self.arrays:
+            return self.arrays[key]
+        kind = type(t).__name__
+        if kind == "LazyZarrArray":
+            out = DeviceArray(t.shape, t.dtype, t.chunks, name=name)
+        elif kind == "VirtualEmptyArray":
+            out = VirtualEmptyArray(t.shape, t.dtype, t.chunks)
+        elif kind == "VirtualFullArray":
+            out = VirtualFullArray(t.shape, t.dtype, t.chunks, fill_value=t.fill_value)
+        elif kind == "VirtualOffsetsArray":
+            out = VirtualOffsetsArray(t.shape)
+        elif kind == "VirtualInMemoryArray":
+            out = VirtualInMemoryArray(np.asarray(t.array), t.chunks)
+        elif kind == "Array" and hasattr(t, "store"):
+            # an existing Zarr array (from_zarr / a computed intermediate)
+            from ..zarr_io import ZarrV2Array
+
+            src = ZarrV2Array.open(_store_path(t))
+            out = DeviceArray(src.shape, src.dtype, src.chunks, name=name)
+            self.sources.append((name, src, out))
+        elif isinstance(t, (DeviceArray, VirtualEmptyArray, VirtualFullArray, VirtualOffsetsArray,
+                            VirtualInMemoryArray)):
+            out = t
+        else:
+            raise LoweringError(f"array {name}: reference target {kind} is not supported")
+        self.arrays[key] = out
+        return out
+
+    def proxy(self, p, name):
+        return CubedArrayProxy(self.array(p.array, name), p.chunks)
+
+    # -- chunk functions -------------------------------------------------------
+    def program(self, op, cfg, reads, write):
+        """IR program of the reference chunk function ``cfg.function``."""
+        out = write.array
+        nd = out.ndim
+        first = tuple(0 for _ in range(nd))
+        try:
+            args = list(cfg.block_function(("out",) + first))
+        except Exception as e:  # noqa: BLE001 -- a key function that fails is not lowerable
+            raise LoweringError(f"op {op}: block function failed on {first}: {e}") from None
+        names = []
+        for nci in args:
+            if not (isinstance(nci, tuple) and nci and isinstance(nci[0], str)):
+                raise LoweringError(f"op {op}: nested block keys (contractions / partial reductions) "
+                                    "of reference chunk functions are not lowered")
+            names.append(nci[0])
+        arrays = [reads[n].array for n in names]
+        self._check_alignment(op, cfg, arrays, out)
+        inds = [tuple(range(nd - a.ndim, nd)) for a in arrays]
+        fn = cfg.function
+        if _is_reference_random(fn):  # the random op itself (not fused)
+            fn = _random_leaf(fn, write.chunks, out.shape, out.dtype)
+        with _random_standins(fn):
+            prog = tracing.trace_callable(fn, arrays, inds, tuple(range(nd)), out.dtype, {})
+        if prog is None:
+            raise LoweringError(
+                f"op {op}: chunk function {cfg.function!r} is not traceable to a fused chunk program "
+                "(elementwise numpy calls and operators are; reductions, side-input reads and "
+                "block_id functions other than random are not)")
+        return prog
+
+    def _check_alignment(self, op, cfg, arrays, out):
+        """The trailing-dims (numpy broadcasting) index mapping the traced
+        program assumes: arg block coordinates equal the output's trailing
+        coordinates, or 0 along dims where the arg has one block."""
+        if out.ndim == 0:
+            return
+        probes = {tuple(0 for _ in out.numblocks), tuple(n - 1 for n in out.numblocks)}
+        for key in probes:
+            for nci, a in zip(cfg.block_function(("out",) + key), arrays):
+                coords = tuple(nci[1:])
+                nb = getattr(a, "numblocks", None)
+                if nb is None:
+                    nb = tuple(len(c) for c in normalize_chunks(a.chunks, a.shape, a.dtype))
+                tail = key[len(key) - len(coords):] if coords else ()
+                want = tuple(0 if n == 1 else k for n, k in zip(nb, tail))
+                if coords != want:
+                    raise LoweringError(f"op {op}: block index mapping {key} -> {coords} is not "
+                                        "elementwise (broadcast over trailing dims)")
+
+    # -- ops -------------------------------------------------------------------
+    def convert(self):
+        ref = self.ref
+        g = nx.MultiDiGraph()
+        nodes = dict(ref.nodes(data=True))
+        targets: Dict[str, DeviceArray] = {}
+        sinks: Dict[str, object] = {}
+        # arrays first: every op's reads / write resolve to the same objects
+        for name, d in nodes.items():
+            if "target" in d and d.get("target") is not None:
+                conv = self.array(d["target"], name)
+                if isinstance(conv, DeviceArray):
+                    targets[name] = conv
+                    if type(d["target"]).__name__ == "LazyZarrArray":
+                        sinks[name] = d["target"]
+        for name, d in nodes.items():
+            attrs = {k: v for k, v in d.items() if k not in ("pipeline", "primitive_op", "target")}
+            if "target" in d:
+                t = d["target"]
+                attrs["target"] = None if t is None else self.array(t, name)
+            p = d.get("pipeline")
+            if p is not None:
+                op = self.op(name, p, d.get("primitive_op"), targets)
+                if op is not None:
+                    attrs.update(primitive_op=op, pipeline=op.pipeline)
+            g.add_node(name, **attrs)
+        for u, v, k in ref.edges(keys=True):
+            g.add_edge(u, v, key=k)
+        # Zarr sources without a producing op: an upload op each
+        for i, (name, src, tgt) in enumerate(self.sources):
+            if any("pipeline" in nodes.get(u, {}) for u in ref.predecessors(name)):
+                continue
+            up = f"upload-{name}"
+            pipe = CubedPipeline(upload_stage, up, [], UploadSpec(src, tgt))
+            op = PrimitiveOperation(pipeline=pipe, target_array=tgt, projected_mem=0, allowed_mem=0,
+                                    reserved_mem=0, num_tasks=tgt.nchunks, fusable=False)
+            g.add_node(up, name=up, op_name="upload", type="op", primitive_op=op, pipeline=pipe)
+            g.add_edge(up, name)
+        return ConvertedDag(nx.freeze(g), targets, sinks)
+
+    def op(self, name, p, pop, targets):
+        fname = getattr(p.function, "__name__", "")
+        cfg = p.config
+        meta = dict(projected_mem=getattr(pop, "projected_mem", 0), allowed_mem=getattr(pop, "allowed_mem", 0),
+                    reserved_mem=getattr(pop, "reserved_mem", 0),
+                    num_tasks=getattr(pop, "num_tasks", 1), fusable=getattr(pop, "fusable", False))
+        if fname == "create_zarr_array":
+            devs = [self.array(t, getattr(t, "name", None) or "array") for t in p.mappable]
+            devs = [t for t in devs if isinstance(t, DeviceArray)]
+            op = create_arrays_op(devs, meta["allowed_mem"], meta["reserved_mem"])
+            return PrimitiveOperation(pipeline=op.pipeline, target_array=None, **meta)
+        if fname == "apply_blockwise":
+            reads = {n: self.proxy(px, n) for n, px in cfg.reads_map.items()}
+            write = self.proxy(cfg.write, name)
+            prog = self.program(name, cfg, reads, write)
+            spec = BlockwiseSpec(cfg.block_function, prog, cfg.function_nargs, reads, write)
+            pipe = CubedPipeline(apply_blockwise, p.name, p.mappable, spec)
+            return PrimitiveOperation(pipeline=pipe, target_array=write.array, **meta)
+        if fname == "copy_read_to_write":
+            spec = CubedCopySpec(self.proxy(cfg.read, name + "-read"), self.proxy(cfg.write, name))
+            pipe = CubedPipeline(copy_read_to_write, p.name, p.mappable, spec)
+            return PrimitiveOperation(pipeline=pipe, target_array=spec.write.array, **meta)
+        raise LoweringError(f"op {name}: reference stage function {fname or p.function!r} is not supported")
+
+
+# ------------------------------------------------------------------ random
+def _is_reference_random(f) -> bool:
+    """``partial(wrap, numblocks=..., root_seed=...)`` where ``wrap`` is
+    map_blocks' ``func_with_block_id`` closure over ``cubed.random._random``."""
+    if not isinstance(f, functools.partial):
+        return False
+    inner = f.func
+    if getattr(inner, "__name__", "") != "wrap" or not inner.__closure__:
+        return False
+    kw = f.keywords or {}
+    if "root_seed" not in kw or "numblocks" not in kw:
+        return False
+    for cell in inner.__closure__:
+        try:
+            v = cell.cell_contents
+        except ValueError:
+            continue
+        if getattr(v, "__name__", "") == "_random" and _module_of(v).endswith("random"):
+            return True
+    return False
+
+
+def _random_leaf(f, out_chunks, shape, dtype):
+    """A traceable stand-in for the reference random chunk function: the
+    Philox leaf reading the block offset from the offsets argument."""
+    kw = f.keywords
+    nd = len(shape)
+    chunks = normalize_chunks(out_chunks, shape, dtype)
+
+    def standin(*args):
+        off = args[-1]
+        if not isinstance(off, tracing._Proxy) or not isinstance(off.expr, ir.Arg):
+            raise tracing._Untraceable("random without its offsets argument")
+        leaf = ir.Philox(root_seed=int(kw["root_seed"]), numblocks=tuple(kw["numblocks"]),
+                         block_arg=off.expr.index, axes=tuple(range(nd)), chunks=chunks)
+        return tracing._Proxy(leaf, nd)
+
+    return standin
+
+
+class _random_standins:
+    """Context: every reference random chunk function reachable from ``fn``
+    (directly, or inside the ``fuse``/``fuse_multiple`` closures through the
+    fused pipelines' BlockwiseSpecs) is swapped for its Philox stand-in while
+    the function is traced, and restored afterwards."""
+
+    def __init__(self, fn):
+        self.fn = fn
+        self.swapped = []
+
+    def __enter__(self):
+        seen = set()
+
+        def visit(obj, depth=0):
+            if id(obj) in seen or depth > 64:
+                return
+            seen.add(id(obj))
+            if isinstance(obj, functools.partial):
+                visit(obj.func, depth + 1)
+                for a in obj.args:
+                    visit(a, depth + 1)
+                for a in (obj.keywords or {}).values():
+                    visit(a, depth + 1)
+            elif callable(obj) and getattr(obj, "__closure__", None):
+                for cell in obj.__closure__:
+                    try:
+                        visit(cell.cell_contents, depth + 1)
+                    except ValueError:
+                        pass
+            cfg = getattr(obj, "config", None)
+            if cfg is not None and hasattr(cfg, "function") and hasattr(cfg, "write"):
+                if _is_reference_random(cfg.function):
+                    w = cfg.write.array
+                    new = _random_leaf(cfg.function, cfg.write.chunks, w.shape, w.dtype)
+                    self.swapped.append((cfg, cfg.function))
+                    object.__setattr__(cfg, "function", new)
+                else:
+                    visit(cfg.function, depth + 1)
+
+        visit(self.fn)
+        return self
+
+    def __exit__(self, *exc):
+        for cfg, f in reversed(self.swapped):
+            object.__setattr__(cfg, "function", f)
+        return False
+
+
+# ------------------------------------------------------------------ run
+_CACHE: Dict[int, tuple] = {}
+
+
+def _drop(key):
+    _CACHE.pop(key, None)
+
+
+def convert_reference_dag(dag) -> ConvertedDag:
+    """The executor-side DAG of a reference DAG, cached while it lives."""
+    key = id(dag)
+    hit = _CACHE.get(key)
+    if hit is not None and hit[0]() is dag:
+        return hit[1]
+    conv = _Converter(dag).convert()
+    _CACHE[key] = (weakref.ref(dag), conv)
+    weakref.finalize(dag, _drop, key)
+    return conv
+
+
+def execute_reference_dag(executor, dag, callbacks=None, array_names=None, resume=None, spec=None,
+                          **kwargs):
+    """Run a reference-built DAG on ``executor`` and write the requested
+    arrays to their Zarr stores."""
+    conv = convert_reference_dag(dag)
+    executor.execute_dag(conv.dag, callbacks=callbacks, array_names=array_names, resume=resume,
+                         spec=spec, **kwargs)
+    write_back(conv, array_names)
+    return conv
+
+
+def write_back(conv: ConvertedDag, array_names):
+    """The requested arrays, device -> their reference Zarr stores (created
+    here with the LazyZarrArray's shape, dtype, chunks and fill value)."""
+    from ..zarr_io import ZarrV2Array, write_device_array
+
+    for name in array_names or ():
+        t = conv.sinks.get(name)
+        d = conv.targets.get(name)
+        if t is None or d is None:
+            continue
+        dst = ZarrV2Array.create(_store_path(t), d.shape, d.dtype, d.chunks,
+                                 fill_value=getattr(t, "fill_value", None), mode="a")
+        write_device_array(d, dst)
+
+
+__all__ = ["is_reference_dag", "convert_reference_dag", "execute_reference_dag", "ConvertedDag"]

@@ -1,0 +1,195 @@
+"""Reference-built DAGs on the MI355X executor (cubed_amd/runtime/
+reference_dag.py): the plug-in contract is "any DAG" (cubed/runtime/
+types.py:9-14).  The reference cannot be imported here, so the DAGs come from
+tests/refdag.py's stand-ins of the reference's classes and chunk-function
+wrappers (API-shape fixtures, see its docstring).
+
+CPU: the conversion (array kinds, traced programs through fuse closures and
+partial binding, the random chunk function recognised as the Philox leaf,
+copy ops) and the launches the dry executor would run; refusals name the op.
+GPU: the whole plan executed, the requested array written to its Zarr store
+and read back bit-exactly against the oracle (numpy Philox, f32 arithmetic).
+"""
+
+import functools
+import random
+
+import numpy as np
+import pytest
+
+import cubed_amd.lowering as L
+from cubed_amd import ir
+from cubed_amd.runtime import reference_dag as RD
+from cubed_amd.storage import DeviceArray, VirtualEmptyArray, VirtualInMemoryArray, VirtualOffsetsArray
+
+import refdag
+
+
+def _seed(s):
+    random.seed(s)
+    return random.getrandbits(128)
+
+
+def _leaves(e, out):
+    """Leaves of an IR expression (Philox / Arg), walking every Expr field."""
+    import dataclasses
+
+    if isinstance(e, (ir.Philox, ir.Arg)):
+        out.append(e)
+        return out
+    if dataclasses.is_dataclass(e):
+        for f in dataclasses.fields(e):
+            v = getattr(e, f.name)
+            for c in (v if isinstance(v, (tuple, list)) else (v,)):
+                if isinstance(c, ir.Expr):
+                    _leaves(c, out)
+    return out
+
+
+def test_reference_dag_is_recognised(tmp_path):
+    dag, out, _ = refdag.example_plan(tmp_path, _seed(1))
+    assert RD.is_reference_dag(dag)
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+
+    a = xp.ones((4, 4), chunks=(2, 2), spec=cubed.Spec(allowed_mem="1GB"))
+    from cubed_amd.core.plan import arrays_to_plan
+
+    assert not RD.is_reference_dag(arrays_to_plan(a + 1)._finalize_dag())
+
+
+def test_conversion_keeps_names_counts_and_traces_programs(tmp_path):
+    seed = _seed(2)
+    dag, out, _ = refdag.example_plan(tmp_path, seed)
+    conv = RD.convert_reference_dag(dag)
+    g = conv.dag
+    assert set(g.nodes) >= set(dag.nodes)
+    for n, d in dag.nodes(data=True):
+        if "primitive_op" in d:
+            assert g.nodes[n]["primitive_op"].num_tasks == d["primitive_op"].num_tasks
+        t = d.get("target")
+        if isinstance(t, refdag.LazyZarrArray):
+            dt = g.nodes[n]["target"]
+            assert isinstance(dt, DeviceArray)
+            assert (dt.shape, dt.dtype, tuple(dt.chunks)) == (t.shape, t.dtype, t.chunks)
+        elif isinstance(t, refdag.VirtualEmptyArray):
+            assert isinstance(g.nodes[n]["target"], VirtualEmptyArray)
+        elif isinstance(t, refdag.VirtualOffsetsArray):
+            assert isinstance(g.nodes[n]["target"], VirtualOffsetsArray)
+        elif isinstance(t, refdag.VirtualInMemoryArray):
+            assert isinstance(g.nodes[n]["target"], VirtualInMemoryArray)
+    progs = {n: d["pipeline"].config.function for n, d in g.nodes(data=True)
+             if d.get("pipeline") is not None and isinstance(d["pipeline"].config, RD.BlockwiseSpec)}
+    kinds = {n: [type(x).__name__ for x in _leaves(p.outputs, [])] for n, p in progs.items()}
+    # the fused random + astype op reads no array: its one leaf is Philox
+    fused = [n for n, k in kinds.items() if k == ["Philox"]]
+    assert len(fused) == 1
+    ph = _leaves(progs[fused[0]].outputs, [])[0]
+    assert ph.root_seed == seed and ph.numblocks == (4, 3) and ph.block_arg == 1
+    assert progs[fused[0]].outputs.dtype == np.float32
+    # the two scalar ops: an array leaf and a 0-d leaf each
+    assert sorted(len(k) for k in kinds.values()) == [1, 2, 2]
+    # the requested output's Zarr sink is the LazyZarrArray's store
+    assert out in conv.sinks
+
+
+def test_dry_run_launches(tmp_path, built, dry):
+    dag, out, _ = refdag.example_plan(tmp_path, _seed(3))
+    dry.launched.clear()
+    dry.execute_dag(RD.convert_reference_dag(dag).dag, array_names=[out])
+    kinds = [type(l).__name__ for l in dry.launched]
+    # the executor fuses the elementwise chain into one streaming launch and
+    # the rechunk into one copy
+    assert kinds.count("CopyLaunch") == 1
+    assert 1 <= kinds.count("FusedLaunch") <= 3
+
+
+def test_unlowerable_reference_op_is_refused(tmp_path):
+    p = refdag.RefPlan(tmp_path)
+    rop, rname, rsrcs = p.random((8, 8), (4, 4), _seed(4))
+    p.add(rop, rname, rsrcs)
+
+    def reduce_like(x):  # a dict of fields, like _mean_func
+        return {"n": x.size, "total": np.sum(x)}
+
+    name = p._name("array")
+    op, _ = p.blockwise_op(reduce_like, name, (8, 8), np.float64, (4, 4), [(rname, p.g.nodes[rname]["target"])])
+    op_name = p.add(op, name, [rname])
+    with pytest.raises(L.LoweringError, match=op_name):
+        RD.convert_reference_dag(p.finalize())
+
+
+def test_non_elementwise_index_mapping_is_refused(tmp_path):
+    p = refdag.RefPlan(tmp_path)
+    rop, rname, rsrcs = p.random((8, 4), (4, 4), _seed(5))
+    p.add(rop, rname, rsrcs)
+    name = p._name("array")
+    op, target = p.blockwise_op(np.negative, name, (4, 8), np.float64, (4, 4),
+                                [(rname, p.g.nodes[rname]["target"])])
+    # a transpose-like key function: output block (i, j) reads (j, i)
+    bf = lambda k: [(rname, k[2], k[1])]  # noqa: E731
+    spec = refdag.BlockwiseSpec(bf, np.negative, 1, op.pipeline.config.reads_map, op.pipeline.config.write)
+    op = refdag.PrimitiveOperation(refdag.CubedPipeline(refdag.apply_blockwise, "t", [], spec), target,
+                                   0, p.MEM, 0, 2, True)
+    op_name = p.add(op, name, [rname])
+    with pytest.raises(L.LoweringError, match=op_name):
+        RD.convert_reference_dag(p.finalize())
+
+
+@pytest.mark.gpu
+def test_reference_plan_runs_on_the_gpu(tmp_path, gpu_executor):
+    """The example plan through GpuDagExecutor.execute_dag (recognised as a
+    reference DAG), the requested array read back from its Zarr store and
+    the intermediate (not requested) left unwritten; values bit-exact vs
+    numpy Philox blocks -> f32 -> * 2 + 1 (f32 arithmetic) -> rechunk."""
+    from cubed_amd.runtime.types import Callback
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    class Rec(Callback):
+        def __init__(self):
+            self.events = []
+
+        def on_task_end(self, event):
+            self.events.append(event)
+
+    seed = _seed(6)
+    shape, chunks = (40, 60), (10, 20)
+    dag, out, mid = refdag.example_plan(tmp_path, seed, shape, chunks, (40, 10))
+    rec = Rec()
+    gpu_executor.execute_dag(dag, callbacks=[rec], array_names=[out])
+    exp = R.random_array(shape, chunks, seed).astype(np.float32) * np.float32(2) + np.float32(1)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    assert got.dtype == np.float32 and got.shape == shape
+    np.testing.assert_array_equal(got, exp)
+    ops = {n: d["primitive_op"].num_tasks for n, d in dag.nodes(data=True) if "primitive_op" in d}
+    got_tasks = {e.array_name: e.num_tasks for e in rec.events}
+    for n, k in ops.items():
+        if n in got_tasks:
+            assert got_tasks[n] == k
+    assert not (tmp_path / f"{mid}.zarr").exists()
+    # a second execute replays (same DAG, same names)
+    gpu_executor.execute_dag(dag, array_names=[out])
+    np.testing.assert_array_equal(ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...], exp)
+
+
+@pytest.mark.gpu
+def test_reference_random_unfused_on_the_gpu(tmp_path, gpu_executor):
+    """random on its own (the op not fused into a consumer) and a fuse-free
+    elementwise consumer reading it from HBM."""
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    seed = _seed(7)
+    p = refdag.RefPlan(tmp_path)
+    rop, rname, rsrcs = p.random((30, 20), (7, 20), seed)
+    p.add(rop, rname, rsrcs)
+    name = p._name("array")
+    op, _ = p.blockwise_op(functools.partial(np.sqrt), name, (30, 20), np.float64, (7, 20),
+                           [(rname, p.g.nodes[rname]["target"])])
+    p.add(op, name, [rname])
+    dag = p.finalize()
+    gpu_executor.execute_dag(dag, array_names=[rname, name])
+    x = R.random_array((30, 20), (7, 20), seed)
+    np.testing.assert_array_equal(ZarrV2Array.open(str(tmp_path / f"{rname}.zarr"))[...], x)
+    np.testing.assert_array_equal(ZarrV2Array.open(str(tmp_path / f"{name}.zarr"))[...], np.sqrt(x))
