@@ -15,13 +15,20 @@ a DAG (stage functions from the ``cubed`` package) and hands it here:
 * every target becomes an HBM ``DeviceArray`` with the same shape, dtype and
   chunks (virtual arrays their ``cubed_amd.storage`` counterparts, Zarr
   sources an upload op reading the store with ``cubed_amd.zarr_io``);
-* every chunk function is lowered by tracing it on proxies
-  (``cubed_amd.tracing``): elementwise numpy / ``array_api_compat`` calls
-  and Python operators, through the reference's ``fuse``/``fuse_multiple``
-  closures, ``functools.partial`` keyword binding and ``astype``; the
-  reference's ``random`` (``map_blocks(_random, ...)`` wrapped by
-  ``func_with_block_id``, cubed/random.py:13-36, core/ops.py:531-560) is
-  recognised and becomes the bit-exact Philox leaf;
+* a pipeline the reference optimizer fused is taken apart into the
+  pipelines its ``fuse``/``fuse_multiple`` closure holds, each converted and
+  fused again with this package's ``fuse``/``fuse_multiple`` (IR programs
+  compose);
+* the reference's own chunk functions map to their IR counterparts: the
+  reduction functions (``_mean_func``/``_mean_combine``/``_mean_aggregate``,
+  the nan variants, ``nxp.sum``/``max``/... with ``axis``/``keepdims``/
+  ``dtype``), ``squeeze``, merge_chunks' ``_copy_chunk`` under map_direct (a
+  ``Region`` leaf), and ``random`` (``map_blocks(_random, ...)`` under
+  ``func_with_block_id``, cubed/random.py:13-36) the bit-exact Philox leaf;
+* any other chunk function is lowered by tracing it on proxies
+  (``cubed_amd.tracing``): elementwise numpy / ``array_api_compat`` calls,
+  Python operators, ``astype``, ``where``, with ``functools.partial``
+  keyword binding;
 * rechunk copies keep their read / write chunking and become copy launches.
 
 The converted DAG keeps the reference's op names, task counts and array
@@ -30,11 +37,10 @@ the run, the requested arrays are written into their Zarr stores (the
 paths of their ``LazyZarrArray``s, Zarr v2 via ``cubed_amd.zarr_io``) where
 the reference's ``compute()`` reads them back.
 
-What is not lowered raises ``LoweringError`` naming the op: chunk functions
-that are not elementwise (the reference's reduction rounds -- ``_mean_func``
-returns a dict of fields, ``merge_chunks``/``index`` read side inputs through
-``map_direct`` --, contractions with nested block keys, functions taking
-``block_id`` other than ``random``).  The reference cannot be imported in
+What is not lowered raises ``LoweringError`` naming the op: user chunk
+functions that are not elementwise, contractions with nested block keys
+(matmul / tensordot / partial_reduce), ``index``'s side-input reads, and
+functions taking ``block_id`` other than ``random``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -168,14 +174,102 @@ class _Converter:
         fn = cfg.function
         if _is_reference_random(fn):  # the random op itself (not fused)
             fn = _random_leaf(fn, write.chunks, out.shape, out.dtype)
-        with _random_standins(fn):
-            prog = tracing.trace_callable(fn, arrays, inds, tuple(range(nd)), out.dtype, {})
+        prog = tracing.trace_callable(fn, arrays, inds, tuple(range(nd)), out.dtype, {})
         if prog is None:
             raise LoweringError(
                 f"op {op}: chunk function {cfg.function!r} is not traceable to a fused chunk program "
                 "(elementwise numpy calls and operators are; reductions, side-input reads and "
                 "block_id functions other than random are not)")
         return prog
+
+    def blockwise(self, name, p, meta):
+        """Our PrimitiveOperation for a reference blockwise pipeline.  A
+        pipeline the reference optimizer fused (``fuse`` / ``fuse_multiple``
+        closures, primitive/blockwise.py:368-508) is taken apart into the
+        pipelines it closes over, each converted, and fused again with this
+        package's ``fuse`` / ``fuse_multiple`` (which compose IR programs)."""
+        parts = _fused_parts(p.config.function)
+        if parts is not None:
+            from ..primitive.blockwise import fuse, fuse_multiple
+
+            kind, data = parts
+            if kind == "fuse":
+                p1, p2 = data
+                return fuse(self.blockwise(name, p1, meta), self.blockwise(name, p2, meta))
+            consumer, preds = data
+            return fuse_multiple(self.blockwise(name, consumer, meta),
+                                 *[self.blockwise(name, pp, meta) if pp is not None else None for pp in preds])
+        cfg = p.config
+        reads = {n: self.proxy(px, n) for n, px in cfg.reads_map.items()}
+        write = self.proxy(cfg.write, name)
+        prog = self.known_program(name, cfg, reads, write)
+        if prog is None:
+            prog = self.program(name, cfg, reads, write)
+        spec = BlockwiseSpec(cfg.block_function, prog, cfg.function_nargs, reads, write)
+        pipe = CubedPipeline(apply_blockwise, p.name, p.mappable, spec)
+        return PrimitiveOperation(pipeline=pipe, target_array=write.array, **meta)
+
+    def known_program(self, op, cfg, reads, write):
+        """IR for the reference's own chunk functions, which are not
+        elementwise and so not traceable: the reduction functions
+        (statistical_functions.py:54-100, nan_functions.py:21-77, ``nxp.sum``
+        / ``max`` / ... with ``axis``/``keepdims``/``dtype``), ``squeeze``
+        (core/ops.py:1156-1169) and merge_chunks' ``_copy_chunk`` under
+        map_direct (core/ops.py:646-787).  None: not one of them."""
+        base, kw, wrappers = _unwrap(cfg.function)
+        bname = getattr(base, "__name__", "")
+        bmod = _module_of(base)
+        out = write.array
+        first = tuple(0 for _ in range(out.ndim))
+        keys = list(cfg.block_function(("out",) + first))
+        if bname == "_copy_chunk" and bmod.startswith("cubed"):
+            src_arr = kw.get("arrays", (None,))[0]
+            tgt = getattr(src_arr, "zarray_maybe_lazy", None)
+            if tgt is None or "target_chunks" not in kw:
+                raise LoweringError(f"op {op}: merge_chunks without its side input / target chunks")
+            src = self.array(tgt, src_arr.name)
+            names = [k[0] for k in keys]
+            block_arg = next((i for i, n in enumerate(names)
+                              if isinstance(reads[n].array, VirtualOffsetsArray)), None)
+            if block_arg is None:
+                raise LoweringError(f"op {op}: map_direct without its block offsets argument")
+            from ..core.ops import _merged_region
+
+            leaf = ir.Region(src_arr.name, src.dtype, tuple(range(src.ndim)),
+                             _merged_region(tuple(tuple(c) for c in kw["target_chunks"])), block_arg, target=src)
+            return ir.ExprProgram(ndim=out.ndim, nargs=len(keys), outputs=leaf,
+                                  out_axes=tuple(range(out.ndim)), name="map_direct")
+        if wrappers:
+            return None  # other block_id / map_direct functions: traced (random) or refused
+        if len(keys) != 1 or not isinstance(keys[0], tuple):
+            return None
+        x = reads[keys[0][0]].array
+        from .. import chunkfuncs as CF
+
+        reductions = {"_mean_func": CF._mean_func, "_mean_combine": CF._mean_combine,
+                      "_nanmean_func": CF._nanmean_func, "_nanmean_combine": CF._nanmean_combine}
+        red = None
+        if bmod.startswith("cubed") and bname in reductions:
+            red = reductions[bname]
+        elif bname in _NUMPY_REDUCTION_NAMES and "axis" in kw and (
+                bmod.startswith("numpy") or bmod.startswith("array_api_compat") or bmod.startswith("cubed")):
+            red = CF.as_chunk_reduction(getattr(np, bname))
+        if red is not None:
+            axis = kw["axis"]
+            axis = (axis,) if isinstance(axis, int) else tuple(axis)
+            extra = {k: v for k, v in kw.items() if k not in ("axis", "keepdims")}
+            return red.program(x.ndim, x.dtype, axis, keepdims=bool(kw.get("keepdims", True)), **extra)
+        if bmod.startswith("cubed") and bname in ("_mean_aggregate", "_nanmean_aggregate"):
+            return CF._mean_aggregate.program(x.ndim, x.dtype)
+        if bname == "squeeze" and "axis" in kw:
+            axis = kw["axis"]
+            axis = (axis,) if isinstance(axis, int) else tuple(axis)
+            axes = tuple(range(x.ndim))
+            outputs = ir.Arg(0, x.dtype, axes) if not x.dtype.names else \
+                tuple((f, ir.Arg(0, x.dtype[f], axes, field=f)) for f in x.dtype.names)
+            return ir.ExprProgram(ndim=x.ndim, nargs=1, outputs=outputs,
+                                  out_axes=tuple(d for d in axes if d not in axis), name="squeeze")
+        return None
 
     def _check_alignment(self, op, cfg, arrays, out):
         """The trailing-dims (numpy broadcasting) index mapping the traced
@@ -248,17 +342,62 @@ class _Converter:
             op = create_arrays_op(devs, meta["allowed_mem"], meta["reserved_mem"])
             return PrimitiveOperation(pipeline=op.pipeline, target_array=None, **meta)
         if fname == "apply_blockwise":
-            reads = {n: self.proxy(px, n) for n, px in cfg.reads_map.items()}
-            write = self.proxy(cfg.write, name)
-            prog = self.program(name, cfg, reads, write)
-            spec = BlockwiseSpec(cfg.block_function, prog, cfg.function_nargs, reads, write)
-            pipe = CubedPipeline(apply_blockwise, p.name, p.mappable, spec)
-            return PrimitiveOperation(pipeline=pipe, target_array=write.array, **meta)
+            return self.blockwise(name, p, meta)
         if fname == "copy_read_to_write":
             spec = CubedCopySpec(self.proxy(cfg.read, name + "-read"), self.proxy(cfg.write, name))
             pipe = CubedPipeline(copy_read_to_write, p.name, p.mappable, spec)
             return PrimitiveOperation(pipeline=pipe, target_array=spec.write.array, **meta)
         raise LoweringError(f"op {name}: reference stage function {fname or p.function!r} is not supported")
+
+
+# ------------------------------------------------------------------ function anatomy
+_NUMPY_REDUCTION_NAMES = {"sum", "prod", "max", "min", "nansum", "nanmax", "nanmin", "all", "any"}
+
+
+def _cells(fn):
+    code = getattr(fn, "__code__", None)
+    if code is None or not fn.__closure__:
+        return {}
+    out = {}
+    for n, c in zip(code.co_freevars, fn.__closure__):
+        try:
+            out[n] = c.cell_contents
+        except ValueError:
+            pass
+    return out
+
+
+def _fused_parts(fn):
+    """("fuse", (pipeline1, pipeline2)) / ("fuse_multiple", (pipeline,
+    predecessor pipelines)) for the reference's fused chunk functions, else
+    None."""
+    if getattr(fn, "__name__", "") != "fused_func":
+        return None
+    cells = _cells(fn)
+    if "pipeline1" in cells and "pipeline2" in cells:
+        return "fuse", (cells["pipeline1"], cells["pipeline2"])
+    if "pipeline" in cells and "predecessor_pipelines" in cells:
+        return "fuse_multiple", (cells["pipeline"], list(cells["predecessor_pipelines"]))
+    return None
+
+
+def _unwrap(fn):
+    """(base function, merged partial keywords, wrappers): through
+    ``functools.partial`` layers and map_blocks' / map_direct's ``wrap``
+    closures (core/ops.py:531-560, 680-697) down to the chunk function."""
+    kw = {}
+    wrappers = []
+    for _ in range(16):
+        if isinstance(fn, functools.partial):
+            kw = {**(fn.keywords or {}), **kw}
+            fn = fn.func
+            continue
+        if getattr(fn, "__name__", "") == "wrap" and "func" in _cells(fn):
+            wrappers.append(fn)
+            fn = _cells(fn)["func"]
+            continue
+        break
+    return fn, kw, wrappers
 
 
 # ------------------------------------------------------------------ random
@@ -299,54 +438,6 @@ def _random_leaf(f, out_chunks, shape, dtype):
         return tracing._Proxy(leaf, nd)
 
     return standin
-
-
-class _random_standins:
-    """Context: every reference random chunk function reachable from ``fn``
-    (directly, or inside the ``fuse``/``fuse_multiple`` closures through the
-    fused pipelines' BlockwiseSpecs) is swapped for its Philox stand-in while
-    the function is traced, and restored afterwards."""
-
-    def __init__(self, fn):
-        self.fn = fn
-        self.swapped = []
-
-    def __enter__(self):
-        seen = set()
-
-        def visit(obj, depth=0):
-            if id(obj) in seen or depth > 64:
-                return
-            seen.add(id(obj))
-            if isinstance(obj, functools.partial):
-                visit(obj.func, depth + 1)
-                for a in obj.args:
-                    visit(a, depth + 1)
-                for a in (obj.keywords or {}).values():
-                    visit(a, depth + 1)
-            elif callable(obj) and getattr(obj, "__closure__", None):
-                for cell in obj.__closure__:
-                    try:
-                        visit(cell.cell_contents, depth + 1)
-                    except ValueError:
-                        pass
-            cfg = getattr(obj, "config", None)
-            if cfg is not None and hasattr(cfg, "function") and hasattr(cfg, "write"):
-                if _is_reference_random(cfg.function):
-                    w = cfg.write.array
-                    new = _random_leaf(cfg.function, cfg.write.chunks, w.shape, w.dtype)
-                    self.swapped.append((cfg, cfg.function))
-                    object.__setattr__(cfg, "function", new)
-                else:
-                    visit(cfg.function, depth + 1)
-
-        visit(self.fn)
-        return self
-
-    def __exit__(self, *exc):
-        for cfg, f in reversed(self.swapped):
-            object.__setattr__(cfg, "function", f)
-        return False
 
 
 # ------------------------------------------------------------------ run

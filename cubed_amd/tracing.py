@@ -53,6 +53,8 @@ class _Proxy:
             x = _lift(args[0])
             dt = np.dtype(kwargs["dtype"]) if kwargs.get("dtype") is not None else x.dtype
             return _Proxy(ir.Const(np.array(fill).astype(dt).item(), dt), x.ndim)
+        if func is getattr(np, "astype", None) and len(args) >= 2 and set(kwargs) <= {"copy"}:
+            return _lift(args[0]).astype(args[1])
         if func is np.where and not kwargs:
             c, a, b = (_lift(x) for x in args)
             dt = np.result_type(_np_like(args[1]), _np_like(args[2]))

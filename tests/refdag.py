@@ -278,3 +278,96 @@ def example_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20), rechunk_t
     p.add(sop, sname, [mname, one])
     out = p.rechunk(sname, rechunk_to)
     return p.finalize(), out, sname
+
+
+# -- reductions (array_api/statistical_functions.py:54-100, core/ops.py:646-903) --
+def _ref_fn(name, module):
+    def f(*a, **k):
+        raise AssertionError("reference chunk functions never run on the MI355X executor")
+
+    f.__name__ = f.__qualname__ = name
+    f.__module__ = module
+    return f
+
+
+_mean_func = _ref_fn("_mean_func", "cubed.array_api.statistical_functions")
+_mean_combine = _ref_fn("_mean_combine", "cubed.array_api.statistical_functions")
+_mean_aggregate = _ref_fn("_mean_aggregate", "cubed.array_api.statistical_functions")
+_copy_chunk = _ref_fn("_copy_chunk", "cubed.core.ops")
+
+
+class RefArray:
+    """The side-input ``Array`` map_direct passes as ``arrays=``."""
+
+    def __init__(self, name, target):
+        self.name = name
+        self.zarray_maybe_lazy = target
+
+
+def map_direct_wrap(func):
+    def wrap(*a, block_id=None, **kw):
+        arrays = kw.pop("arrays")
+        return func(*(a + arrays), block_id=block_id, **kw)
+
+    return wrap
+
+
+def mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20)):
+    """``xp.mean(random(shape, chunks), axis=0)`` as the reference plans it at
+    2 GB under its default optimizer: random fused into the per-chunk
+    ``_mean_func`` (one op, a task per chunk), then ONE op fusing
+    merge_chunks (map_direct over the partials), ``_mean_combine``,
+    ``_mean_aggregate`` and ``squeeze`` -- the ``merge_chunks -> combine ->
+    aggregate -> squeeze`` chain simple_optimize_dag fuses
+    (core/optimization.py:11-68)."""
+    p = RefPlan(work_dir)
+    idt = np.dtype([("n", np.int64), ("total", np.float64)])
+    nr = -(-shape[0] // chunks[0])
+    rop, rname, rsrcs = p.random(shape, chunks, root_seed)
+    # per-chunk reduce
+    pname = p._name("array")
+    pshape, pchunks = (nr, shape[1]), (1, chunks[1])
+    mop, ptarget = p.blockwise_op(functools.partial(_mean_func, axis=(0,), keepdims=True,
+                                                    dtype=[("n", np.int64), ("total", np.float64)]),
+                                  pname, pshape, idt, pchunks, [(rname, p.g.nodes[rname]["target"])])
+    # the partials' block function maps the output key straight to the input key
+    a_op = fuse(rop, mop)
+    p.g.remove_node(rname)
+    p.lazy = [t for t in p.lazy if t is not rop.target_array]
+    p.add(a_op, pname, rsrcs)
+    # merge_chunks: map_direct(_copy_chunk, partials, target_chunks) -> (nr, c1) chunks
+    tchunks = (nr, chunks[1])
+    nb = numblocks(pshape, tchunks)
+    tnorm = tuple(tuple(min(c, s - i) for i in range(0, s, c)) for s, c in zip(pshape, tchunks))
+    empty, offs = p._name("empty"), p._name("offsets")
+    p._array(empty, VirtualEmptyArray(pshape, idt, tchunks))
+    p._array(offs, VirtualOffsetsArray(nb))
+    mfn = functools.partial(func_with_block_id(map_direct_wrap(_copy_chunk), nb),
+                            arrays=(RefArray(pname, ptarget),), target_chunks=tnorm)
+    gname = p._name("array")
+    gop, _ = p.blockwise_op(mfn, gname, pshape, idt, tchunks,
+                            [(empty, p.g.nodes[empty]["target"]), (offs, p.g.nodes[offs]["target"])])
+    # combine -> (1, shape[1]) chunks (1, c1)
+    cname = p._name("array")
+    cop, _ = p.blockwise_op(functools.partial(_mean_combine, axis=(0,), keepdims=True,
+                                              dtype=[("n", np.int64), ("total", np.float64)]),
+                            cname, (1, shape[1]), idt, (1, chunks[1]), [(gname, p.g.nodes[gname]["target"])])
+    # aggregate (f64) and squeeze
+    aname = p._name("array")
+    agg, _ = p.blockwise_op(functools.partial(_mean_aggregate), aname, (1, shape[1]), np.float64,
+                            (1, chunks[1]), [(cname, p.g.nodes[cname]["target"])])
+    sname = p._name("array")
+    sq, starget = p.blockwise_op(functools.partial(np.squeeze, axis=(0,)), sname, (shape[1],), np.float64,
+                                 (chunks[1],), [(aname, p.g.nodes[aname]["target"])])
+    # squeeze's key function: output block (j,) reads aggregate block (0, j)
+    sq_spec = BlockwiseSpec(lambda k: [(aname, 0, k[1])], sq.pipeline.config.function, 1,
+                            sq.pipeline.config.reads_map, sq.pipeline.config.write)
+    sq = PrimitiveOperation(CubedPipeline(apply_blockwise, "apply_blockwise-sq", sq.pipeline.mappable, sq_spec),
+                            starget, 0, p.MEM, 0, sq.num_tasks, True)
+    b_op = fuse(fuse(fuse(gop, cop), agg), sq)
+    for n in (gname, cname, aname):
+        t = p.g.nodes[n]["target"]
+        p.g.remove_node(n)
+        p.lazy = [x for x in p.lazy if x is not t]
+    name = p._op(b_op, sname, [empty, offs, pname], b_op.num_tasks)
+    return p.finalize(), sname, pname, name

@@ -193,3 +193,50 @@ def test_reference_random_unfused_on_the_gpu(tmp_path, gpu_executor):
     x = R.random_array((30, 20), (7, 20), seed)
     np.testing.assert_array_equal(ZarrV2Array.open(str(tmp_path / f"{rname}.zarr"))[...], x)
     np.testing.assert_array_equal(ZarrV2Array.open(str(tmp_path / f"{name}.zarr"))[...], np.sqrt(x))
+
+
+def test_reference_mean_plan_converts_to_one_chain(tmp_path, built, dry):
+    """The reference's mean plan (random fused into _mean_func; merge_chunks
+    + _mean_combine + _mean_aggregate + squeeze fused into one op): the
+    fused closures are taken apart and re-fused, the reduction functions map
+    to the IR reductions, and the executor runs the whole chain as fused
+    launches (no host code, nothing refused)."""
+    dag, out, partials, op = refdag.mean_plan(tmp_path, _seed(8))
+    conv = RD.convert_reference_dag(dag)
+    prog = conv.dag.nodes[op]["pipeline"].config.function
+    assert isinstance(prog, ir.ExprProgram)
+    first = [d for n, d in conv.dag.nodes(data=True) if d.get("pipeline") is not None
+             and n != op and isinstance(d["pipeline"].config, RD.BlockwiseSpec)]
+    assert len(first) == 1 and first[0]["pipeline"].config.function.reduce is not None
+    dry.launched.clear()
+    dry.execute_dag(conv.dag, array_names=[out])
+    assert dry.launched and all(type(l).__name__ in ("FusedLaunch",) for l in dry.launched)
+
+
+@pytest.mark.gpu
+def test_reference_mean_plan_on_the_gpu(tmp_path, gpu_executor):
+    """mean(random(40, 60), axis=0) built as the reference builds it: the
+    result written to its Zarr store, rtol 1e-12 against the oracle's f64
+    column means of the same numpy Philox blocks; TaskEndEvents carry the
+    reference's task counts (12 per-chunk tasks, 3 merge tasks)."""
+    from cubed_amd.runtime.types import Callback
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    class Rec(Callback):
+        def __init__(self):
+            self.events = []
+
+        def on_task_end(self, event):
+            self.events.append(event)
+
+    seed = _seed(9)
+    dag, out, partials, op = refdag.mean_plan(tmp_path, seed, (40, 60), (10, 20))
+    rec = Rec()
+    gpu_executor.execute_dag(dag, callbacks=[rec], array_names=[out])
+    x = R.random_array((40, 60), (10, 20), seed)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    assert got.shape == (60,) and got.dtype == np.float64
+    np.testing.assert_allclose(got, x.mean(axis=0), rtol=1e-12, atol=0)
+    counts = {e.array_name: e.num_tasks for e in rec.events}
+    assert counts.get(op) == 3
