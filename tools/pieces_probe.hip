@@ -69,6 +69,39 @@ __global__ __launch_bounds__(256) void k_pieces(const float* __restrict__ x, dou
   }
 }
 
+// the library's geometry for the same work (stream_body, W = 1): one task
+// per 1000-column output block, its 50000 rows split S ways (contiguous row
+// ranges crossing row chunks), a runtime row stride, partials per split
+template <int U, int S>
+__global__ __launch_bounds__(256) void k_libshape(const float* __restrict__ x, double* __restrict__ part,
+                                                   long stride) {
+  const long g = blockIdx.x;
+  const int s = (int)(g % S);
+  const long j = g / S;
+  const long r0 = NR * s / S, r1 = NR * (s + 1) / S;
+  const int c4 = threadIdx.x;
+  if (c4 * 4 >= CB) return;
+  const long col = j * CB + c4 * 4;
+  const float* p = x + r0 * stride + col;
+  double acc[4] = {0, 0, 0, 0};
+  long r = r0;
+  for (; r + U <= r1; r += U) {
+    f32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load((const G f32x4*)(p + u * stride));
+    p += U * stride;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w;
+    }
+  }
+  for (; r < r1; ++r, p += stride) {
+    const f32x4 v = __builtin_nontemporal_load((const G f32x4*)p);
+    acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+  }
+  for (int e = 0; e < 4; ++e) part[(long)s * NC + col + e] = acc[e];
+}
+
 // contiguous read-only stream of the same bytes (the ceiling)
 __global__ __launch_bounds__(256) void k_read(const f32x4* __restrict__ x, long n4, double* out) {
   double a = 0;
@@ -90,7 +123,7 @@ int main(int argc, char** argv) {
   float* x;
   double *part, *ref;
   CHECK(hipMalloc(&x, NR * NC * 4));
-  CHECK(hipMalloc(&part, NI * NC * 8));
+  CHECK(hipMalloc(&part, 64 * NC * 8));
   CHECK(hipMalloc(&ref, NI * NC * 8));
   hipLaunchKernelGGL(k_fill, dim3(8192), dim3(256), 0, 0, x, NR * NC, 7u);
   CHECK(hipDeviceSynchronize());
@@ -149,5 +182,23 @@ int main(int argc, char** argv) {
   run("i-major xcd-remap nt U8, 2 pieces/WG", k_pieces<true, true, true, 8, 2>, 2, false);
   run("i-major xcd-remap cached U20, 2 pieces/WG", k_pieces<true, true, false, 20, 2>, 2, false);
   run("j-major plain nt U8 (again)", k_pieces<false, false, true, 8, 1>, 1, false);
+  auto runlib = [&](const char* name, void (*k)(const float*, double*, long), int S) {
+    float best = 1e30f;
+    for (int r = 0; r < reps + 1; ++r) {
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k, dim3(NJ * S), dim3(256), 0, 0, x, part, NC);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-44s %.3f ms %6.0f GB/s\n", name, best, NR * NC * 4 / (best * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+  runlib("library shape U8, 19 splits (950 WGs)", k_libshape<8, 19>, 19);
+  runlib("library shape U8, 50 splits (2500 WGs)", k_libshape<8, 50>, 50);
+  runlib("library shape U8, 64 splits (3200 WGs)", k_libshape<8, 64>, 64);
+  runlib("library shape U16, 19 splits", k_libshape<16, 19>, 19);
   return 0;
 }
