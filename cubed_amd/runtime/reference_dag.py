@@ -23,8 +23,11 @@ a DAG (stage functions from the ``cubed`` package) and hands it here:
   reduction functions (``_mean_func``/``_mean_combine``/``_mean_aggregate``,
   the nan variants, ``nxp.sum``/``max``/... with ``axis``/``keepdims``/
   ``dtype``), ``squeeze``, merge_chunks' ``_copy_chunk`` under map_direct (a
-  ``Region`` leaf), and ``random`` (``map_blocks(_random, ...)`` under
-  ``func_with_block_id``, cubed/random.py:13-36) the bit-exact Philox leaf;
+  ``Region`` leaf), matmul's ``_matmul`` chunk product and ``_chunk_sum``
+  (linear_algebra_functions.py:13-78: the executor runs the product and its
+  k-sum rounds as one chained GEMM), and ``random`` (``map_blocks(_random,
+  ...)`` under ``func_with_block_id``, cubed/random.py:13-36) the bit-exact
+  Philox leaf;
 * any other chunk function is lowered by tracing it on proxies
   (``cubed_amd.tracing``): elementwise numpy / ``array_api_compat`` calls,
   Python operators, ``astype``, ``where``, with ``functools.partial``
@@ -39,8 +42,8 @@ the reference's ``compute()`` reads them back.
 
 What is not lowered raises ``LoweringError`` naming the op: user chunk
 functions that are not elementwise, contractions with nested block keys
-(matmul / tensordot / partial_reduce), ``index``'s side-input reads, and
-functions taking ``block_id`` other than ``random``.  The reference cannot be imported in
+(tensordot / partial_reduce), ``index``'s side-input reads, and functions
+taking ``block_id`` other than ``random``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -241,13 +244,17 @@ class _Converter:
                                   out_axes=tuple(range(out.ndim)), name="map_direct")
         if wrappers:
             return None  # other block_id / map_direct functions: traced (random) or refused
+        if bname == "_matmul" and bmod.startswith("cubed") and len(keys) == 2:
+            # per (i, k, j) task: A_ik @ B_kj with a unit k dim (linear_algebra_functions.py:62-64)
+            return ir.MatmulProgram(out_dtype=np.dtype(out.dtype))
         if len(keys) != 1 or not isinstance(keys[0], tuple):
             return None
         x = reads[keys[0][0]].array
         from .. import chunkfuncs as CF
 
         reductions = {"_mean_func": CF._mean_func, "_mean_combine": CF._mean_combine,
-                      "_nanmean_func": CF._nanmean_func, "_nanmean_combine": CF._nanmean_combine}
+                      "_nanmean_func": CF._nanmean_func, "_nanmean_combine": CF._nanmean_combine,
+                      "_chunk_sum": CF._chunk_sum}
         red = None
         if bmod.startswith("cubed") and bname in reductions:
             red = reductions[bname]

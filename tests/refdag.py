@@ -371,3 +371,68 @@ def mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20)):
         p.lazy = [x for x in p.lazy if x is not t]
     name = p._op(b_op, sname, [empty, offs, pname], b_op.num_tasks)
     return p.finalize(), sname, pname, name
+
+
+# -- matmul (array_api/linear_algebra_functions.py:13-78) -----------------------
+_matmul = _ref_fn("_matmul", "cubed.array_api.linear_algebra_functions")
+_chunk_sum = _ref_fn("_chunk_sum", "cubed.array_api.linear_algebra_functions")
+
+
+def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20):
+    """``xp.matmul(A, B)`` of two random f64 arrays as the reference plans it
+    under its default optimizer: the (i, k, j) chunk products ``_matmul``
+    fused with the first ``_chunk_sum`` over the unit k dim, then one op
+    fusing merge_chunks (map_direct over the k partials), the combining
+    ``_chunk_sum`` and ``squeeze``."""
+    p = RefPlan(work_dir)
+    aop, aname, asrcs = p.random((m, k), (cm, ck), seed_a)
+    p.add(aop, aname, asrcs)
+    bop, bname, bsrcs = p.random((k, n), (ck, cn), seed_b)
+    p.add(bop, bname, bsrcs)
+    kb = -(-k // ck)
+    pshape, pchunks = (m, kb, n), (cm, 1, cn)
+    A, B = p.g.nodes[aname]["target"], p.g.nodes[bname]["target"]
+    prod_name = p._name("array")
+    prod_t = p.lazy_target(prod_name, pshape, np.float64, pchunks)
+    spec = BlockwiseSpec(lambda key: [(aname, key[1], key[2]), (bname, key[2], key[3])], functools.partial(_matmul),
+                         2, {aname: CubedArrayProxy(A, A.chunks), bname: CubedArrayProxy(B, B.chunks)},
+                         CubedArrayProxy(prod_t, pchunks))
+    ntasks = int(np.prod(numblocks(pshape, pchunks)))
+    mm = PrimitiveOperation(CubedPipeline(apply_blockwise, p._name("apply_blockwise"), [], spec), prod_t,
+                            0, p.MEM, 0, ntasks, True)
+    sname = p._name("array")
+    sop, st = p.blockwise_op(functools.partial(_chunk_sum, axis=(1,), keepdims=True, dtype=np.float64),
+                             sname, pshape, np.float64, pchunks, [(prod_name, prod_t)])
+    first = fuse(mm, sop)
+    p.g.remove_node(prod_name)
+    p.lazy = [t for t in p.lazy if t is not prod_t]
+    p.add(first, sname, [aname, bname])
+    # merge the kb partials along axis 1, combine, squeeze
+    tchunks = (cm, kb, cn)
+    nb = numblocks(pshape, tchunks)
+    tnorm = tuple(tuple(min(c, s - i) for i in range(0, s, c)) for s, c in zip(pshape, tchunks))
+    empty, offs = p._name("empty"), p._name("offsets")
+    p._array(empty, VirtualEmptyArray(pshape, np.float64, tchunks))
+    p._array(offs, VirtualOffsetsArray(nb))
+    mfn = functools.partial(func_with_block_id(map_direct_wrap(_copy_chunk), nb),
+                            arrays=(RefArray(sname, st),), target_chunks=tnorm)
+    gname = p._name("array")
+    gop, _ = p.blockwise_op(mfn, gname, pshape, np.float64, tchunks,
+                            [(empty, p.g.nodes[empty]["target"]), (offs, p.g.nodes[offs]["target"])])
+    cname = p._name("array")
+    cop, _ = p.blockwise_op(functools.partial(_chunk_sum, axis=(1,), keepdims=True, dtype=np.float64),
+                            cname, (m, 1, n), np.float64, pchunks, [(gname, p.g.nodes[gname]["target"])])
+    qname = p._name("array")
+    qop, qt = p.blockwise_op(functools.partial(np.squeeze, axis=(1,)), qname, (m, n), np.float64, (cm, cn),
+                             [(cname, p.g.nodes[cname]["target"])])
+    q_spec = BlockwiseSpec(lambda key: [(cname, key[1], 0, key[2])], qop.pipeline.config.function, 1,
+                           qop.pipeline.config.reads_map, qop.pipeline.config.write)
+    qop = PrimitiveOperation(CubedPipeline(apply_blockwise, "apply_blockwise-sq", [], q_spec), qt, 0, p.MEM, 0,
+                             qop.num_tasks, True)
+    second = fuse(fuse(gop, cop), qop)
+    for nm in (gname, cname):
+        t = p.g.nodes[nm]["target"]
+        p.g.remove_node(nm)
+        p.lazy = [x for x in p.lazy if x is not t]
+    op = p._op(second, qname, [empty, offs, sname], second.num_tasks)
+    return p.finalize(), qname, aname, bname, op

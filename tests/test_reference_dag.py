@@ -240,3 +240,36 @@ def test_reference_mean_plan_on_the_gpu(tmp_path, gpu_executor):
     np.testing.assert_allclose(got, x.mean(axis=0), rtol=1e-12, atol=0)
     counts = {e.array_name: e.num_tasks for e in rec.events}
     assert counts.get(op) == 3
+
+
+def test_reference_matmul_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
+    """The reference matmul plan (_matmul fused with the first _chunk_sum;
+    merge_chunks + _chunk_sum + squeeze fused): the product becomes the
+    chunk GEMM program and the executor runs one chained GEMM launch (the
+    partial-product arrays elided), as for cubed_amd's own matmul."""
+    dag, out, a, b, op = refdag.matmul_plan(tmp_path, _seed(10), _seed(11))
+    conv = RD.convert_reference_dag(dag)
+    progs = [d["pipeline"].config.function for _, d in conv.dag.nodes(data=True)
+             if d.get("pipeline") is not None and isinstance(d["pipeline"].config, RD.BlockwiseSpec)]
+    assert any(isinstance(p, ir.GemmThenProgram) for p in progs)
+    dry.launched.clear()
+    dry.execute_dag(conv.dag, array_names=[out])
+    kinds = [type(l).__name__ for l in dry.launched]
+    assert kinds.count("GemmLaunch") == 1
+
+
+@pytest.mark.gpu
+def test_reference_matmul_plan_on_the_gpu(tmp_path, gpu_executor):
+    """matmul of two random f64 arrays built as the reference builds it:
+    the result (written to its Zarr store) against the f64 product of the
+    oracle's Philox blocks, rtol 1e-12."""
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    sa, sb = _seed(12), _seed(13)
+    dag, out, a, b, op = refdag.matmul_plan(tmp_path, sa, sb)
+    gpu_executor.execute_dag(dag, array_names=[out])
+    A = R.random_array((60, 80), (20, 20), sa)
+    B = R.random_array((80, 40), (20, 20), sb)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    np.testing.assert_allclose(got, A @ B, rtol=1e-12, atol=0)
