@@ -23,7 +23,8 @@ a DAG (stage functions from the ``cubed`` package) and hands it here:
   reduction functions (``_mean_func``/``_mean_combine``/``_mean_aggregate``,
   the nan variants, ``nxp.sum``/``max``/... with ``axis``/``keepdims``/
   ``dtype``), ``squeeze``, merge_chunks' ``_copy_chunk`` under map_direct (a
-  ``Region`` leaf), matmul's ``_matmul`` chunk product and ``_chunk_sum``
+  ``Region`` leaf), ``index``'s ``_read_index_chunk`` (a Region leaf with the
+  selection), matmul's ``_matmul`` chunk product and ``_chunk_sum``
   (linear_algebra_functions.py:13-78: the executor runs the product and its
   k-sum rounds as one chained GEMM), and ``random`` (``map_blocks(_random,
   ...)`` under ``func_with_block_id``, cubed/random.py:13-36) the bit-exact
@@ -42,8 +43,8 @@ the reference's ``compute()`` reads them back.
 
 What is not lowered raises ``LoweringError`` naming the op: user chunk
 functions that are not elementwise, contractions with nested block keys
-(tensordot / partial_reduce), ``index``'s side-input reads, and functions
-taking ``block_id`` other than ``random``.  The reference cannot be imported in
+(tensordot / partial_reduce), and functions taking ``block_id`` other
+than ``random``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -242,6 +243,8 @@ class _Converter:
                              _merged_region(tuple(tuple(c) for c in kw["target_chunks"])), block_arg, target=src)
             return ir.ExprProgram(ndim=out.ndim, nargs=len(keys), outputs=leaf,
                                   out_axes=tuple(range(out.ndim)), name="map_direct")
+        if bname == "_read_index_chunk" and bmod.startswith("cubed"):
+            return self._index_program(op, kw, keys, reads, out)
         if wrappers:
             return None  # other block_id / map_direct functions: traced (random) or refused
         if bname == "_matmul" and bmod.startswith("cubed") and len(keys) == 2:
@@ -277,6 +280,43 @@ class _Converter:
             return ir.ExprProgram(ndim=x.ndim, nargs=1, outputs=outputs,
                                   out_axes=tuple(d for d in axes if d not in axis), name="squeeze")
         return None
+
+    def _index_program(self, op, kw, keys, reads, out):
+        """``index``'s map_direct function (core/ops.py:374-517): output block
+        b reads ``x.oindex[_target_chunk_selection(target_chunks, b,
+        selection)]`` -- a Region leaf over the side input with this package's
+        ``_read_index_region`` (same selection arithmetic)."""
+        from ..core.ops import _read_index_region
+
+        src_arr = kw.get("arrays", (None,))[0]
+        tgt = getattr(src_arr, "zarray_maybe_lazy", None)
+        if tgt is None or "selection" not in kw or "target_chunks" not in kw:
+            raise LoweringError(f"op {op}: index without its side input / selection")
+        src = self.array(tgt, src_arr.name)
+        norm, axes, k = [], [], 0
+        for d, sel in enumerate(kw["selection"]):
+            n = src.shape[d]
+            if isinstance(sel, slice):
+                start, stop, step = sel.indices(n)
+                norm.append(slice(start, stop, step))
+                axes.append(k)
+                k += 1
+            elif isinstance(sel, (list, tuple)):
+                norm.append([int(v) + n if int(v) < 0 else int(v) for v in sel])
+                axes.append(k)
+                k += 1
+            else:
+                v = int(sel)
+                norm.append(v + n if v < 0 else v)
+                axes.append(None)
+        names = [kk[0] for kk in keys]
+        block_arg = next((i for i, nm in enumerate(names) if isinstance(reads[nm].array, VirtualOffsetsArray)), None)
+        if block_arg is None:
+            raise LoweringError(f"op {op}: map_direct without its block offsets argument")
+        region = _read_index_region(tuple(norm), tuple(tuple(c) for c in kw["target_chunks"]))
+        leaf = ir.Region(src_arr.name, src.dtype, tuple(axes), region, block_arg, target=src)
+        return ir.ExprProgram(ndim=out.ndim, nargs=len(keys), outputs=leaf, out_axes=tuple(range(out.ndim)),
+                              name="map_direct")
 
     def _check_alignment(self, op, cfg, arrays, out):
         """The trailing-dims (numpy broadcasting) index mapping the traced

@@ -436,3 +436,42 @@ def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20)
         p.lazy = [x for x in p.lazy if x is not t]
     op = p._op(second, qname, [empty, offs, sname], second.num_tasks)
     return p.finalize(), qname, aname, bname, op
+
+
+# -- index (core/ops.py:374-517) ------------------------------------------------
+_read_index_chunk = _ref_fn("_read_index_chunk", "cubed.core.ops")
+
+
+def index_plan(work_dir, seed, shape=(30, 8), chunks=(10, 8), selection=(slice(1, None, None),)):
+    """``-(random(shape)[selection])``: index's map_direct op (target chunks
+    = the source chunk lengths along sliced dims, step 1) fused into the
+    ``negative`` that consumes it (in-degree 1)."""
+    p = RefPlan(work_dir)
+    rop, rname, rsrcs = p.random(shape, chunks, seed)
+    p.add(rop, rname, rsrcs)
+    src = p.g.nodes[rname]["target"]
+    sel = tuple(selection) + (slice(None),) * (len(shape) - len(selection))
+    out_shape, out_chunks = [], []
+    for s, n, c in zip(sel, shape, chunks):
+        if isinstance(s, slice):
+            a, b, st = s.indices(n)
+            out_shape.append(max(0, (b - a + st - 1) // st))
+            out_chunks.append(max(c // st, 1))
+    out_shape, out_chunks = tuple(out_shape), tuple(out_chunks)
+    tnorm = tuple(tuple(min(c, s - i) for i in range(0, s, c)) for s, c in zip(out_shape, out_chunks))
+    nb = numblocks(out_shape, out_chunks)
+    empty, offs = p._name("empty"), p._name("offsets")
+    p._array(empty, VirtualEmptyArray(out_shape, np.float64, out_chunks))
+    p._array(offs, VirtualOffsetsArray(nb))
+    fn = functools.partial(func_with_block_id(map_direct_wrap(_read_index_chunk), nb),
+                           arrays=(RefArray(rname, src),), target_chunks=tnorm, selection=sel)
+    iname = p._name("array")
+    iop, it = p.blockwise_op(fn, iname, out_shape, np.float64, out_chunks,
+                             [(empty, p.g.nodes[empty]["target"]), (offs, p.g.nodes[offs]["target"])])
+    nname = p._name("array")
+    nop, _ = p.blockwise_op(np.negative, nname, out_shape, np.float64, out_chunks, [(iname, it)])
+    fused = fuse(iop, nop)
+    p.g.remove_node(iname)
+    p.lazy = [t for t in p.lazy if t is not it]
+    p._op(fused, nname, [empty, offs, rname], fused.num_tasks)
+    return p.finalize(), nname, rname
