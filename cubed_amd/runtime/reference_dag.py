@@ -52,6 +52,7 @@ with the same class names and attributes (tests/test_reference_dag.py).
 from __future__ import annotations
 
 import functools
+import os
 import weakref
 from typing import Dict
 
@@ -111,8 +112,6 @@ def _store_path(t):
     else:
         raise LoweringError(f"Zarr target {t!r}: only local directory stores are supported")
     sub = getattr(t, "path", "") if type(t).__name__ != "LazyZarrArray" else ""
-    import os
-
     return os.path.join(base, sub) if sub else base
 
 
