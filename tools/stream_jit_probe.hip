@@ -102,7 +102,34 @@ int main(int argc, char** argv) {
     printf("%-40s best %.3f ms mean %.3f ms %6.0f GB/s\n", name, best, sum / reps, NR * NC * 4 / (best * 1e-3) / 1e9);
     fflush(stdout);
   };
+  // hipRTC-built code objects of the same source (argv[2], argv[3], ...): the
+  // library's own build path
+  struct Mod { const char* path; hipFunction_t fn; };
+  std::vector<Mod> mods;
+  for (int a = 2; a < argc; ++a) {
+    FILE* f = fopen(argv[a], "rb");
+    if (!f) { printf("cannot open %s\n", argv[a]); return 1; }
+    std::vector<char> buf;
+    char tmp[65536];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+    fclose(f);
+    hipModule_t m;
+    CHECK(hipModuleLoadData(&m, buf.data()));
+    hipFunction_t fn;
+    CHECK(hipModuleGetFunction(&fn, m, "jit_stream"));
+    mods.push_back({argv[a], fn});
+  }
   for (int rep = 0; rep < 2; ++rep) {
+    for (auto& md : mods) {
+      timeit(md.path, [&] {
+        struct { const cubed_task_t* t; int64_t nt; int64_t bpt; int32_t ns; int32_t pad; cubed::Acc* ws; int64_t mk; } args;
+        args.t = dt; args.nt = NJ; args.bpt = 1; args.ns = S; args.pad = 0; args.ws = ws; args.mk = CB;
+        size_t sz = sizeof(args);
+        void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+        CHECK(hipModuleLaunchKernel(md.fn, NJ * S, 1, 1, 256, 1, 1, 0, 0, nullptr, cfg));
+      });
+    }
     timeit("library JIT stream_body<f32,1,8,1>", [&] {
       hipLaunchKernelGGL(jit_stream, dim3(NJ * S), dim3(256), 0, 0, dt, (int64_t)NJ, (int64_t)1, (int32_t)S, ws,
                          (int64_t)CB);
