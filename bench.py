@@ -574,7 +574,8 @@ def matmul_extra(args, ex, rank, world, dt_name):
     m = xp.matmul(A, B)
     plan = arrays_to_plan(m)
     step = step_fn(plan, ex, [m], (A, B))
-    step()
+    step()  # records the launch schedule
+    step()  # first replay (one-off host costs) stays out of the two timed steps
     dt, summ = timed_launches(ex, step, 2, world)
     flop = 2.0 * n ** 3
     gemm = [v for k, v in summ.items() if k[2] == "GemmLaunch"]
