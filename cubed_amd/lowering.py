@@ -943,6 +943,7 @@ class Lowerer:
         kinds = [self.leaf_kind(l) for l in leaves]
         gathers = []
         group_start = None
+        merge_ok = MERGE_ROWS and not partials and all(k == LEAF_ARRAY for k in kinds)
         if rows_fn is not None:
             res = rows_fn(leaves, kinds)
             rows, red_axes = res[0], res[1]
@@ -951,6 +952,8 @@ class Lowerer:
                 # rows of several groups (chain_piece_rows): partials + grouped finish
                 group_keys = res[2]
                 gathers += res[3]
+                if merge_ok:
+                    rows, group_keys = _merge_group_rows(rows, group_keys, red_axes, leaves)
                 starts = [i for i in range(len(group_keys)) if i == 0 or group_keys[i] != group_keys[i - 1]]
                 group_start = np.array(starts + [len(group_keys)], dtype=np.int64)
                 partials = partials or len(starts) < len(group_keys)
@@ -963,6 +966,8 @@ class Lowerer:
                                          structured_out, gathers)
                 rows += r
                 group_keys += gk
+            if merge_ok and program.reduce is not None and len(set(group_keys)) < len(group_keys):
+                rows, group_keys = _merge_group_rows(rows, group_keys, red_axes, leaves)
             if program.reduce is not None and len(set(group_keys)) < len(group_keys):
                 # pieces reduce into shared outputs: partials + grouped finish
                 partials = True
@@ -986,7 +991,17 @@ class Lowerer:
         P.ndim = layout.ndim
         P.nred = layout.nred
         P.mode = layout.mode
-        if _stream_ok(layout, leaves, kinds, P.vtype, check_outputs=not lifted):
+        stream = _stream_ok(layout, leaves, kinds, P.vtype, check_outputs=not lifted)
+        if stream and merge_ok and not partials and not lifted and \
+                (group_start is None or len(group_start) == len(rows) + 1):
+            out_isz = [target.field_dtype(n if structured_out else None).itemsize for n, _ in out_items]
+            merged = _merge_kept_runs(layout, [np.dtype(l.dtype).itemsize for l in leaves], out_isz)
+            if merged is not None:
+                layout = merged
+                rows = layout.rows
+                if group_start is not None:
+                    group_start = np.arange(len(rows) + 1, dtype=np.int64)
+        if stream:
             P.mode |= MODE_STREAM | _stream_groups_mode(P, len(rows), layout.max_kept)
         if partials:
             if P.nfields == 0:
@@ -1681,6 +1696,79 @@ def _stream_ok(layout: Layout, leaves, kinds, vtype, check_outputs=True) -> bool
             if check_outputs and st[-1] != 1:
                 return False
     return True
+
+
+MERGE_ROWS = True  # tests set False to run the unmerged task / piece rows
+
+
+def _merge_group_rows(rows, group_keys, red_axes, leaves):
+    """Rows of one output group (pieces of a task cut at source-chunk
+    boundaries, chain_piece_rows' per-chunk rows) that continue each other
+    along a reduced dim IN MEMORY -- the stacked row bands of one HBM array
+    are one run of addresses -- merged into one row per run: config 3's
+    read-through column block walks its 50000 rows as one row instead of 50
+    pieces combined by a grouped finish.  Only the association of the
+    (associative) field reductions changes.  Returns (rows, group keys)."""
+    from .chains import _try_merge
+
+    isz = [np.dtype(l.dtype).itemsize for l in leaves]
+    red = sorted(red_axes)
+    out_rows, out_keys = [], []
+    i = 0
+    while i < len(rows):
+        j = i
+        while j < len(rows) and group_keys[j] == group_keys[i]:
+            j += 1
+        acc = []
+        for r in rows[i:j]:
+            for a, q in enumerate(acc):
+                if q.obases != r.obases or q.ostrides != r.ostrides or \
+                        (q.key_lo, q.key_hi, q.block_offset) != (r.key_lo, r.key_hi, r.block_offset):
+                    continue
+                m = _try_merge(q, r, red, isz)
+                if m is None:
+                    m = _try_merge(r, q, red, isz)
+                if m is not None:
+                    acc[a] = m
+                    break
+            else:
+                acc.append(r)
+        out_rows += acc
+        out_keys += [group_keys[i]] * len(acc)
+        i = j
+    return out_rows, out_keys
+
+
+def _merge_kept_runs(layout: Layout, leaf_isz, out_isz):
+    """A streaming layout whose consecutive tasks continue each other along
+    the packed kept dim -- same reduced extents and strides, every leaf and
+    output base exactly one kept extent further on -- as fewer, wider tasks
+    (None when nothing merges).  The column blocks of one row-major array
+    read through an elided rechunk are such tasks: 50 tasks of 4000-B piece
+    rows that start mid-line become one task of whole 200000-B rows, so
+    workgroup boundaries fall on 128-B lines and no boundary line is fetched
+    twice.  Rows come back in kernel dims (identity groups); each output
+    element still sums the same rows of the same leaves."""
+    krows = []
+    for r in layout.rows:
+        ext, ls, os_ = _apply_groups(r, layout.groups)
+        krows.append(TaskRow(list(ext), list(r.bases), [list(s) for s in ls], list(r.obases),
+                             [list(s) for s in os_], r.key_lo, r.key_hi, r.block_offset))
+    out = [krows[0]]
+    for b in krows[1:]:
+        a = out[-1]
+        n = a.extent[-1]
+        if a.extent[:-1] == b.extent[:-1] and a.lstrides == b.lstrides and a.ostrides == b.ostrides and \
+                all(bb == ab + n * s for ab, bb, s in zip(a.bases, b.bases, leaf_isz)) and \
+                all(bb == ab + n * s for ab, bb, s in zip(a.obases, b.obases, out_isz)):
+            a.extent[-1] += b.extent[-1]
+        else:
+            out.append(b)
+    if len(out) == len(krows):
+        return None
+    nd = layout.ndim
+    return Layout(list(range(nd)), [[d] for d in range(nd)], nd, layout.nred, layout.mode, out,
+                  max(1, max(r.extent[-1] for r in out)), layout.max_red)
 
 
 def _groups_contiguous(group, d, order):

@@ -30,7 +30,13 @@ from .utils import (
     to_chunksize,
 )
 
-SLOT_ALIGN = 256  # bytes; keeps every chunk base 16-byte (dwordx4) aligned
+# bytes between chunk slots: four 8-byte elements, the alignment the
+# vectorised kernels need of every chunk base (lowering._vec_ok).  Slots are
+# otherwise packed end to end, so the stacked row bands of an array are one
+# run of addresses and consecutive output chunks continue each other -- the
+# executor walks such runs as single task rows (lowering._merge_group_rows /
+# _merge_kept_runs)
+SLOT_ALIGN = 32
 
 _GEOMETRY_ONLY = [False]
 

@@ -6,6 +6,7 @@ performance: how many launches a pipeline becomes, whether the streaming
 fast path is taken, and that reduction chains are fused into one pass.
 """
 
+import math
 import random
 
 import numpy as np
@@ -14,6 +15,7 @@ import pytest
 import cubed_amd as cubed
 import cubed_amd.array_api as xp
 import cubed_amd.random as crandom
+import cubed_amd.lowering as Lw
 from cubed_amd import _native as nat
 from cubed_amd import ir
 from cubed_amd.core.plan import arrays_to_plan
@@ -253,11 +255,15 @@ def test_vorticity_regions_are_pieces_not_gathers(built, dry):
     assert first.ntasks > first.ngroups
 
 
-def test_vorticity_chain_walks_source_chunks(built, dry):
+@pytest.mark.parametrize("merge", [False, True])
+def test_vorticity_chain_walks_source_chunks(built, dry, monkeypatch, merge):
     """The whole reduction (per-chunk mean + merge/combine rounds + aggregate)
     is ONE launch whose rows are the source chunks: the tail plane of task j
     and the head of task j+1 (both in source chunk j+1) are merged, so no
-    single-plane pieces remain and there is one group (the scalar)."""
+    single-plane pieces remain and there is one group (the scalar).  With
+    row merging (the default) the chunks of one T band, consecutive slots
+    of a and of x, become one row with a chunk dim."""
+    monkeypatch.setattr(Lw, "MERGE_ROWS", merge)
     spec = cubed.Spec(allowed_mem="2GB", executor=dry)
     random.seed(1)
     a = crandom.random((40, 18, 16), chunks=(10, 9, 8), spec=spec)
@@ -271,23 +277,40 @@ def test_vorticity_chain_walks_source_chunks(built, dry):
     fused = _fused(dry)
     assert len(fused) == 1
     f = fused[0]
-    assert f.ngroups == 1 and f.ntasks == 4 * 2 * 2  # source chunks x kept blocks
-    assert sorted(r.extent[3] for r in f.layout.rows) == [9] * 4 + [10] * 12
+    # every element of a[1:] read exactly once, merged or not
+    assert sum(math.prod(r.extent) for r in f.layout.rows) == 39 * 18 * 16
+    if not merge:
+        assert f.ngroups == 1 and f.ntasks == 4 * 2 * 2  # source chunks x kept blocks
+        assert sorted(r.extent[3] for r in f.layout.rows) == [9] * 4 + [10] * 12
+    else:
+        assert f.ntasks == 4  # one row per source T band
+        assert sorted(r.extent[3] for r in f.layout.rows) == [9, 10, 10, 10]
 
 
-def test_rechunk_then_mean_reads_the_source(built, dry):
+@pytest.mark.parametrize("merge", [False, True])
+def test_rechunk_then_mean_reads_the_source(built, dry, monkeypatch, merge):
     """rechunk rows -> columns then mean(axis=0): no copy launch; the mean's
-    tasks are cut into per-source-chunk pieces (partials + grouped finish)."""
+    tasks are cut into per-source-chunk pieces (partials + grouped finish).
+    With row merging (the default) the pieces of a column block -- the
+    source's stacked row bands, one run of addresses -- are one row, and the
+    column blocks -- consecutive columns of the same rows, writing consecutive
+    output chunks -- one task of whole rows."""
+    monkeypatch.setattr(Lw, "MERGE_ROWS", merge)
     spec = cubed.Spec(allowed_mem="288GB", executor=dry)
     random.seed(1)
     x = xp.astype(crandom.random((500, 500), chunks=(10, 500), spec=spec), xp.float32)
     arrays_to_plan(x).execute(executor=dry, array_names=[x.name])
     dry.launched.clear()
-    m = xp.mean(x.rechunk((500, 10)), axis=0)
+    m = xp.mean(x.rechunk((500, 40)), axis=0)
     arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
     assert not [l for l in dry.launched if isinstance(l, CopyLaunch)]
     fused = _fused(dry)
-    assert len(fused) == 1 and fused[0].ntasks == 50 * 50 and fused[0].ngroups == 50
+    if not merge:
+        assert len(fused) == 1 and fused[0].ntasks == 50 * 13 and fused[0].ngroups == 13
+    else:
+        f = fused[0]
+        assert len(fused) == 1 and f.ntasks == 1 and f.groups is None and f.max_kept == 500
+        assert f.layout.rows[0].extent == [500, 500] and f.prog.mode & Lw.MODE_STREAM
     assert not fused[0].gathers
 
 
@@ -484,7 +507,8 @@ def test_five_input_map_splits_into_two_fused_launches(built, dry):
     fused = _fused(dry)
     assert len(fused) == 2
     assert fused[0].prog.nleaves <= 4 and fused[1].prog.nleaves <= 4
-    assert fused[0].ntasks == fused[1].ntasks == 4
+    # the 4 chunk tasks read and write consecutive slots: one streaming task
+    assert fused[0].ntasks == fused[1].ntasks == 1
 
 
 def test_split_program_keeps_every_input():
