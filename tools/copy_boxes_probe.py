@@ -1,7 +1,7 @@
 """Development probe (not part of the library): the box tables of the config 3
 rechunk copy under the reference's 2 GB plan (two ops composed into one copy)
 and the 288 GB plan (one op), with each launch's time.  Run on the GPU box:
-    python tools/copy_boxes_probe.py [N]
+    python tools/copy_boxes_probe.py [N] [plans, e.g. 288GB,2GB] [untimed launches before the 5 timed]
 """
 import collections
 import os
@@ -25,7 +25,15 @@ from cubed_amd.runtime.executors.gpu import GpuDagExecutor  # noqa: E402
 def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 50000
     ex = GpuDagExecutor()
-    for mem in ("2GB", "288GB"):
+    pre = float(os.environ.get("PRE_ALLOC_GB", "0"))
+    if pre:  # allocate + free a dummy buffer first (placement diagnosis)
+        d = torch.empty(int(pre * 2**30), dtype=torch.uint8, device="cuda")
+        d.fill_(1)
+        torch.cuda.synchronize()
+        del d
+        if os.environ.get("PRE_EMPTY"):
+            torch.cuda.empty_cache()
+    for mem in (sys.argv[2].split(",") if len(sys.argv) > 2 else ("2GB", "288GB")):
         spec = cubed.Spec(allowed_mem=mem, executor=ex)
         random.seed(2000)
         x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
@@ -52,9 +60,10 @@ def main():
                     print(f"    box src +{b.src - src[0]} dst {b.dst:#x}")
                 s = torch.cuda.Stream()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                warm = int(sys.argv[3]) if len(sys.argv) > 3 else 1
                 with torch.cuda.stream(s):
-                    for r in range(6):
-                        if r == 1:
+                    for r in range(warm + 5):
+                        if r == warm:
                             e0.record(s)
                         L.run(s.cuda_stream)
                     e1.record(s)
