@@ -418,6 +418,11 @@ def rechunk_mean_extra(args, ex, rank, world):
         r = dict(metric=f"rechunk+mean effective input GB/s ({mode})", value=round(x.nbytes / dt / 1e9, 1),
                  ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ), **overhead(dt, summ, 10))
         if world == 1:
+            key, ms = dominant(summ, "FusedLaunch")
+            if mode.startswith("rechunk"):
+                # one read of x (the 50000 f32 means written are 0.002 % more)
+                r["roofline"] = roofline_hbm(x.nbytes, ms, "rechunk_mean_stream", args,
+                                             f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
             if exp is None:
                 exp = column_means_f64(x.zarray).astype(np.float32)
             got = m.compute(resume=True)

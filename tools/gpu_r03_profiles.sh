@@ -10,7 +10,7 @@ cd "$R" && mkdir -p gpurun_out
 export TMPDIR=/tmp
 ARGS="--steps 5 --warmup 1 --no-cpu-baseline"
 KERNELS="quad_means_fused=cubed_stream_f32_l2_r1 rechunk_copy=k_copy_flat config1_stream=cubed_stream_f64_l1_r2 \
-vorticity_pieces=cubed_stream_f64_l4_r1_partials matmul_f32=k_gemm_f32_chain matmul_bf16=k_gemm_bf16_chain \
+vorticity_pieces=cubed_stream_f64_l4_r2_partials matmul_f32=k_gemm_f32_chain matmul_bf16=k_gemm_bf16_chain \
 rechunk_mean_stream=cubed_stream_f32_l1_r1"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" $ARGS > "$R/gpurun_out/prof.log" 2>&1 || { echo prof failed; tail -20 "$R/gpurun_out/prof.log"; exit 1; }
@@ -23,6 +23,16 @@ timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAV
 echo mfma-done
 cd "$R"
 python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $KERNELS > gpurun_out/traffic.json || exit 1
+# the elided rechunk + mean shares its kernel name with the per-rank share and
+# the materialised mean: its own pass, told apart by grid size
+ONLY=rechunk_mean KERNELS="rechunk_mean_stream=cubed_stream_f32_l1_r1@238336 rechunk_mean_materialised=cubed_stream_f32_l1_r1@243200" \
+  bash tools/gpu_pmc_only.sh > /dev/null || { echo pmc only failed; exit 1; }
+python - <<'PY' || exit 1
+import json
+t = json.load(open("gpurun_out/traffic.json"))
+t.update(json.load(open("gpurun_out/traffic_only.json")))
+json.dump(t, open("gpurun_out/traffic.json", "w"), indent=1)
+PY
 cp gpurun_out/traffic.json profiles/traffic.json
 timeout -k 10 180 tools/pieces_probe 5 > gpurun_out/pieces_probe.log 2>&1 || { echo probe failed; tail -5 gpurun_out/pieces_probe.log; exit 1; }
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; tail -20 gpurun_out/bench.err; exit 1; }

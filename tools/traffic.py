@@ -6,7 +6,9 @@ Usage (on the GPU box, two separate counter passes, kernel-trace only):
     python tools/traffic.py OUT/fetch OUT/write KEY=KERNEL [KEY=KERNEL ...] > traffic.json
 
 KERNEL is matched against the dispatched kernel's base name (the name without
-"void ", namespaces, template arguments and parameters), exactly.
+"void ", namespaces, template arguments and parameters), exactly; KERNEL@GRID
+keeps only dispatches of that grid size (kernels of one name in several
+extras, e.g. the elided rechunk + mean and the materialised mean).
 FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section),
 gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B/lane stores.
@@ -30,12 +32,17 @@ def base_name(name):
 
 
 def per_dispatch(d, counter, kernel_sub):
+    grid = None
+    if "@" in kernel_sub:
+        kernel_sub, grid = kernel_sub.split("@", 1)
     vals = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name") or row.get("Kernel-Name") or ""
                 if base_name(name) != kernel_sub or row.get("Counter_Name") != counter:
+                    continue
+                if grid is not None and (row.get("Grid_Size") or row.get("Grid_Size_X")) != grid:
                     continue
                 key = (path, row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals)))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
