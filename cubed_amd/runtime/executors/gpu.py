@@ -503,6 +503,12 @@ class GpuDagExecutor(DagExecutor):
                                 row = dataclasses.replace(row, obases=[meta["discard"]] * len(row.obases))
                             rows.append(row)
                             gkeys.append((key, gk))
+            from ... import lowering as L
+
+            if L.MERGE_ROWS and all(k == L.LEAF_ARRAY for k in kinds):
+                # this rank's row bands of one group continue each other in its
+                # slab (its chunks' slots are consecutive): one row per run
+                rows, gkeys = L._merge_group_rows(rows, gkeys, red, leaves)
             meta["starts"] = [i for i in range(len(gkeys)) if i == 0 or gkeys[i] != gkeys[i - 1]]
             meta["mko"] = mko
             return rows, red

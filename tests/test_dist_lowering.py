@@ -154,11 +154,17 @@ def test_ranks_issue_the_same_collectives(built, world):
     assert ["PartialsLaunch"] in seqs[0] and ["FetchLaunch"] in seqs[0]
 
 
-def test_rechunk_mean_runs_pieces_where_chunks_live(built):
+@pytest.mark.parametrize("merge", [False, True])
+def test_rechunk_mean_runs_pieces_where_chunks_live(built, monkeypatch, merge):
     """rechunk rows -> columns read through by mean(axis=0) on 4 ranks: each
     rank runs only the pieces of the source chunks it holds (no fetch, no
     all-to-all), one partials row per piece plus an identity row for groups
-    without local pieces."""
+    without local pieces.  With row merging (the default) a rank's pieces of
+    one output block -- its row bands, consecutive slots of its slab -- are
+    one row."""
+    import cubed_amd.lowering as Lw
+
+    monkeypatch.setattr(Lw, "MERGE_ROWS", merge)
     world = 4
     x = np.ones((500, 500), dtype=np.float32)
     total = 0
@@ -175,6 +181,8 @@ def test_rechunk_mean_runs_pieces_where_chunks_live(built):
         dp = dry.launched[0]
         assert dp.ngroups == 50 and dp.root is None
         mine = len([c for c in range(50) if c % world == rank])  # source chunks held here
-        assert dp.fused.ntasks == mine * 50
+        assert dp.fused.ntasks == (mine * 50 if not merge else 50)
+        rows = sum(r.extent[0] for r in dp.fused.layout.rows)
+        assert rows == mine * 10 * 50  # every local source row once per output block
         total += dp.fused.ntasks
-    assert total == 50 * 50
+    assert total == (50 * 50 if not merge else 50 * world)
