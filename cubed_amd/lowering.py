@@ -992,7 +992,7 @@ class Lowerer:
         P.nred = layout.nred
         P.mode = layout.mode
         stream = _stream_ok(layout, leaves, kinds, P.vtype, check_outputs=not lifted)
-        if stream and merge_ok and not partials and not lifted and \
+        if stream and merge_ok and MERGE_KEPT and not partials and not lifted and \
                 (group_start is None or len(group_start) == len(rows) + 1):
             out_isz = [target.field_dtype(n if structured_out else None).itemsize for n, _ in out_items]
             merged = _merge_kept_runs(layout, [np.dtype(l.dtype).itemsize for l in leaves], out_isz)
@@ -1699,6 +1699,7 @@ def _stream_ok(layout: Layout, leaves, kinds, vtype, check_outputs=True) -> bool
 
 
 MERGE_ROWS = True  # tests set False to run the unmerged task / piece rows
+MERGE_KEPT = True  # probes set False to keep one task per output chunk
 
 
 def _merge_group_rows(rows, group_keys, red_axes, leaves):
