@@ -26,7 +26,8 @@ a DAG (stage functions from the ``cubed`` package) and hands it here:
   ``Region`` leaf), ``index``'s ``_read_index_chunk`` (a Region leaf with the
   selection), matmul's ``_matmul`` chunk product and ``_chunk_sum``
   (linear_algebra_functions.py:13-78: the executor runs the product and its
-  k-sum rounds as one chained GEMM), and ``random`` (``map_blocks(_random,
+  k-sum rounds as one chained GEMM), tensordot's ``_tensordot`` (:96-153,
+  with the ``sum`` over the contracted dims), and ``random`` (``map_blocks(_random,
   ...)`` under ``func_with_block_id``, cubed/random.py:13-36) the bit-exact
   Philox leaf;
 * any other chunk function is lowered by tracing it on proxies
@@ -42,9 +43,9 @@ paths of their ``LazyZarrArray``s, Zarr v2 via ``cubed_amd.zarr_io``) where
 the reference's ``compute()`` reads them back.
 
 What is not lowered raises ``LoweringError`` naming the op: user chunk
-functions that are not elementwise, contractions with nested block keys
-(tensordot / partial_reduce), and functions taking ``block_id`` other
-than ``random``.  The reference cannot be imported in
+functions that are not elementwise, ``partial_reduce``'s nested block keys
+(``reduction(..., use_new_impl=True)``), and functions taking ``block_id``
+other than ``random``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -198,10 +199,11 @@ class _Converter:
             kind, data = parts
             if kind == "fuse":
                 p1, p2 = data
-                return fuse(self.blockwise(name, p1, meta), self.blockwise(name, p2, meta))
+                return fuse(self.blockwise(_written_name(p1, [p2], name), p1, meta), self.blockwise(name, p2, meta))
             consumer, preds = data
             return fuse_multiple(self.blockwise(name, consumer, meta),
-                                 *[self.blockwise(name, pp, meta) if pp is not None else None for pp in preds])
+                                 *[self.blockwise(_written_name(pp, [consumer], name), pp, meta)
+                                   if pp is not None else None for pp in preds])
         cfg = p.config
         reads = {n: self.proxy(px, n) for n, px in cfg.reads_map.items()}
         write = self.proxy(cfg.write, name)
@@ -249,6 +251,11 @@ class _Converter:
         if bname == "_matmul" and bmod.startswith("cubed") and len(keys) == 2:
             # per (i, k, j) task: A_ik @ B_kj with a unit k dim (linear_algebra_functions.py:62-64)
             return ir.MatmulProgram(out_dtype=np.dtype(out.dtype))
+        if bname == "_tensordot" and bmod.startswith("cubed") and len(keys) == 2 and "axes" in kw:
+            # tensordot's chunk contraction with a unit dim per contracted axis
+            # (linear_algebra_functions.py:96-153); its sum over those dims follows
+            axes = tuple(tuple(int(a) for a in ((ax,) if isinstance(ax, int) else ax)) for ax in kw["axes"])
+            return ir.TensordotProgram(axes=axes, out_dtype=np.dtype(out.dtype))
         if len(keys) != 1 or not isinstance(keys[0], tuple):
             return None
         x = reads[keys[0][0]].array
@@ -394,6 +401,25 @@ class _Converter:
             pipe = CubedPipeline(copy_read_to_write, p.name, p.mappable, spec)
             return PrimitiveOperation(pipeline=pipe, target_array=spec.write.array, **meta)
         raise LoweringError(f"op {name}: reference stage function {fname or p.function!r} is not supported")
+
+
+def _written_name(producer, consumers, default):
+    """The array name a fused-away producer pipeline writes: the key its
+    consumer's ``reads_map`` holds for that target (the DAG no longer has a
+    node for it)."""
+    t = producer.config.write.array
+    for c in consumers:
+        for k, px in getattr(c.config, "reads_map", {}).items():
+            if px.array is t:
+                return k
+        inner = _fused_parts(c.config.function)
+        if inner is not None:
+            kind, data = inner
+            subs = list(data) if kind == "fuse" else [data[0]] + [q for q in data[1] if q is not None]
+            found = _written_name(producer, subs, None)
+            if found is not None:
+                return found
+    return default
 
 
 # ------------------------------------------------------------------ function anatomy

@@ -378,7 +378,19 @@ _matmul = _ref_fn("_matmul", "cubed.array_api.linear_algebra_functions")
 _chunk_sum = _ref_fn("_chunk_sum", "cubed.array_api.linear_algebra_functions")
 
 
-def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20):
+_tensordot = _ref_fn("_tensordot", "cubed.array_api.linear_algebra_functions")
+
+
+def tensordot_plan(work_dir, seed_a, seed_b, **kw):
+    """``xp.tensordot(A, B, axes=1)`` as the reference plans it: blockwise
+    ``_tensordot`` (axes ((1,), (0,))) keeping a unit dim per contracted axis,
+    then ``sum`` over it (a numpy ``sum`` per chunk, merge_chunks, sum,
+    squeeze) -- the matmul plan's shape with the tensordot chunk functions."""
+    return matmul_plan(work_dir, seed_a, seed_b, product=functools.partial(_tensordot, axes=((1,), (0,))),
+                       ksum=np.sum, **kw)
+
+
+def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20, product=None, ksum=None):
     """``xp.matmul(A, B)`` of two random f64 arrays as the reference plans it
     under its default optimizer: the (i, k, j) chunk products ``_matmul``
     fused with the first ``_chunk_sum`` over the unit k dim, then one op
@@ -394,14 +406,16 @@ def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20)
     A, B = p.g.nodes[aname]["target"], p.g.nodes[bname]["target"]
     prod_name = p._name("array")
     prod_t = p.lazy_target(prod_name, pshape, np.float64, pchunks)
-    spec = BlockwiseSpec(lambda key: [(aname, key[1], key[2]), (bname, key[2], key[3])], functools.partial(_matmul),
+    product = product if product is not None else functools.partial(_matmul)
+    ksum = ksum if ksum is not None else _chunk_sum
+    spec = BlockwiseSpec(lambda key: [(aname, key[1], key[2]), (bname, key[2], key[3])], product,
                          2, {aname: CubedArrayProxy(A, A.chunks), bname: CubedArrayProxy(B, B.chunks)},
                          CubedArrayProxy(prod_t, pchunks))
     ntasks = int(np.prod(numblocks(pshape, pchunks)))
     mm = PrimitiveOperation(CubedPipeline(apply_blockwise, p._name("apply_blockwise"), [], spec), prod_t,
                             0, p.MEM, 0, ntasks, True)
     sname = p._name("array")
-    sop, st = p.blockwise_op(functools.partial(_chunk_sum, axis=(1,), keepdims=True, dtype=np.float64),
+    sop, st = p.blockwise_op(functools.partial(ksum, axis=(1,), keepdims=True, dtype=np.float64),
                              sname, pshape, np.float64, pchunks, [(prod_name, prod_t)])
     first = fuse(mm, sop)
     p.g.remove_node(prod_name)
@@ -420,7 +434,7 @@ def matmul_plan(work_dir, seed_a, seed_b, m=60, k=80, n=40, cm=20, ck=20, cn=20)
     gop, _ = p.blockwise_op(mfn, gname, pshape, np.float64, tchunks,
                             [(empty, p.g.nodes[empty]["target"]), (offs, p.g.nodes[offs]["target"])])
     cname = p._name("array")
-    cop, _ = p.blockwise_op(functools.partial(_chunk_sum, axis=(1,), keepdims=True, dtype=np.float64),
+    cop, _ = p.blockwise_op(functools.partial(ksum, axis=(1,), keepdims=True, dtype=np.float64),
                             cname, (m, 1, n), np.float64, pchunks, [(gname, p.g.nodes[gname]["target"])])
     qname = p._name("array")
     qop, qt = p.blockwise_op(functools.partial(np.squeeze, axis=(1,)), qname, (m, n), np.float64, (cm, cn),

@@ -258,6 +258,37 @@ def test_reference_matmul_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
     assert kinds.count("GemmLaunch") == 1
 
 
+def test_reference_tensordot_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
+    """The reference tensordot plan (_tensordot keeping a unit contracted
+    dim, then numpy sum over it through merge_chunks) runs as one chained GEMM
+    launch, as cubed_amd's own tensordot does."""
+    dag, out, a, b, op = refdag.tensordot_plan(tmp_path, _seed(15), _seed(16))
+    conv = RD.convert_reference_dag(dag)
+    progs = [d["pipeline"].config.function for _, d in conv.dag.nodes(data=True)
+             if d.get("pipeline") is not None and isinstance(d["pipeline"].config, RD.BlockwiseSpec)]
+    assert any(isinstance(p, ir.GemmThenProgram) for p in progs)
+    dry.launched.clear()
+    dry.execute_dag(conv.dag, array_names=[out])
+    kinds = [type(l).__name__ for l in dry.launched]
+    assert kinds.count("GemmLaunch") == 1
+
+
+@pytest.mark.gpu
+def test_reference_tensordot_plan_on_the_gpu(tmp_path, gpu_executor):
+    """tensordot(A, B, axes=1) of two random f64 arrays built as the reference
+    builds it, against the f64 product of the oracle's Philox blocks."""
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    sa, sb = _seed(17), _seed(18)
+    dag, out, a, b, op = refdag.tensordot_plan(tmp_path, sa, sb)
+    gpu_executor.execute_dag(dag, array_names=[out])
+    A = R.random_array((60, 80), (20, 20), sa)
+    B = R.random_array((80, 40), (20, 20), sb)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    np.testing.assert_allclose(got, A @ B, rtol=1e-12, atol=0)
+
+
 @pytest.mark.gpu
 def test_reference_matmul_plan_on_the_gpu(tmp_path, gpu_executor):
     """matmul of two random f64 arrays built as the reference builds it:
