@@ -194,7 +194,9 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     const int64_t inflight = (int64_t)kBlock * stream_unroll(isz, P->nleaves) * P->nleaves * W * 4 * isz;
     if (P->nfields > 0 && base * inflight < (int64_t)256 * 96 * 1024 && max_red >= 64)
       L.nsplit = (int32_t)choose_split(base, max_red / 16, kStreamTarget);
-    L.blocks = ntasks * L.nsplit * L.bpt;
+    // a multiple of 8 workgroups (the surplus exits at once): stream_body
+    // maps them to XCD-contiguous runs
+    L.blocks = (ntasks * L.nsplit * L.bpt + 7) / 8 * 8;
   } else if (L.kernel == 0) {
     const int64_t items = (max_kept + L.vec - 1) / L.vec;
     L.bpt = (items + kBlock - 1) / kBlock;

@@ -828,7 +828,15 @@ template <typename V, int NL, int U, int W = 1>
 CUBED_DEV void stream_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
-  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  // XCD-contiguous runs: dispatch is round-robin over the 8 XCDs, so
+  // workgroup g runs logical index (g % 8) * (G / 8) + g / 8 -- each XCD
+  // walks one contiguous run of (task, split, column block), and the column
+  // blocks either side of a 128-B line a misaligned row splits share its L2
+  // (the launcher pads the grid to a multiple of 8; the surplus exits).
+  // Vorticity -2 %, config 1 -0.8 %, others equal (profiles/r03_stream_xcd_ab.log)
+  const int64_t G = (int64_t)gridDim.x * gridDim.y;
+  int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  if ((G & 7) == 0) g = (g & 7) * (G >> 3) + (g >> 3);
   const int64_t b = g % bpt;
   const int64_t rest = g / bpt;
   const int s = (int)(rest % nsplit);
