@@ -25,7 +25,7 @@ cd "$R"
 python tools/traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write $KERNELS > gpurun_out/traffic.json || exit 1
 # the elided rechunk + mean shares its kernel name with the per-rank share and
 # the materialised mean: its own pass, told apart by grid size
-ONLY=rechunk_mean KERNELS="rechunk_mean_stream=cubed_stream_f32_l1_r1@238336 rechunk_mean_materialised=cubed_stream_f32_l1_r1@243200" \
+ONLY=rechunk_mean KERNELS="rechunk_mean_stream=cubed_stream_f32_l1_r1@239616 rechunk_mean_materialised=cubed_stream_f32_l1_r1@243712" \
   bash tools/gpu_pmc_only.sh > /dev/null || { echo pmc only failed; exit 1; }
 python - <<'PY' || exit 1
 import json
