@@ -203,6 +203,23 @@ class _Splitter:
             return ("c", ir.Where(zero, r, cr, p), ir.Where(zero, im, ci, p))
         if op == "log":
             return ("c", _un("log", _bin("hypot", re, im, p), p), _bin("atan2", im, re, p))
+        if op in ("log2", "log10"):
+            # numpy: log(z) / log(base), part by part
+            k = _const(1.0 / np.log(2.0 if op == "log2" else 10.0), p)
+            return ("c", _bin("multiply", _un("log", _bin("hypot", re, im, p), p), k, p),
+                    _bin("multiply", _bin("atan2", im, re, p), k, p))
+        if op == "log1p":
+            # log|1 + z| = log1p(2x + x^2 + y^2) / 2 (no cancellation for small z), arg = atan2(y, 1 + x)
+            one = _const(1, p)
+            t = _bin("add", _bin("multiply", re, _bin("add", _const(2, p), re, p), p), _bin("multiply", im, im, p), p)
+            return ("c", _bin("multiply", _un("log1p", t, p), _const(0.5, p), p),
+                    _bin("atan2", im, _bin("add", one, re, p), p))
+        if op == "expm1":
+            # numpy nc_expm1: (expm1(x) cos y - 2 sin^2(y/2), exp(x) sin y)
+            s2 = _un("sin", _bin("multiply", im, _const(0.5, p), p), p)
+            r = _bin("subtract", _bin("multiply", _un("expm1", re, p), _un("cos", im, p), p),
+                     _bin("multiply", _const(2, p), _bin("multiply", s2, s2, p), p), p)
+            return ("c", r, _bin("multiply", _un("exp", re, p), _un("sin", im, p), p))
         if op == "sqrt":
             return self._sqrt(re, im, p)
         if op in ("sinh", "cosh", "sin", "cos"):
@@ -213,6 +230,8 @@ class _Splitter:
             # tan z = -i tanh(i z), i z = (-im, re)
             _, a, b = self._tanh(_un("negative", im, p), re, p)
             return ("c", b, _un("negative", a, p))
+        if op in ("asin", "acos", "asinh", "acosh", "atan", "atanh"):
+            return self._inverse(op, re, im, p)
         if op == "sign":
             # numpy 2: z / |z|, 0 at 0
             a = _bin("hypot", re, im, p)
@@ -243,6 +262,51 @@ class _Splitter:
         if op == "sin":   # -i (a + i b) = (b, -a)
             return ("c", b, _un("negative", a, p))
         return ("c", a, b)
+
+    def _inverse(self, op, re, im, p) -> Val:
+        """Inverse trigonometric / hyperbolic functions on the principal
+        branches numpy uses (C99 casin & co., branch cuts on the axes), from
+        Kahan's acos ("Branch cuts for complex elementary functions", 1987),
+        which avoids the cancellation of 1 - z^2:
+            A = sqrt(1 - z), B = sqrt(1 + z):
+            acos z = (2 atan2(re A, re B), asinh(im(conj(B) A)))
+            asin z = pi/2 - acos z,  acosh z = +-i acos z (re >= 0)
+            atanh z = (log1p(4x / ((1 - x)^2 + y^2)) / 4,
+                       atan2(2y, (1 - x)(1 + x) - y^2) / 2)
+            asinh z = -i asin(i z), atan z = -i atanh(i z).
+        Finite inputs; |z| near the overflow threshold of the part type is
+        not rescaled."""
+        one = _const(1, p)
+        if op in ("asinh", "atan"):
+            # -i f(i z), i z = (-y, x); -i (a + i b) = (b, -a)
+            _, a, b = self._inverse("asin" if op == "asinh" else "atanh", _un("negative", im, p), re, p)
+            return ("c", b, _un("negative", a, p))
+        if op == "atanh":
+            x, y = re, im
+            omx = _bin("subtract", one, x, p)
+            d = _bin("add", _bin("multiply", omx, omx, p), _bin("multiply", y, y, p), p)
+            r = _bin("multiply", _un("log1p", _bin("divide", _bin("multiply", _const(4, p), x, p), d, p), p),
+                     _const(0.25, p), p)
+            den = _bin("subtract", _bin("multiply", omx, _bin("add", one, x, p), p), _bin("multiply", y, y, p), p)
+            i = _bin("multiply", _bin("atan2", _bin("multiply", _const(2, p), y, p), den, p), _const(0.5, p), p)
+            return ("c", r, i)
+        # acos (Kahan): A = sqrt(1 - z), B = sqrt(1 + z)
+        _, ar, ai = self._sqrt(_bin("subtract", one, re, p), _un("negative", im, p), p)
+        _, br, bi = self._sqrt(_bin("add", one, re, p), im, p)
+        a = _bin("multiply", _const(2, p), _bin("atan2", ar, br, p), p)
+        b = _un("asinh", _bin("subtract", _bin("multiply", br, ai, p), _bin("multiply", bi, ar, p), p), p)
+        if op == "acos":
+            return ("c", a, b)
+        if op == "asin":
+            # asin z = pi/2 - acos z (Kahan's asin part im(conj(A) B) is exactly
+            # -im(conj(B) A)); the real part carries an absolute error of an ulp
+            # of pi/2 rather than a relative one -- one fused program (the VM's
+            # 6 registers do not hold both of Kahan's products)
+            return ("c", _bin("subtract", _const(np.pi / 2, p), a, p), _un("negative", b, p))
+        # acosh z = +-i acos z, the sign that makes the real part >= 0:
+        # (|b|, copysign(a, -b)) -- im(acos z) carries the opposite sign of
+        # im z, signed zeros included, so z need not stay live
+        return ("c", _un("abs", b, p), _bin("copysign", a, _un("negative", b, p), p))
 
     def _tanh(self, re, im, p) -> Val:
         # npy_ctanh (FreeBSD s_ctanh.c, Kahan's algorithm) for finite values:

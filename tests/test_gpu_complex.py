@@ -222,11 +222,26 @@ def test_trigonometric_hyperbolic_and_pow(ex, dtype):
         close(got, exp, dtype, ulps=64, scale=np.maximum(np.abs(exp), 1e-30))
 
 
-def test_unsupported_complex_ops_raise(ex):
-    Z = cdata((4, 4), "complex128", 8, specials=False)
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_inverse_trigonometric_hyperbolic_and_logs(ex, dtype):
+    """asin/acos/atan/asinh/acosh/atanh of complex values (Kahan's branch-cut
+    formulas, the principal branches of numpy's C99 casin & co.) and
+    log1p/expm1/log2/log10 against numpy, finite inputs incl. points on the
+    real and imaginary axes (|x| > 1 on the cuts, with a +0 / -0 imaginary
+    part); bound: 64 ulps of max(|result|, 1) (atan / atanh: 256, their
+    real part ~ log1p of a ratio near the unit circle)."""
+    Z = cdata((6, 7), dtype, 13, specials=False) * 2
+    f = Z.reshape(-1)
+    f[0], f[1], f[2], f[3] = complex(2, 0), complex(-3, -0.0), complex(0, 0.5), complex(0.3, 0)
+    f[4], f[5] = complex(1e-3, -2e-3), complex(-0.0, 1.5)
     spec = mkspec(ex)
-    z = cubed.from_array(Z, chunks=(2, 2), spec=spec)
-    from cubed_amd.lowering import LoweringError
-
-    with pytest.raises(LoweringError, match="complex"):
-        xp.asin(z).compute()
+    z = cubed.from_array(Z, chunks=(3, 4), spec=spec)
+    names = {"asin": "arcsin", "acos": "arccos", "atan": "arctan", "asinh": "arcsinh",
+             "acosh": "arccosh", "atanh": "arctanh", "log1p": "log1p", "expm1": "expm1",
+             "log2": "log2", "log10": "log10"}
+    with np.errstate(all="ignore"):
+        for name, npname in names.items():
+            got = getattr(xp, name)(z).compute()
+            exp = getattr(np, npname)(Z)
+            close(got, exp, dtype, ulps=256 if name in ("atan", "atanh") else 64,
+                  scale=np.maximum(np.abs(exp), 1.0))
