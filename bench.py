@@ -245,12 +245,14 @@ def roofline_hbm(algo_bytes, ms, traffic_key, args, kernel):
 
 
 def free_gpu():
+    """Drop the finished extra's arrays.  Their HBM stays in torch's cache for
+    the next extra (as in any long-running executor process): handing it back
+    to the driver (empty_cache) and re-allocating made the next large array
+    slower to stream -- the read-through rechunk + mean 1.58-1.64 vs 1.505 ms
+    after the rechunk extra, profiles/r03_alloc_reuse.log."""
     import gc
 
-    import torch
-
     gc.collect()
-    torch.cuda.empty_cache()
 
 
 # --------------------------------------------------------------------------- value checks
