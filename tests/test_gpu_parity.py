@@ -715,3 +715,33 @@ def test_specialised_kernels_match_interpreter(monkeypatch, case):
     exp = run()
     assert got.dtype == exp.dtype
     assert np.array_equal(got, exp, equal_nan=True)
+
+
+@pytest.mark.parametrize("merge", [True, False])
+def test_row_merging_values(ex, monkeypatch, merge):
+    """Task-row merging (lowering._merge_group_rows / _merge_kept_runs) on
+    stream-eligible geometries -- a read-through rechunk + mean / int64 sum
+    (one task of whole rows when merged, 6 x 8 pieces + grouped finish when
+    not) and the vorticity chain mean(a[1:] * x + b[1:] * y) (one row per T
+    band with a chunk dim) -- against numpy: int64 exact, f32 means of f64
+    sums rtol 1e-6, f64 rtol 1e-12."""
+    from cubed_amd import lowering as L
+
+    monkeypatch.setattr(L, "MERGE_ROWS", merge)
+    rng = np.random.default_rng(21)
+    X = rng.random((600, 2048)).astype(np.float32)
+    I = rng.integers(-1000, 1000, (600, 2048))
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    x = cubed.from_array(X, chunks=(100, 2048), spec=spec)
+    i = cubed.from_array(I, chunks=(100, 2048), spec=spec)
+    got = xp.mean(x.rechunk((600, 256)), axis=0).compute()
+    np.testing.assert_allclose(got, X.astype(np.float64).mean(axis=0).astype(np.float32), rtol=1e-6, atol=0)
+    assert np.array_equal(xp.sum(i.rechunk((600, 256)), axis=0).compute(), I.sum(axis=0))
+    A, B = rng.random((41, 24, 32)), rng.random((41, 24, 32))
+    XX, YY = rng.random((24, 32)), rng.random((24, 32))
+    a = cubed.from_array(A, chunks=(10, 8, 8), spec=spec)
+    b = cubed.from_array(B, chunks=(10, 8, 8), spec=spec)
+    xx = cubed.from_array(XX, chunks=(8, 8), spec=spec)
+    yy = cubed.from_array(YY, chunks=(8, 8), spec=spec)
+    got = xp.mean(a[1:] * xx + b[1:] * yy).compute()
+    np.testing.assert_allclose(got, (A[1:] * XX + B[1:] * YY).mean(), rtol=1e-12, atol=0)
