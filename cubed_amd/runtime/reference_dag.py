@@ -27,7 +27,9 @@ a DAG (stage functions from the ``cubed`` package) and hands it here:
   selection), matmul's ``_matmul`` chunk product and ``_chunk_sum``
   (linear_algebra_functions.py:13-78: the executor runs the product and its
   k-sum rounds as one chained GEMM), tensordot's ``_tensordot`` (:96-153,
-  with the ``sum`` over the contracted dims), and ``random`` (``map_blocks(_random,
+  with the ``sum`` over the contracted dims), ``arg_reduction``'s
+  ``_arg_map_func`` (a block_id map: a pair reduction with an Iota leaf) /
+  ``_arg_func`` / ``_arg_combine`` / ``_arg_aggregate``, and ``random`` (``map_blocks(_random,
   ...)`` under ``func_with_block_id``, cubed/random.py:13-36) the bit-exact
   Philox leaf;
 * any other chunk function is lowered by tracing it on proxies
@@ -45,7 +47,7 @@ the reference's ``compute()`` reads them back.
 What is not lowered raises ``LoweringError`` naming the op: user chunk
 functions that are not elementwise, ``partial_reduce``'s nested block keys
 (``reduction(..., use_new_impl=True)``), and functions taking ``block_id``
-other than ``random``.  The reference cannot be imported in
+other than ``random`` and ``_arg_map_func``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -246,6 +248,8 @@ class _Converter:
                                   out_axes=tuple(range(out.ndim)), name="map_direct")
         if bname == "_read_index_chunk" and bmod.startswith("cubed"):
             return self._index_program(op, kw, keys, reads, out)
+        if bmod.startswith("cubed") and bname in ("_arg_map_func", "_arg_func", "_arg_combine", "_arg_aggregate"):
+            return self._arg_program(op, bname, kw, keys, reads, out)
         if wrappers:
             return None  # other block_id / map_direct functions: traced (random) or refused
         if bname == "_matmul" and bmod.startswith("cubed") and len(keys) == 2:
@@ -286,6 +290,47 @@ class _Converter:
             return ir.ExprProgram(ndim=x.ndim, nargs=1, outputs=outputs,
                                   out_axes=tuple(d for d in axes if d not in axis), name="squeeze")
         return None
+
+    def _arg_program(self, op, bname, kw, keys, reads, out):
+        """``arg_reduction``'s chunk functions (core/ops.py:1093-1153): the
+        block_id map ``_arg_map_func`` -- per block {i, v} with i the GLOBAL
+        index (block offset + local argmax) -- is one pair reduction over the
+        block with an Iota leaf for i; ``_arg_combine`` is this package's pair
+        reduction over {v, i} (chunkfuncs.ArgReduction: first NaN, else the
+        larger / smaller value, ties to the smaller index -- numpy's
+        argmax/argmin, so the combine order does not change the result);
+        ``_arg_func`` passes the pairs through and ``_arg_aggregate`` keeps i."""
+        from .. import chunkfuncs as CF
+
+        x = reads[keys[0][0]].array
+        dt = np.dtype(x.dtype)
+        n = x.ndim
+        axes = tuple(range(n))
+        if bname in ("_arg_map_func", "_arg_combine"):
+            name = getattr(kw.get("arg_func"), "__name__", "")
+            if name not in ("argmax", "argmin"):
+                raise LoweringError(f"op {op}: arg reduction with {kw.get('arg_func')!r}")
+        if bname == "_arg_map_func":
+            if dt.names or dt.kind not in "fiub":
+                raise LoweringError(f"op {op}: arg reduction of {dt}")
+            axis = int(kw["axis"])
+            chunks = tuple(tuple(c) for c in normalize_chunks(x.chunks, x.shape, dt))
+            idx = ir.Iota(axis, 0, axes, chunks)
+            fields = (ir.ReduceField("v", name, ir.Arg(0, dt, axes), dt),
+                      ir.ReduceField("i", "pair_index", idx, np.dtype(np.int64)))
+            return ir.ExprProgram(ndim=n, nargs=len(keys),
+                                  outputs=tuple((f, ir.Field(f, fd.dtype)) for f, fd in
+                                                (("i", fields[1]), ("v", fields[0]))),
+                                  out_axes=axes, reduce=ir.ReduceStage((axis,), fields), name="_arg_map_func")
+        if bname == "_arg_func":
+            return ir.ExprProgram(ndim=n, nargs=1,
+                                  outputs=tuple((f, ir.Arg(0, dt[f], axes, field=f)) for f in ("i", "v")),
+                                  out_axes=axes, name="_arg_func")
+        if bname == "_arg_combine":
+            axis = kw["axis"]
+            axis = (axis,) if isinstance(axis, int) else tuple(axis)
+            return CF.ArgReduction(name).program(n, dt, axis, keepdims=True)
+        return CF._arg_aggregate.program(n, dt)
 
     def _index_program(self, op, kw, keys, reads, out):
         """``index``'s map_direct function (core/ops.py:374-517): output block

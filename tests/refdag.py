@@ -373,6 +373,72 @@ def mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20)):
     return p.finalize(), sname, pname, name
 
 
+# -- arg reductions (core/ops.py:1093-1153) -------------------------------------
+_arg_map_func = _ref_fn("_arg_map_func", "cubed.core.ops")
+_arg_func = _ref_fn("_arg_func", "cubed.core.ops")
+_arg_combine = _ref_fn("_arg_combine", "cubed.core.ops")
+_arg_aggregate = _ref_fn("_arg_aggregate", "cubed.core.ops")
+
+
+def argreduce_plan(work_dir, root_seed, arg_func=np.argmax, shape=(40, 60), chunks=(10, 20)):
+    """``xp.argmax(random(shape, chunks), axis=0)`` as the reference plans it
+    (arg_reduction): map_blocks(_arg_map_func) with block_id over the
+    materialised input (a task per chunk, {i, v} blocks of one row), fused
+    with reduction's pass-through ``_arg_func``; then ONE op fusing
+    merge_chunks, ``_arg_combine``, ``_arg_aggregate`` and squeeze."""
+    p = RefPlan(work_dir)
+    rop, rname, rsrcs = p.random(shape, chunks, root_seed)
+    p.add(rop, rname, rsrcs)
+    idt = np.dtype([("i", np.int64), ("v", np.float64)])
+    nb = numblocks(shape, chunks)
+    nr = nb[0]
+    offs = p._name("offsets")
+    p._array(offs, VirtualOffsetsArray(nb))
+    mname = p._name("array")
+    pshape, pchunks = (nr, shape[1]), (1, chunks[1])
+    fn = functools.partial(func_with_block_id(_arg_map_func, nb), axis=0, arg_func=arg_func, size=chunks[0])
+    mop, mt = p.blockwise_op(fn, mname, pshape, idt, pchunks,
+                             [(rname, p.g.nodes[rname]["target"]), (offs, p.g.nodes[offs]["target"])])
+    fname = p._name("array")
+    fop, ft = p.blockwise_op(functools.partial(_arg_func, axis=(0,), keepdims=True), fname, pshape, idt, pchunks,
+                             [(mname, mt)])
+    a_op = fuse(mop, fop)
+    p.g.remove_node(mname)
+    p.lazy = [t for t in p.lazy if t is not mt]
+    p.add(a_op, fname, [rname, offs])
+    tchunks = (nr, chunks[1])
+    tnb = numblocks(pshape, tchunks)
+    tnorm = tuple(tuple(min(c, s - i) for i in range(0, s, c)) for s, c in zip(pshape, tchunks))
+    empty, toffs = p._name("empty"), p._name("offsets")
+    p._array(empty, VirtualEmptyArray(pshape, idt, tchunks))
+    p._array(toffs, VirtualOffsetsArray(tnb))
+    mfn = functools.partial(func_with_block_id(map_direct_wrap(_copy_chunk), tnb),
+                            arrays=(RefArray(fname, ft),), target_chunks=tnorm)
+    gname = p._name("array")
+    gop, _ = p.blockwise_op(mfn, gname, pshape, idt, tchunks,
+                            [(empty, p.g.nodes[empty]["target"]), (toffs, p.g.nodes[toffs]["target"])])
+    cname = p._name("array")
+    cop, _ = p.blockwise_op(functools.partial(_arg_combine, arg_func=arg_func, axis=(0,), keepdims=True),
+                            cname, (1, shape[1]), idt, (1, chunks[1]), [(gname, p.g.nodes[gname]["target"])])
+    aname = p._name("array")
+    agg, _ = p.blockwise_op(functools.partial(_arg_aggregate), aname, (1, shape[1]), np.int64,
+                            (1, chunks[1]), [(cname, p.g.nodes[cname]["target"])])
+    sname = p._name("array")
+    sq, starget = p.blockwise_op(functools.partial(np.squeeze, axis=(0,)), sname, (shape[1],), np.int64,
+                                 (chunks[1],), [(aname, p.g.nodes[aname]["target"])])
+    sq_spec = BlockwiseSpec(lambda k: [(aname, 0, k[1])], sq.pipeline.config.function, 1,
+                            sq.pipeline.config.reads_map, sq.pipeline.config.write)
+    sq = PrimitiveOperation(CubedPipeline(apply_blockwise, "apply_blockwise-sq", sq.pipeline.mappable, sq_spec),
+                            starget, 0, p.MEM, 0, sq.num_tasks, True)
+    b_op = fuse(fuse(fuse(gop, cop), agg), sq)
+    for nm in (gname, cname, aname):
+        t = p.g.nodes[nm]["target"]
+        p.g.remove_node(nm)
+        p.lazy = [x for x in p.lazy if x is not t]
+    name = p._op(b_op, sname, [empty, toffs, fname], b_op.num_tasks)
+    return p.finalize(), sname, rname, name
+
+
 # -- matmul (array_api/linear_algebra_functions.py:13-78) -----------------------
 _matmul = _ref_fn("_matmul", "cubed.array_api.linear_algebra_functions")
 _chunk_sum = _ref_fn("_chunk_sum", "cubed.array_api.linear_algebra_functions")

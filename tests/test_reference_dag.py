@@ -258,6 +258,36 @@ def test_reference_matmul_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
     assert kinds.count("GemmLaunch") == 1
 
 
+def test_reference_argmax_plan_converts(tmp_path, built, dry):
+    """The reference arg_reduction plan (map_blocks(_arg_map_func) with
+    block_id + _arg_func, merge_chunks + _arg_combine + _arg_aggregate +
+    squeeze) converts: the block_id map is a pair reduction with an Iota
+    leaf, and the plan lowers to fused launches only."""
+    dag, out, src, op = refdag.argreduce_plan(tmp_path, _seed(19))
+    conv = RD.convert_reference_dag(dag)
+    dry.launched.clear()
+    dry.execute_dag(conv.dag, array_names=[out])
+    kinds = {type(l).__name__ for l in dry.launched}
+    assert kinds <= {"FusedLaunch", "CopyLaunch", "_Alloc"}, kinds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", ["argmax", "argmin"])
+def test_reference_argmax_plan_on_the_gpu(tmp_path, gpu_executor, fn):
+    """argmax / argmin along axis 0 of a random f64 array, built as the
+    reference builds it: bit-exact indices against numpy on the oracle's
+    Philox blocks."""
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    seed = _seed(20)
+    dag, out, src, op = refdag.argreduce_plan(tmp_path, seed, arg_func=getattr(np, fn))
+    gpu_executor.execute_dag(dag, array_names=[out])
+    X = R.random_array((40, 60), (10, 20), seed)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    assert np.array_equal(got, getattr(np, fn)(X, axis=0))
+
+
 def test_reference_tensordot_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
     """The reference tensordot plan (_tensordot keeping a unit contracted
     dim, then numpy sum over it through merge_chunks) runs as one chained GEMM
