@@ -27,6 +27,7 @@ __global__ void k_fill(unsigned* p, long n) {
     p[i] = (unsigned)i * 2654435761u;
 }
 
+template <int LD, int ST>  // LD: 0 cached, 1 non-temporal loads; ST: 0 non-temporal, 1 plain stores
 __global__ __launch_bounds__(kBlock) void k_flat(const cubed_box_t* __restrict__ boxes, long nboxes, long bpb,
                                                  long rot) {
   const long g = blockIdx.x;
@@ -52,13 +53,18 @@ __global__ __launch_bounds__(kBlock) void k_flat(const cubed_box_t* __restrict__
       const long i = i0 + k * 64 + lane;
       if (i < w_end) {
         const unsigned r = (unsigned)i / nw, c = (unsigned)i - r * nw;
-        v[k] = ((const GA u32x4*)(uintptr_t)(sbase + (long)r * sstr))[c];
+        const GA u32x4* q = (const GA u32x4*)(uintptr_t)(sbase + (long)r * sstr) + c;
+        if constexpr (LD == 1) v[k] = __builtin_nontemporal_load(q);
+        else v[k] = *q;
       }
     }
 #pragma unroll
     for (int k = 0; k < UN; ++k) {
       const long i = i0 + k * 64 + lane;
-      if (i < w_end) __builtin_nontemporal_store(v[k], dst + i);
+      if (i < w_end) {
+        if constexpr (ST == 1) dst[i] = v[k];
+        else __builtin_nontemporal_store(v[k], dst + i);
+      }
     }
   }
 }
@@ -95,21 +101,40 @@ int main(int argc, char** argv) {
     std::sort(h.begin(), h.end(), [](const cubed_box_t& a, const cubed_box_t& b) { return a.src_base < b.src_base; });
     CHECK(hipMemcpy(d_boxes, h.data(), nb * sizeof(cubed_box_t), hipMemcpyHostToDevice));
   };
+  int variant = 0;  // 0: cached loads + NT stores (library), 1: NT loads, 2: plain stores, 3: NT loads + plain stores
+  auto launch = [&](long rot) {
+    switch (variant) {
+      case 1: hipLaunchKernelGGL((k_flat<1, 0>), dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot); break;
+      case 2: hipLaunchKernelGGL((k_flat<0, 1>), dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot); break;
+      case 3: hipLaunchKernelGGL((k_flat<1, 1>), dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot); break;
+      default: hipLaunchKernelGGL((k_flat<0, 0>), dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot); break;
+    }
+  };
   auto run = [&](const char* tag, long rot) {
-    for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k_flat, dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot);
+    for (int w = 0; w < 2; ++w) launch(rot);
     CHECK(hipEventRecord(e0));
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k_flat, dim3(nb * bpb), dim3(kBlock), 0, 0, d_boxes, nb, bpb, rot);
+    for (int r = 0; r < reps; ++r) launch(rot);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms;
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     ms /= reps;
-    printf("%-26s rot %4ld  %.4f ms  %.0f GB/s moved\n", tag, rot, ms, 2.0 * N * N * 4 / (ms * 1e-3) / 1e9);
+    printf("%-26s var %d rot %4ld  %.4f ms  %.0f GB/s moved\n", tag, variant, rot, ms, 2.0 * N * N * 4 / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
   const long rots[] = {0, 1, 7, 37, bpb / 2, 0};
   printf("bpb %ld, y - x = %ld B\n", bpb, (long)(y - x));
   build(y);
+  if (argc > 2) {  // load/store form sweep on both placements, rot 0
+    build(y);
+    for (variant = 0; variant < 4; ++variant) run("placement 1 (first y)", 0);
+    char* y3;
+    CHECK(hipMalloc(&y3, N * N * 4));
+    CHECK(hipFree(y));
+    build(y3);
+    for (variant = 0; variant < 4; ++variant) run("placement 2 (second y)", 0);
+    return 0;
+  }
   for (long r : rots) run("placement 1 (first y)", r);
   char* y2;
   CHECK(hipMalloc(&y2, N * N * 4));
