@@ -45,9 +45,9 @@ paths of their ``LazyZarrArray``s, Zarr v2 via ``cubed_amd.zarr_io``) where
 the reference's ``compute()`` reads them back.
 
 What is not lowered raises ``LoweringError`` naming the op: user chunk
-functions that are not elementwise, ``partial_reduce``'s nested block keys
-(``reduction(..., use_new_impl=True)``), and functions taking ``block_id``
-other than ``random`` and ``_arg_map_func``.  The reference cannot be imported in
+functions that are not elementwise, nested block keys other than
+``partial_reduce``'s, and functions taking ``block_id`` other than
+``random`` and ``_arg_map_func``.  The reference cannot be imported in
 this image, so the tests build DAGs of the reference's shape from stand-ins
 with the same class names and attributes (tests/test_reference_dag.py).
 """
@@ -250,6 +250,8 @@ class _Converter:
             return self._index_program(op, kw, keys, reads, out)
         if bmod.startswith("cubed") and bname in ("_arg_map_func", "_arg_func", "_arg_combine", "_arg_aggregate"):
             return self._arg_program(op, bname, kw, keys, reads, out)
+        if bname == "_partial_reduce" and bmod.startswith("cubed"):
+            return self._partial_reduce_program(op, cfg, kw, reads, first)
         if wrappers:
             return None  # other block_id / map_direct functions: traced (random) or refused
         if bname == "_matmul" and bmod.startswith("cubed") and len(keys) == 2:
@@ -331,6 +333,42 @@ class _Converter:
             axis = (axis,) if isinstance(axis, int) else tuple(axis)
             return CF.ArgReduction(name).program(n, dt, axis, keepdims=True)
         return CF._arg_aggregate.program(n, dt)
+
+    def _partial_reduce_program(self, op, cfg, kw, reads, first):
+        """``partial_reduce``'s ``_partial_reduce`` (core/ops.py:1008-1090,
+        reduction(..., use_new_impl=True) and tree_reduce): the block
+        function yields an ITERATOR of input keys (a group of blocks), which
+        this package's partial_reduce lowers the same way -- one task
+        reduces the merged view of its group with the initial function's
+        fields (reduce_func's when there is none), e.g. mean's {n, total}."""
+        group = cfg.block_function(("out",) + first)[0]
+        k0 = next(iter(group))
+        x = reads[k0[0]].array
+        f = kw.get("initial_func") or kw.get("reduce_func")
+        r = self._chunk_reduction(op, f)
+        axis = kw["axis"]
+        axis = (axis,) if isinstance(axis, int) else tuple(axis)
+        return r.program(x.ndim, x.dtype, axis, keepdims=True)
+
+    def _chunk_reduction(self, op, f):
+        """This package's ChunkReduction for a reference reduction callable
+        (a partial of ``_mean_func`` & co. or of a numpy reduction)."""
+        from .. import chunkfuncs as CF
+
+        base, kw, _ = _unwrap(f)
+        name, mod = getattr(base, "__name__", ""), _module_of(base)
+        named = {"_mean_func": CF._mean_func, "_mean_combine": CF._mean_combine,
+                 "_nanmean_func": CF._nanmean_func, "_nanmean_combine": CF._nanmean_combine,
+                 "_chunk_sum": CF._chunk_sum}
+        inner = None
+        if mod.startswith("cubed") and name in named:
+            inner = named[name]
+        elif name in _NUMPY_REDUCTION_NAMES:
+            inner = CF.as_chunk_reduction(getattr(np, name))
+        if inner is None:
+            raise LoweringError(f"op {op}: partial_reduce with {f!r} is not lowered")
+        kw = {k: v for k, v in kw.items() if k not in ("axis", "keepdims")}
+        return CF._BoundReduction(inner, kw) if kw else inner
 
     def _index_program(self, op, kw, keys, reads, out):
         """``index``'s map_direct function (core/ops.py:374-517): output block

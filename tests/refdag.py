@@ -373,6 +373,54 @@ def mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20)):
     return p.finalize(), sname, pname, name
 
 
+# -- reduction(..., use_new_impl=True): partial_reduce (core/ops.py:906-1090) --
+_partial_reduce = _ref_fn("_partial_reduce", "cubed.core.ops")
+
+
+def partial_reduce_mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20)):
+    """``reduction_new`` of the mean over axis 0 with split_every 4: ONE
+    partial_reduce op whose block function yields an iterator over the 4 row
+    blocks of a column block (initial_func ``_mean_func``, reduce_func
+    ``_mean_combine``), then ``_mean_aggregate`` + squeeze fused."""
+    p = RefPlan(work_dir)
+    rop, rname, rsrcs = p.random(shape, chunks, root_seed)
+    p.add(rop, rname, rsrcs)
+    X = p.g.nodes[rname]["target"]
+    idt = np.dtype([("n", np.int64), ("total", np.float64)])
+    nb = numblocks(shape, chunks)
+    pname = p._name("array")
+    pt = p.lazy_target(pname, (1, shape[1]), idt, (1, chunks[1]))
+
+    def block_function(out_key):
+        j = out_key[2]
+        return (iter([(rname, i, j) for i in range(nb[0])]),)
+
+    fn = functools.partial(_partial_reduce,
+                           reduce_func=functools.partial(_mean_combine, dtype=[("n", np.int64), ("total", np.float64)]),
+                           initial_func=functools.partial(_mean_func, dtype=[("n", np.int64), ("total", np.float64)]),
+                           axis=(0,))
+    spec = BlockwiseSpec(block_function, fn, 1, {rname: CubedArrayProxy(X, X.chunks)}, CubedArrayProxy(pt, pt.chunks))
+    pop = PrimitiveOperation(CubedPipeline(apply_blockwise, p._name("apply_blockwise"), [], spec), pt,
+                             0, p.MEM, 0, nb[1], True)
+    p.add(pop, pname, [rname])
+    aname = p._name("array")
+    agg, _ = p.blockwise_op(functools.partial(_mean_aggregate), aname, (1, shape[1]), np.float64,
+                            (1, chunks[1]), [(pname, pt)])
+    sname = p._name("array")
+    sq, starget = p.blockwise_op(functools.partial(np.squeeze, axis=(0,)), sname, (shape[1],), np.float64,
+                                 (chunks[1],), [(aname, p.g.nodes[aname]["target"])])
+    sq_spec = BlockwiseSpec(lambda k: [(aname, 0, k[1])], sq.pipeline.config.function, 1,
+                            sq.pipeline.config.reads_map, sq.pipeline.config.write)
+    sq = PrimitiveOperation(CubedPipeline(apply_blockwise, "apply_blockwise-sq", sq.pipeline.mappable, sq_spec),
+                            starget, 0, p.MEM, 0, sq.num_tasks, True)
+    b_op = fuse(agg, sq)
+    t = p.g.nodes[aname]["target"]
+    p.g.remove_node(aname)
+    p.lazy = [x for x in p.lazy if x is not t]
+    name = p._op(b_op, sname, [pname], b_op.num_tasks)
+    return p.finalize(), sname, rname, name
+
+
 # -- arg reductions (core/ops.py:1093-1153) -------------------------------------
 _arg_map_func = _ref_fn("_arg_map_func", "cubed.core.ops")
 _arg_func = _ref_fn("_arg_func", "cubed.core.ops")

@@ -258,6 +258,32 @@ def test_reference_matmul_plan_converts_to_a_gemm_chain(tmp_path, built, dry):
     assert kinds.count("GemmLaunch") == 1
 
 
+def test_reference_partial_reduce_plan_converts(tmp_path, built, dry):
+    """reduction(..., use_new_impl=True)'s partial_reduce op (a block
+    function yielding an iterator of input keys) converts and lowers."""
+    dag, out, src, op = refdag.partial_reduce_mean_plan(tmp_path, _seed(22))
+    conv = RD.convert_reference_dag(dag)
+    dry.launched.clear()
+    dry.execute_dag(conv.dag, array_names=[out])
+    kinds = {type(l).__name__ for l in dry.launched}
+    assert "FusedLaunch" in kinds and kinds <= {"FusedLaunch", "CopyLaunch", "_Alloc"}, kinds
+
+
+@pytest.mark.gpu
+def test_reference_partial_reduce_plan_on_the_gpu(tmp_path, gpu_executor):
+    """The partial_reduce mean against the f64 column means of the oracle's
+    Philox blocks, rtol 1e-12."""
+    from cubed_amd.zarr_io import ZarrV2Array
+    from oracle import cubed_ref as R
+
+    seed = _seed(23)
+    dag, out, src, op = refdag.partial_reduce_mean_plan(tmp_path, seed)
+    gpu_executor.execute_dag(dag, array_names=[out])
+    X = R.random_array((40, 60), (10, 20), seed)
+    got = ZarrV2Array.open(str(tmp_path / f"{out}.zarr"))[...]
+    np.testing.assert_allclose(got, X.mean(axis=0), rtol=1e-12, atol=0)
+
+
 def test_reference_argmax_plan_converts(tmp_path, built, dry):
     """The reference arg_reduction plan (map_blocks(_arg_map_func) with
     block_id + _arg_func, merge_chunks + _arg_combine + _arg_aggregate +
