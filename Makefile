@@ -2,7 +2,7 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := cubed_amd/csrc
-SRCS := $(CSRC)/fused.hip $(CSRC)/stream.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm_chain.hip
+SRCS := $(CSRC)/fused.hip $(CSRC)/stream_f32.hip $(CSRC)/stream_f64.hip $(CSRC)/stream_i64.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm_chain.hip
 CPPSRCS := $(CSRC)/codec.cpp
 OBJS := $(SRCS:.hip=.o) $(CPPSRCS:.cpp=.o)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
@@ -11,7 +11,7 @@ LIB := cubed_amd/libcubed_amd.so
 
 all: $(LIB) oracle
 
-$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h $(CSRC)/kernels.h include/cubed_amd.h
+$(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h $(CSRC)/kernels.h $(CSRC)/stream_impl.h include/cubed_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/%.o: $(CSRC)/%.cpp include/cubed_amd.h

@@ -59,8 +59,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
-EXTRAS = ("rechunk", "rechunk_mean", "rechunk_mean_share", "config1", "vorticity", "matmul_f32",
-          "matmul_bf16")
+EXTRAS = ("rechunk", "rechunk_mean", "rechunk_mean_share", "rechunk_mean_rehearsal", "config1", "vorticity",
+          "matmul_f32", "matmul_bf16")
+# RCCL all-reduce of the rehearsed ranks' group partials (50000 f64 totals =
+# 400 KB, + 50 int64 counts) over 8 GPUs: NOT measured here (one GPU per box);
+# an allowance added to the rehearsed per-rank step for the 8-GPU prediction
+RCCL_ALLOWANCE_US = 40.0
 
 
 def parse(argv=None):
@@ -77,6 +81,10 @@ def parse(argv=None):
     p.add_argument("--backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU or on CPU)")
+    p.add_argument("--rehearse-world", type=int, default=8,
+                   help="rechunk_mean_rehearsal: the world size whose ranks are rehearsed on one GPU")
+    p.add_argument("--rehearse-rank", default="all",
+                   help="rechunk_mean_rehearsal: comma list of ranks to rehearse (default: all)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC (see profiles/README.md)")
     return p.parse_args(argv)
@@ -476,6 +484,55 @@ def rechunk_mean_share_extra(args, ex, rank, world):
     return out
 
 
+def rechunk_mean_rehearsal_extra(args, rank, world, t1_ms=None):
+    """Config 3's rechunk+reduce as rank r of an N-rank job, rehearsed on this
+    one GPU (runtime.comm.LoopbackComm): the executor allocates rank r's
+    block-cyclic share of x (50000^2 f32, row chunks of 1000), lowers
+    mean(x.rechunk(columns), axis=0) with the rechunk read through exactly as
+    on N GPUs (DistPiecesLaunch: this rank's pieces -> SoA partials per output
+    group -> collective -> finish of its own output blocks), and every
+    collective is a local copy of the same bytes.  The step time is what rank
+    r's GPU spends outside xGMI; the 8-GPU prediction adds a stated RCCL
+    allowance (RCCL_ALLOWANCE_US, not measured) to the busiest rank."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.comm import LoopbackComm
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    W = args.rehearse_world
+    ranks = list(range(W)) if args.rehearse_rank == "all" else [int(r) for r in args.rehearse_rank.split(",")]
+    N = 50000
+    out = {"world": W, "ranks": {}}
+    for r in ranks:
+        ex = GpuDagExecutor(comm=LoopbackComm(r, W))
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2000)
+        x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        m = xp.mean(x.rechunk((N, 1000)), axis=0)
+        plan = arrays_to_plan(m)
+        step = step_fn(plan, ex, [m], x)
+        step()
+        step()
+        dt, summ = timed_launches(ex, step, 20, 1)
+        nchunks = len([c for c in range(x.numblocks[0]) if c % W == r])
+        out["ranks"][r] = dict(ms=round(dt * 1e3, 4), row_chunks=nchunks,
+                               input_gbs=round(nchunks * 1000 * N * 4 / dt / 1e9, 1),
+                               launches_ms=fmt_launches(summ), **overhead(dt, summ, 20))
+        del x, m, plan, ex
+        free_gpu()
+    busiest = max(v["ms"] for v in out["ranks"].values())
+    out["busiest_ms"] = busiest
+    out["rccl_allowance_us"] = RCCL_ALLOWANCE_US
+    out["predicted_step_ms"] = round(busiest + RCCL_ALLOWANCE_US / 1e3, 4)
+    if t1_ms:
+        out["one_gpu_step_ms"] = t1_ms
+        out["predicted_speedup"] = round(t1_ms / out["predicted_step_ms"], 2)
+    return out
+
+
 def config1_extra(args, ex, rank, world):
     import cubed_amd as cubed
     import cubed_amd.array_api as xp
@@ -758,6 +815,10 @@ def main(argv=None):
                 extra[name] = rechunk_mean_extra(args, ex, rank, world)
             elif name == "rechunk_mean_share":
                 extra[name] = rechunk_mean_share_extra(args, ex, rank, world)
+            elif name == "rechunk_mean_rehearsal":
+                if world == 1:
+                    t1 = extra.get("rechunk_mean", {}).get("elided", {}).get("ms")
+                    extra[name] = rechunk_mean_rehearsal_extra(args, rank, world, t1)
             elif name == "config1":
                 extra[name] = config1_extra(args, ex, rank, world)
             elif name == "vorticity":

@@ -30,14 +30,14 @@ import numpy as np
 
 MAX_DIMS = 6
 MAX_LEAVES = 4
-MAX_FIELDS = 2
-MAX_OUTS = 2
+MAX_FIELDS = 3
+MAX_OUTS = 3
 MAX_INSNS = 48
 MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 11  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 12  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -57,9 +57,9 @@ class Program(Structure):
         ("leaf_kind", c_uint8 * MAX_LEAVES), ("leaf_dtype", c_uint8 * MAX_LEAVES),
         ("nfields", c_int32),
         ("field_rop", c_uint8 * MAX_FIELDS), ("field_acc", c_uint8 * MAX_FIELDS),
-        ("field_src", c_uint8 * MAX_FIELDS), ("pad0", c_uint8 * 2),
+        ("field_src", c_uint8 * MAX_FIELDS), ("pad0", c_uint8 * 3),
         ("nouts", c_int32),
-        ("out_dtype", c_uint8 * MAX_OUTS), ("out_src", c_uint8 * MAX_OUTS),
+        ("out_dtype", c_uint8 * MAX_OUTS), ("out_src", c_uint8 * MAX_OUTS), ("pad1", c_uint8 * 2),
         ("ninsns", c_int32), ("nepi", c_int32),
         ("insns", Insn * MAX_INSNS), ("epi", Insn * MAX_EPI),
         ("consts", ConstVal * MAX_CONSTS),

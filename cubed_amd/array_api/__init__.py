@@ -55,5 +55,5 @@ from .manipulation_functions import (
     stack,
 )
 from .searching_functions import argmax, argmin, where
-from .statistical_functions import max, mean, min, prod, sum
+from .statistical_functions import max, mean, min, prod, std, sum, var
 from .utility_functions import all, any

@@ -6,7 +6,8 @@ functions are the program builders of cubed_amd.chunkfuncs."""
 
 import numpy as np
 
-from ..chunkfuncs import NumpyReduction, _mean_aggregate, _mean_combine, _mean_func
+from ..chunkfuncs import (NumpyReduction, _mean_aggregate, _mean_combine, _mean_func, _var_combine,
+                          _var_func, _VarAggregate)
 from ..core import reduction
 from .dtypes import (
     _numeric_dtypes,
@@ -80,3 +81,28 @@ def sum(x, /, *, axis=None, dtype=None, keepdims=False):
         dtype = _default_sum_dtype(x.dtype)
     return reduction(x, _np_sum, axis=axis, dtype=dtype, keepdims=keepdims,
                      extra_func_kwargs=dict(dtype=dtype))
+
+
+def _var_std(x, axis, correction, keepdims, use_new_impl, sqrt):
+    if x.dtype not in _real_floating_dtypes:
+        raise TypeError(f"Only real floating-point dtypes are allowed in {'std' if sqrt else 'var'}")
+    intermediate_dtype = [("n", np.int64), ("mu", np.float64), ("M2", np.float64)]
+    return reduction(x, _var_func, combine_func=_var_combine,
+                     aggegrate_func=_VarAggregate(correction, sqrt), axis=axis,
+                     intermediate_dtype=intermediate_dtype, dtype=x.dtype, keepdims=keepdims,
+                     use_new_impl=use_new_impl, extra_func_kwargs=dict(dtype=intermediate_dtype))
+
+
+def var(x, /, *, axis=None, correction=0.0, keepdims=False, use_new_impl=False):
+    """Array API ``var`` (not in the reference v0.12.0, api_status.md:74):
+    one fused pass of the {n, mu, M2} triple reduction (Welford per element,
+    Chan's update across chunks, merge rounds and GPUs) in f64, then
+    M2 / max(n - correction, 0), cast to x's dtype.  Matches numpy's
+    ``var(ddof=correction)`` computed in f64."""
+    return _var_std(x, axis, correction, keepdims, use_new_impl, sqrt=False)
+
+
+def std(x, /, *, axis=None, correction=0.0, keepdims=False, use_new_impl=False):
+    """Array API ``std`` (api_status.md:72): the square root of ``var``'s
+    aggregate, same single pass."""
+    return _var_std(x, axis, correction, keepdims, use_new_impl, sqrt=True)

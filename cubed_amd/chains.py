@@ -55,6 +55,8 @@ COMPOSE = {
     ("nanprod", "nanprod"): "nanprod", ("any", "any"): "any", ("all", "all"): "all",
     ("argmax", "argmax"): "argmax", ("argmin", "argmin"): "argmin", ("cprod", "cprod"): "cprod",
     ("pair_index", "pair_index"): "pair_index", ("pair_imag", "pair_imag"): "pair_imag",
+    ("var", "varc"): "var", ("varc", "varc"): "varc", ("var_mean", "var_mean"): "var_mean",
+    ("var_m2", "var_m2"): "var_m2",
 }
 
 

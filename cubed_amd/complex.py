@@ -74,6 +74,28 @@ def _const(v, dt):
     return ir.Const(np.array(v, dtype=dt).item(), np.dtype(dt))
 
 
+def _const_value(e):
+    """The value of a constant expression (a Const, possibly cast), else None."""
+    while isinstance(e, ir.Cast):
+        e = e.x
+    return e.value if isinstance(e, ir.Const) else None
+
+
+def _integral_exponent(br, bi):
+    """n when the exponent is the constant n + 0i with n integral and
+    |n| < 100 (npy_cpow's ``(n = (npy_intp)br) == br`` test), else None."""
+    r, i = _const_value(br), _const_value(bi)
+    if r is None or i is None:
+        return None
+    try:
+        r, i = float(np.real(r)), float(np.real(i))
+    except (TypeError, ValueError):
+        return None
+    if i != 0.0 or not np.isfinite(r) or r != int(r) or not -100 < int(r) < 100:
+        return None
+    return int(r)
+
+
 class _Splitter:
     def __init__(self):
         self.memo: Dict[int, Val] = {}
@@ -329,10 +351,49 @@ class _Splitter:
                                                                   _un("cos", y, p), p), p), e, p)
         return ("c", ir.Where(big, _bin("copysign", one, x, p), a, p), ir.Where(big, bb, b, p))
 
+    def _ipow(self, ar, ai, n, p) -> Val:
+        """npy_cpow's integer branch (numpy npymath npy_math_complex.c.src):
+        w = n + 0i with |n| < 100 multiplied out -- n = 1, 2, 3 directly,
+        otherwise binary exponentiation from 1 + 0i, and 1 / z^|n| (Smith's
+        division) for n < 0; z = 0 gives 0 + 0i for n > 0, nan + nan i for
+        n < 0.  The same IEEE operations in the same order, so x**2 of a
+        complex x is bit-identical to numpy (signed zeros included)."""
+        zero = _const(0, p)
+        if n == 0:
+            return ("c", _const(1, p), zero)
+        if n == 1:
+            res = ("c", ar, ai)
+        elif n == 2:
+            res = self._mul(ar, ai, ar, ai, p)
+        elif n == 3:
+            _, sr, si = self._mul(ar, ai, ar, ai, p)
+            res = self._mul(ar, ai, sr, si, p)
+        else:
+            m, mask = abs(n), 1
+            aa = (_const(1, p), zero)
+            pw = (ar, ai)
+            while True:
+                if m & mask:
+                    aa = self._mul(aa[0], aa[1], pw[0], pw[1], p)[1:]
+                mask <<= 1
+                if m < mask:
+                    break
+                pw = self._mul(pw[0], pw[1], pw[0], pw[1], p)[1:]
+            res = ("c",) + tuple(aa)
+            if n < 0:
+                res = self._div(_const(1, p), zero, res[1], res[2], p)
+        zero_z = _bin("logical_and", _bin("equal", ar, zero, np.bool_), _bin("equal", ai, zero, np.bool_),
+                      np.bool_)
+        zval = zero if n > 0 else _const(np.nan, p)
+        return ("c", ir.Where(zero_z, zval, res[1], p), ir.Where(zero_z, zval, res[2], p))
+
     def _pow(self, ar, ai, br, bi, p) -> Val:
         # z ** w = exp(w log z) (npy_cpow's general branch); w = 0 -> 1 + 0i,
-        # z = 0 with real w > 0 -> 0 + 0i.  numpy multiplies small integer
-        # powers out instead: the results agree to a few ulps (tested bound)
+        # z = 0 with real w > 0 -> 0 + 0i.  A constant integral w with |w| <
+        # 100 takes numpy's multiplied-out branch (_ipow)
+        n = _integral_exponent(br, bi)
+        if n is not None:
+            return self._ipow(ar, ai, n, p)
         lr = _un("log", _bin("hypot", ar, ai, p), p)
         li = _bin("atan2", ai, ar, p)
         _, er, ei = self._mul(br, bi, lr, li, p)

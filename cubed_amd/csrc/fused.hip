@@ -222,6 +222,12 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
   L.ws_bytes = (L.nsplit > 1 || partials)
                    ? (L.soa_elems + (int64_t)L.nsplit * ntasks * max_kept * P->nfields) * (int64_t)sizeof(Acc)
                    : 0;
+  if ((P->mode & CUBED_MODE_STREAM) && P->nfields > 0 && L.nsplit > 1) {
+    // stream_body's arrival counters: one uint32 per (task, column block)
+    const int64_t W = stream_w;
+    const int64_t slots = ((max_kept + 256 * W - 1) / (256 * W)) * 64;
+    L.ws_bytes += ntasks * ((slots + kBlock - 1) / kBlock) * 4;
+  }
   return L;
 }
 
@@ -258,14 +264,22 @@ int check_program(const cubed_program_t& P) {
     set_err("cubed_fused_chunks: program header out of range");
     return CUBED_E_ARG;
   }
+  const bool triple = P.nfields > 0 && triple_rop(P.field_rop[0]);
+  if (triple && (P.nfields != 3 || P.field_rop[1] != CUBED_R_VAR_MEAN || P.field_rop[2] != CUBED_R_VAR_M2 ||
+                 P.field_acc[0] != 1 || P.field_acc[1] != 0 || P.field_acc[2] != 0)) {
+    set_err("cubed_fused_chunks: a var triple is fields {n (i64), mu (f64), M2 (f64)}");
+    return CUBED_E_ARG;
+  }
   for (int f = 0; f < P.nfields; ++f) {
     const int rop = P.field_rop[f];
     const bool partner = rop == CUBED_R_PAIR_INDEX || rop == CUBED_R_PAIR_IMAG;
+    const bool tpartner = rop == CUBED_R_VAR_MEAN || rop == CUBED_R_VAR_M2;
     const bool pair_ok = f == 0 ? (!pair_rop(rop) || (P.nfields == 2 &&
                                    P.field_rop[1] == (rop == CUBED_R_CPROD ? CUBED_R_PAIR_IMAG : CUBED_R_PAIR_INDEX)))
                                 : (partner == pair_rop(P.field_rop[0]));
-    if (rop < CUBED_R_SUM || rop > CUBED_R_PAIR_IMAG || (f == 0 && partner) || !pair_ok) {
-      set_err("cubed_fused_chunks: bad reduction op (pair ops need their partner as field 1)");
+    if (rop < CUBED_R_SUM || rop > CUBED_R_VAR_M2 || (f == 0 && (partner || tpartner)) || !pair_ok ||
+        (f > 0 && tpartner != triple) || (f > 0 && triple_rop(rop))) {
+      set_err("cubed_fused_chunks: bad reduction op (pair / triple leads need their partners)");
       return CUBED_E_ARG;
     }
   }
@@ -331,6 +345,8 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
+  // streaming kernels fold their splits and write SoA partials themselves
+  if (P.mode & CUBED_MODE_STREAM) return 0;
   if (P.mode & CUBED_MODE_PARTIALS)
     return launch_collect(P, d_prog, L, d_tasks, ntasks, max_kept, (Acc*)d_workspace, st);
   if (L.nsplit > 1) {

@@ -89,7 +89,7 @@ CUBED_DEV void fused_a_body(
 
   for (int64_t item = b * kBlock + threadIdx.x; item < items; item += bpt * kBlock) {
     int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-    int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+    int64_t ooff[CUBED_MAX_OUTS] = {};
     int64_t k = item * VEC;
     const int64_t kflat = k;
 #pragma unroll
@@ -198,7 +198,7 @@ CUBED_DEV void fused_b_body(
   if (k >= nk) return;
 
   int64_t loff[CUBED_MAX_LEAVES] = {0, 0, 0, 0};
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t ooff[CUBED_MAX_OUTS] = {};
   {
     int64_t kk = k;
 #pragma unroll
@@ -379,7 +379,7 @@ CUBED_DEV void finalize_body(
   int64_t nk = 1;
   for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
   if (k >= nk) return;
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t ooff[CUBED_MAX_OUTS] = {};
   int64_t kk = k;
   for (int d = kd1 - 1; d >= kd0; --d) {
     int64_t q, c;
@@ -429,7 +429,7 @@ CUBED_DEV void finish_soa_body(
   int64_t nk = 1;
   for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
   if (k >= nk) return;
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t ooff[CUBED_MAX_OUTS] = {};
   int64_t kk = k;
   for (int d = kd1 - 1; d >= kd0; --d) {
     int64_t q, c;
@@ -460,7 +460,7 @@ CUBED_DEV void finish_groups_body(
   int64_t nk = 1;
   for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
   if (k >= nk) return;
-  int64_t ooff[CUBED_MAX_OUTS] = {0, 0};
+  int64_t ooff[CUBED_MAX_OUTS] = {};
   int64_t kk = k;
   for (int d = kd1 - 1; d >= kd0; --d) {
     int64_t q, c;
@@ -817,6 +817,18 @@ CUBED_DEV void stream_rows(Acc (&acc)[W][CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
   }
 }
 
+// Split accumulators shared between the workgroups of one column block:
+// agent-scope relaxed atomics, i.e. stores written through to memory and
+// loads that miss the (per-XCD, non-coherent) L2.
+CUBED_DEV void store_through(Acc* p, Acc v) {
+  __hip_atomic_store(&p->i, v.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+CUBED_DEV Acc load_through(const Acc* p) {
+  Acc v;
+  v.i = __hip_atomic_load(&p->i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
 // W: kept VEC groups per thread (stream_groups()).  The 64 lanes of a wave
 // own a block of 256 * W consecutive kept elements: group j of lane L starts
 // at block + 256 j + 4 L (4-byte elements: every 16-byte load instruction of
@@ -824,7 +836,9 @@ CUBED_DEV void stream_rows(Acc (&acc)[W][CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
 // block + 256 j + 2 L as the pairs (k, k+1), (k+128, k+129) (again 1 KiB per
 // instruction); a last partial 256-element run of 8-byte elements falls back
 // to 4 consecutive elements per lane (dk = 2).  W = 1 is the round-2 mapping.
-template <typename V, int NL, int U, int W = 1>
+// SPLIT: the kernel variant for nsplit > 1 (the split handshake and fold);
+// the unsplit variant carries none of it (same registers as a plain stream).
+template <typename V, int NL, int U, int W = 1, bool SPLIT = false>
 CUBED_DEV void stream_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t bpt, int32_t nsplit, Acc* __restrict__ ws, int64_t max_kept) {
@@ -870,11 +884,10 @@ CUBED_DEV void stream_body(
   for (int l = 0; l < NL; ++l) all_streamed = all_streamed && rs[l] != 0;
 
   constexpr bool IL = sizeof(V) == 8;
-  for (int64_t it = b * kBlock + threadIdx.x; it < slots; it += bpt * kBlock) {
+  // a wave's W groups of 4 kept elements (the lane-interleaved mapping above)
+  auto groups_of = [&](int64_t it, int64_t (&go)[W], int64_t (&dk)[W], bool (&gv)[W]) {
     const int64_t wb = (it >> 6) * (256 * W);
     const int lane = (int)(it & 63);
-    int64_t go[W], dk[W];
-    bool gv[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const int64_t sub = wb + 256 * j;
@@ -887,8 +900,13 @@ CUBED_DEV void stream_body(
       }
       gv[j] = go[j] + 4 <= nk || (dk[j] == 128);
     }
-    Regs<V, 4> regs;
-    if (P.nfields == 0) {
+  };
+  if (P.nfields == 0) {
+    for (int64_t it = b * kBlock + threadIdx.x; it < slots; it += bpt * kBlock) {
+      int64_t go[W], dk[W];
+      bool gv[W];
+      groups_of(it, go, dk, gv);
+      Regs<V, 4> regs;
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         if (!gv[j]) continue;
@@ -915,8 +933,49 @@ CUBED_DEV void stream_body(
           }
         }
       }
-      continue;
     }
+    return;
+  }
+
+  // ---- reductions.  Three endings per kept element:
+  //  * unsplit: the epilogue (or, in partials mode, the SoA partials) here;
+  //  * split: every workgroup leaves its split's accumulators in the
+  //    workspace, and the LAST workgroup of the nsplit splits of one column
+  //    block to arrive (a per-(task, block) arrival counter) folds them in
+  //    split order -- k_finalize's order, so the same bits -- and finishes.
+  //    No second launch.  COUNT fields are never stored: every split counts
+  //    its own trip count, the fold takes the whole reduced extent.
+  // Workspace layout: [SoA partials (partials mode)] [split accumulators]
+  // [arrival counters, uint32 per (task, column block)]; the counters start at
+  // zero (the host zeroes the workspace once) and the last arrival resets
+  // its counter, so they are zero again after every launch.
+  const bool partials = (P.mode & CUBED_MODE_PARTIALS) != 0;
+  const int nf = P.nfields;
+  const int64_t nsoa = ntasks * max_kept;
+  Acc* __restrict__ soa = ws - (int64_t)nf * nsoa;
+  const int64_t slots_max = ((max_kept + 256 * W - 1) / (256 * W)) * 64;
+  const int64_t nblk = (slots_max + kBlock - 1) / kBlock;
+  uint32_t* __restrict__ cnt = (uint32_t*)(ws + (int64_t)nsplit * nsoa * nf);
+  __shared__ int last_arrival;
+  // partials mode writes every element < max_kept (the identity past an
+  // edge task's extent), so every column block of max_kept takes part
+  const int64_t wslots = partials ? slots_max : slots;
+  auto store_soa = [&](int64_t el, const Acc (&x)[CUBED_MAX_FIELDS], bool valid) {
+    if (el >= max_kept) return;
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+      if (f < nf) soa[f * nsoa + t * max_kept + el] = valid ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
+  };
+  // (block-uniform trip count: the arrival handshake below has barriers)
+  for (int64_t bb = b * kBlock; bb < wslots; bb += bpt * kBlock) {
+    const int64_t it = bb + threadIdx.x;
+    int64_t go[W], dk[W];
+    bool gv[W];
+    groups_of(it, go, dk, gv);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < W; ++j) any = any || gv[j];
+    Regs<V, 4> regs;
     Acc acc[W][CUBED_MAX_FIELDS][4];
 #pragma unroll
     for (int j = 0; j < W; ++j)
@@ -926,7 +985,7 @@ CUBED_DEV void stream_body(
         for (int e = 0; e < 4; ++e) acc[j][f][e] = acc_init(P.field_rop[f], P.field_acc[f]);
 
     // flattened reduced range [r0, r1) = (chunk q, row) pairs in order
-    for (int64_t q = nrow ? r0 / nrow : 0; q < nq && q * nrow < r1; ++q) {
+    for (int64_t q = nrow ? r0 / nrow : 0; any && q < nq && q * nrow < r1; ++q) {
       const int64_t lo = (r0 > q * nrow ? r0 : q * nrow) - q * nrow;
       const int64_t hi = (r1 < (q + 1) * nrow ? r1 : (q + 1) * nrow) - q * nrow;
       const CUBED_G V* p[NL];
@@ -937,43 +996,122 @@ CUBED_DEV void stream_body(
       else
         stream_rows<V, NL, U, W, true>(acc, regs, P, p, rs, lo, hi, go, dk, gv);
     }
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      if (!gv[j]) continue;
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-        if (f < P.nfields && P.field_rop[f] == CUBED_R_COUNT)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[j][f][e].i += r1 - r0;
 
-      int64_t ooff[CUBED_MAX_OUTS];
+    if constexpr (SPLIT) {
+      Acc* __restrict__ w = ws + ((int64_t)(s * ntasks + t) * max_kept) * nf;
 #pragma unroll
-      for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] = go[j];
-      if (nsplit == 1 && !(P.mode & CUBED_MODE_PARTIALS)) {
-        if constexpr (IL) {
-          Acc a0[CUBED_MAX_FIELDS][2], a1[CUBED_MAX_FIELDS][2];
-#pragma unroll
-          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-            a0[f][0] = acc[j][f][0]; a0[f][1] = acc[j][f][1];
-            a1[f][0] = acc[j][f][2]; a1[f][1] = acc[j][f][3];
-          }
-          int64_t o1[CUBED_MAX_OUTS];
-#pragma unroll
-          for (int o = 0; o < CUBED_MAX_OUTS; ++o) o1[o] = ooff[o] + dk[j];
-          finish<2>(P, T, a0, ooff);
-          finish<2>(P, T, a1, o1);
-        } else {
-          finish<4>(P, T, acc[j], ooff);
-        }
-      } else {
-        Acc* w = ws + ((int64_t)(s * ntasks + t) * max_kept) * P.nfields;
+      for (int j = 0; j < W; ++j) {
+        if (!gv[j]) continue;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int64_t el = go[j] + (e >> 1) * dk[j] + (e & 1);
 #pragma unroll
           for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-            if (f < P.nfields) w[el * P.nfields + f] = acc[j][f][e];
+            if (f < nf && P.field_rop[f] != CUBED_R_COUNT) store_through(&w[el * nf + f], acc[j][f][e]);
         }
+      }
+      // Handshake without L2 maintenance: the accumulators above are
+      // write-through stores (agent scope) -- the 8 XCDs' L2s are not
+      // coherent with each other, and an agent-scope release/acquire fence
+      // would write back and invalidate this XCD's whole L2 per workgroup
+      // (measured 2x slower on the per-rank share).  Waiting for the stores
+      // to complete before the barrier orders them before the arrival count.
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t* c = cnt + t * nblk + bb / kBlock;
+        const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int lastv = old == (uint32_t)(nsplit - 1);
+        if (lastv) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_arrival = lastv;
+      }
+      __syncthreads();
+      if (!last_arrival) continue;
+      // the other splits' accumulators: read past this XCD's L2 (load_through)
+      // fold splits 0..nsplit-1 in order (this workgroup's own included)
+      const int64_t sstride = nsoa * nf;
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (!gv[j]) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t el = go[j] + (e >> 1) * dk[j] + (e & 1);
+          const Acc* __restrict__ pp = ws + ((int64_t)t * max_kept + el) * nf;
+          Acc x[CUBED_MAX_FIELDS];
+#pragma unroll
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+            if (f < nf && P.field_rop[f] != CUBED_R_COUNT) x[f] = load_through(&pp[f]);
+            else x[f] = acc_init(P.field_rop[f], P.field_acc[f]);
+          }
+          int sp = 1;
+          for (; sp + 4 <= nsplit; sp += 4) {
+            Acc v[4][CUBED_MAX_FIELDS];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+              for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+                v[u][f] = (f < nf && P.field_rop[f] != CUBED_R_COUNT)
+                              ? load_through(&pp[(int64_t)(sp + u) * sstride + f])
+                              : acc_init(P.field_rop[f], P.field_acc[f]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fields_combine(x, v[u], P);
+          }
+          for (; sp < nsplit; ++sp) {
+            Acc v[CUBED_MAX_FIELDS];
+#pragma unroll
+            for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+              v[f] = (f < nf && P.field_rop[f] != CUBED_R_COUNT) ? load_through(&pp[(int64_t)sp * sstride + f])
+                                                                   : acc_init(P.field_rop[f], P.field_acc[f]);
+            fields_combine(x, v, P);
+          }
+#pragma unroll
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+            if (f < nf && P.field_rop[f] == CUBED_R_COUNT) x[f].i = nrd;
+            acc[j][f][e] = x[f];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+#pragma unroll
+        for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+          if (f < nf && P.field_rop[f] == CUBED_R_COUNT)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[j][f][e].i += r1 - r0;
+    }
+
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (partials) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t el = go[j] + (e >> 1) * dk[j] + (e & 1);
+          Acc x[CUBED_MAX_FIELDS];
+#pragma unroll
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) x[f] = acc[j][f][e];
+          store_soa(el, x, gv[j]);
+        }
+        continue;
+      }
+      if (!gv[j]) continue;
+      int64_t ooff[CUBED_MAX_OUTS];
+#pragma unroll
+      for (int o = 0; o < CUBED_MAX_OUTS; ++o) ooff[o] = go[j];
+      if constexpr (IL) {
+        Acc a0[CUBED_MAX_FIELDS][2], a1[CUBED_MAX_FIELDS][2];
+#pragma unroll
+        for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
+          a0[f][0] = acc[j][f][0]; a0[f][1] = acc[j][f][1];
+          a1[f][0] = acc[j][f][2]; a1[f][1] = acc[j][f][3];
+        }
+        int64_t o1[CUBED_MAX_OUTS];
+#pragma unroll
+        for (int o = 0; o < CUBED_MAX_OUTS; ++o) o1[o] = ooff[o] + dk[j];
+        finish<2>(P, T, a0, ooff);
+        finish<2>(P, T, a1, o1);
+      } else {
+        finish<4>(P, T, acc[j], ooff);
       }
     }
   }

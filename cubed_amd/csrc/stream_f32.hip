@@ -1,0 +1,3 @@
+// stream_f32.hip -- the streaming kernels (stream_impl.h) for float values.
+#define CUBED_STREAM_V float
+#include "stream_impl.h"

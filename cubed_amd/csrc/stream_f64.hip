@@ -1,0 +1,3 @@
+// stream_f64.hip -- the streaming kernels (stream_impl.h) for double values.
+#define CUBED_STREAM_V double
+#include "stream_impl.h"

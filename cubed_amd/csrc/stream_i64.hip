@@ -1,0 +1,3 @@
+// stream_i64.hip -- the streaming kernels (stream_impl.h) for int64_t values.
+#define CUBED_STREAM_V int64_t
+#include "stream_impl.h"

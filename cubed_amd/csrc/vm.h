@@ -306,6 +306,9 @@ CUBED_DEV Acc acc_init(int rop, int acc_i) {
     case CUBED_R_PAIR_INDEX: a.i = INT64_MAX; break;
     case CUBED_R_CPROD: a.f = 1.0; break;
     case CUBED_R_PAIR_IMAG: a.f = 0.0; break;
+    // var triples start empty: {n = 0, mu = 0, M2 = 0}
+    case CUBED_R_VAR: case CUBED_R_VARC: a.i = 0; break;
+    case CUBED_R_VAR_MEAN: case CUBED_R_VAR_M2: a.f = 0.0; break;
     default: a.i = 0; break;
   }
   return a;
@@ -336,6 +339,33 @@ CUBED_DEV void pair_combine(Acc& a0, Acc& a1, Acc b0, Acc b1, int rop, int acc_i
               : (bn || (mx ? b0.f > a0.f : b0.f < a0.f) || (b0.f == a0.f && b1.i < a1.i));
   }
   if (take) { a0 = b0; a1 = b1; }
+}
+
+// ---- var triples {n, mu, M2} (field 0 leads; include/cubed_amd.h cubed_rop)
+__host__ __device__ inline bool triple_rop(int rop) { return rop == CUBED_R_VAR || rop == CUBED_R_VARC; }
+
+// Chan, Golub & LeVeque's pairwise update: {n, mu, M2} (+)= {nb, mb, Mb}.
+// An empty side leaves the other unchanged (so identities and empty tasks
+// fold away exactly); NaN / inf propagate through d as in numpy's var.
+CUBED_DEV void var_combine(Acc& n, Acc& mu, Acc& m2, int64_t nb, double mb, double Mb) {
+#pragma clang fp contract(off)
+  if (nb == 0) return;
+  if (n.i == 0) { n.i = nb; mu.f = mb; m2.f = Mb; return; }
+  const int64_t na = n.i, nn = na + nb;
+  const double d = mb - mu.f;
+  const double fb = (double)nb / (double)nn;
+  mu.f = mu.f + d * fb;
+  m2.f = m2.f + Mb + d * d * ((double)na * fb);
+  n.i = nn;
+}
+
+// Welford's update: fold one value x into {n, mu, M2}
+CUBED_DEV void var_add(Acc& n, Acc& mu, Acc& m2, double x) {
+#pragma clang fp contract(off)
+  n.i += 1;
+  const double d = x - mu.f;
+  mu.f = mu.f + d / (double)n.i;
+  m2.f = m2.f + d * (x - mu.f);
 }
 
 template <typename V>
@@ -413,6 +443,10 @@ CUBED_DEV Acc shfl_xor_acc(Acc a, int m) {
 // one; its partner rop leaves acc_combine a no-op)
 CUBED_DEV void fields_combine(Acc (&x)[CUBED_MAX_FIELDS], const Acc (&y)[CUBED_MAX_FIELDS],
                               const cubed_program_t& P) {
+  if (triple_rop(P.field_rop[0])) {
+    var_combine(x[0], x[1], x[2], y[0].i, y[1].f, y[2].f);
+    return;
+  }
   if (pair_rop(P.field_rop[0])) {
     pair_combine(x[0], x[1], y[0], y[1], P.field_rop[0], P.field_acc[0]);
     return;
@@ -427,6 +461,17 @@ CUBED_DEV void fields_combine(Acc (&x)[CUBED_MAX_FIELDS], const Acc (&y)[CUBED_M
 template <typename V, int VEC, bool SKIP_COUNT = false>
 CUBED_DEV void fields_add(Acc (&acc)[CUBED_MAX_FIELDS][VEC], const V (&src)[CUBED_MAX_FIELDS][VEC],
                           const cubed_program_t& P) {
+  if (triple_rop(P.field_rop[0])) {
+    if (P.field_rop[0] == CUBED_R_VAR) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) var_add(acc[0][j], acc[1][j], acc[2][j], (double)src[0][j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        var_combine(acc[0][j], acc[1][j], acc[2][j], to_i64(src[0][j]), (double)src[1][j], (double)src[2][j]);
+    }
+    return;
+  }
   if (pair_rop(P.field_rop[0])) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j)

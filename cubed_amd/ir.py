@@ -127,8 +127,12 @@ ROPS = {"sum": 1, "nansum": 2, "count": 3, "count_nonnan": 4, "max": 5, "min": 6
         "prod": 7, "nanmax": 8, "nanmin": 9, "any": 10, "all": 11, "nanprod": 12,
         # pair reductions: field 0 = the lead, field 1 = its partner
         # (include/cubed_amd.h cubed_rop)
-        "argmax": 13, "argmin": 14, "cprod": 15, "pair_index": 16, "pair_imag": 17}
+        "argmax": 13, "argmin": 14, "cprod": 15, "pair_index": 16, "pair_imag": 17,
+        # var triples: field 0 = n (var: folds values, varc: folds {n, mu, M2}
+        # partials), field 1 = mu, field 2 = M2 (Chan's pairwise update)
+        "var": 18, "varc": 19, "var_mean": 20, "var_m2": 21}
 PAIR_PARTNER = {"argmax": "pair_index", "argmin": "pair_index", "cprod": "pair_imag"}
+TRIPLE_ROPS = ("var", "varc")
 
 
 # ----------------------------------------------------------------- expressions
@@ -764,9 +768,9 @@ def reduction_result_dtype(rop: str, dtype, requested=None) -> np.dtype:
 
 def acc_is_int(rop: str, dtype) -> bool:
     dtype = np.dtype(dtype)
-    if rop in ("count", "count_nonnan", "any", "all", "pair_index"):
+    if rop in ("count", "count_nonnan", "any", "all", "pair_index", "var", "varc"):
         return True
-    if rop in ("cprod", "pair_imag"):
+    if rop in ("cprod", "pair_imag", "var_mean", "var_m2"):
         return False
     return dtype.kind in "iub"
 

@@ -675,7 +675,9 @@ class FusedLaunch:
         self.max_kept = max_kept
         self.max_red = max_red
         self.gathers = gathers
-        self.ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=device) if ws_bytes else None
+        # zeroed once: the streaming kernels' split-arrival counters live at its
+        # end and are reset to zero by the kernels themselves
+        self.ws = torch.zeros(max(ws_bytes, 16), dtype=torch.uint8, device=device) if ws_bytes else None
         self.ws_bytes = ws_bytes
 
     groups = None
@@ -794,7 +796,8 @@ class Lowerer:
         return self.ctx.device_source(proxy.array)
 
     def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
-                            rows_fn=None, sample_key=None, partials=False, lift=True):
+                            rows_fn=None, sample_key=None, partials=False, lift=True,
+                            merge_kept_groups=False):
         """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
         ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
         per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
@@ -927,6 +930,8 @@ class Lowerer:
 
         # outputs
         fields_of_target = target.fields
+        if len(out_items) > nat.MAX_OUTS:
+            raise LoweringError(f"fused program writes {len(out_items)} outputs (max {nat.MAX_OUTS})")
         P.nouts = len(out_items)
         for o, (name, _) in enumerate(out_items):
             fname = name if structured_out else None
@@ -1001,6 +1006,23 @@ class Lowerer:
                 rows = layout.rows
                 if group_start is not None:
                     group_start = np.arange(len(rows) + 1, dtype=np.int64)
+        group_layout = None
+        if stream and merge_kept_groups and merge_kept_groups() and MERGE_KEPT and partials and not lifted \
+                and group_start is None:
+            # one row per output group (DistPiecesLaunch): consecutive groups
+            # whose rows continue each other along the packed kept dim stream
+            # as one wide task.  The main kernel writes only SoA partials, so
+            # outputs do not constrain the merge; kept only when the merged
+            # SoA [task][kept] is byte-identical to the per-group SoA
+            # [group][kept] (every task and every group the same extent).
+            merged = _merge_kept_runs(layout, [np.dtype(l.dtype).itemsize for l in leaves], [])
+            if merged is not None and \
+                    all(r.extent[-1] == merged.max_kept for r in merged.rows) and \
+                    all(_apply_groups(r, layout.groups)[0][-1] == layout.max_kept for r in layout.rows) and \
+                    len(merged.rows) * merged.max_kept == len(layout.rows) * layout.max_kept:
+                group_layout = layout
+                layout = merged
+                rows = layout.rows
         if stream:
             P.mode |= MODE_STREAM | _stream_groups_mode(P, len(rows), layout.max_kept)
         if partials:
@@ -1012,6 +1034,7 @@ class Lowerer:
         launch = FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
                              gathers, self.ctx.device)
         launch.layout = layout
+        launch.group_layout = group_layout
         if lifted:
             # the epilogue program: same instructions, every dim reduced (one output per task)
             fin = nat.Program()
@@ -1674,7 +1697,7 @@ def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
 
 
 def _stream_ok(layout: Layout, leaves, kinds, vtype, check_outputs=True) -> bool:
-    """Geometry of the streaming fast path (stream.hip): kernel A with VEC=4,
+    """Geometry of the streaming fast path (stream_impl.h): kernel A with VEC=4,
     one kept kernel dim (packed in every leaf and output) after at most two
     reduced dims (chunk index x rows), every leaf an array chunk in the VM's
     own dtype."""

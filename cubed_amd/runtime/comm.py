@@ -145,6 +145,78 @@ class Pending:
         self.works, self.fixups = [], []
 
 
+class LoopbackComm:
+    """Rank ``rank`` of a ``world``-rank job, rehearsed in ONE process on one
+    GPU: the executor plans, allocates and launches exactly what that rank
+    runs (its block-cyclic share of every array, its pieces, its partials),
+    and every collective becomes a local device copy of the same bytes on the
+    current stream -- the HBM traffic the rank's own side of the collective
+    causes, without the xGMI transfer.  Values are NOT combined across ranks
+    (there are no other ranks): a rehearsal times the per-rank launch list; a
+    test folds the recorded partials of all ``world`` rehearsed ranks itself
+    (``record=True`` keeps a copy of every reduce / all-reduce input, in
+    issue order, in ``self.records``)."""
+
+    backend = "loopback"
+    staged = False
+
+    def __init__(self, rank: int, world: int, record: bool = False):
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside a world of {world}")
+        self.rank, self.world = rank, world
+        self.record = record
+        self.records: List = []
+        self._scratch = None
+
+    def _copy(self, t):
+        """Read + write ``t``'s bytes once (into a scratch buffer)."""
+        import torch
+
+        flat = t.reshape(-1)
+        if self._scratch is None or self._scratch.numel() < flat.numel() * flat.element_size() \
+                or self._scratch.device != flat.device:
+            self._scratch = torch.empty(max(flat.numel() * flat.element_size(), 16), dtype=torch.uint8,
+                                        device=flat.device)
+        self._scratch[:flat.numel() * flat.element_size()].view(flat.dtype).copy_(flat)
+
+    def barrier(self):
+        pass
+
+    def all_to_all(self, recv, send, recv_splits, send_splits):
+        n = min(sum(map(int, recv_splits)), sum(map(int, send_splits)))
+        if n:
+            recv[:n].copy_(send[:n])
+
+    def exchange(self, sends, recvs) -> "Pending":
+        for (s, _), (r, _) in zip(sends, recvs):
+            n = min(s.numel(), r.numel())
+            r.reshape(-1)[:n].copy_(s.reshape(-1)[:n])
+        return Pending([], [])
+
+    def _reduce(self, kind, t):
+        if self.record:
+            self.records.append((kind, t.detach().clone()))
+        self._copy(t)
+
+    def all_reduce_sum(self, t):
+        self._reduce("all_reduce_sum", t)
+
+    def reduce_sum(self, t, dst: int):
+        self._reduce("reduce_sum", t)
+
+    def all_gather(self, out, t):
+        flat = t.reshape(-1)
+        o = out.reshape(-1)
+        for r in range(self.world):
+            o[r * flat.numel():(r + 1) * flat.numel()].copy_(flat)
+
+    def broadcast(self, t, src: int):
+        self._copy(t)
+
+    def all_ok(self, ok: bool) -> bool:
+        return bool(ok)
+
+
 def default_comm() -> Optional[Comm]:
     """The world process group when torch.distributed runs with > 1 rank."""
     try:

@@ -290,7 +290,8 @@ class DistPiecesLaunch:
     combined over RCCL, and the owners of the outputs run the epilogue
     (cubed_fused_finish over one row per group)."""
 
-    def __init__(self, ctx, fused, group_start, group_table, max_kept_out, rops, acc_int, owners):
+    def __init__(self, ctx, fused, group_start, group_table, max_kept_out, rops, acc_int, owners,
+                 soa_direct=False):
         import torch
 
         self.ctx = ctx
@@ -301,7 +302,18 @@ class DistPiecesLaunch:
         self.mko = max_kept_out
         self.nf = len(rops)
         self.n = self.ngroups * max_kept_out
-        self.gsoa = torch.empty(max(self.nf * self.n * 8, 16), dtype=torch.uint8, device=ctx.device)
+        # soa_direct: the fused launch streamed this rank's one row per group as
+        # merged kept runs; its SoA partials [f][task][kept] are byte for byte
+        # the per-group partials [f][group][kept], so no combine_groups pass
+        self.soa_direct = soa_direct
+        if soa_direct:
+            assert fused.ntasks * fused.max_kept == self.n
+            self.gsoa = fused.ws
+        else:
+            self.gsoa = torch.empty(max(self.nf * self.n * 8, 16), dtype=torch.uint8, device=ctx.device)
+        # a plain COUNT field (mean's n) is uniform over the kept elements of a
+        # group: one int64 per group crosses the ranks (as in PartialsLaunch)
+        self.uniform = [r == "count" for r in rops]
         self.sum_only = all(r in SUM_ROPS for r in rops)
         self.acc_int = acc_int
         uniq = sorted(set(owners))
@@ -320,17 +332,25 @@ class DistPiecesLaunch:
         F = self.fused
         L = nat.lib()
         F.run(stream)
-        nat.check(L.cubed_combine_groups(F.prog, F.d_prog.data_ptr(), F.table.data_ptr(), F.ntasks,
-                                         F.max_kept, F.ws.data_ptr(), self.gs.data_ptr(), self.ngroups,
-                                         self.mko, self.gsoa.data_ptr(), stream), "cubed_combine_groups")
+        if not self.soa_direct:
+            nat.check(L.cubed_combine_groups(F.prog, F.d_prog.data_ptr(), F.table.data_ptr(), F.ntasks,
+                                             F.max_kept, F.ws.data_ptr(), self.gs.data_ptr(), self.ngroups,
+                                             self.mko, self.gsoa.data_ptr(), stream), "cubed_combine_groups")
         comm = self.ctx.comm
         if self.sum_only:
+            mk = self.mko
             for f in range(self.nf):
                 v = self.field_view(f)
+                per_group = self.uniform[f] and mk > 1
+                if per_group:
+                    blocks = v.view(-1, mk)
+                    v = blocks[:, 0].contiguous()
                 if self.root is not None:
                     comm.reduce_sum(v, self.root)
                 else:
                     comm.all_reduce_sum(v)
+                if per_group and (self.root is None or self.ctx.rank == self.root):
+                    blocks.copy_(v[:, None].expand_as(blocks))
         else:
             comm.all_gather(self.gathered, self.gsoa[: self.nf * self.n * 8])
             if self.finish_here:

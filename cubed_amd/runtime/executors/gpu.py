@@ -510,22 +510,35 @@ class GpuDagExecutor(DagExecutor):
                 # slab (its chunks' slots are consecutive): one row per run
                 rows, gkeys = L._merge_group_rows(rows, gkeys, red, leaves)
             meta["starts"] = [i for i in range(len(gkeys)) if i == 0 or gkeys[i] != gkeys[i - 1]]
+            meta["nrows"] = len(rows)
+            meta["kept_ok"] = all(math.prod(r.extent[d] for d in range(len(r.extent)) if d not in red) == mko
+                                  for r in rows)
             meta["mko"] = mko
             return rows, red
 
+        def one_row_per_group():
+            return meta["nrows"] == len(meta["starts"]) and meta["kept_ok"]
+
         try:
             launch = low.lower_expr_pipeline(program, cfg, target, keys, rows_fn=rows_fn,
-                                             sample_key=keys[0], partials=True, lift=False)
+                                             sample_key=keys[0], partials=True, lift=False,
+                                             merge_kept_groups=one_row_per_group)
         except LoweringError:
             return None
         starts = meta["starts"]
-        lay = launch.layout
+        lay = launch.group_layout or launch.layout
         table = dataclasses.replace(lay, rows=[lay.rows[i] for i in starts]).table(self.device)
         rops = [f.rop for f in program.reduce.fields]
         acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
+        # one row per group streamed as wide merged tasks: the kernel's SoA
+        # partials already are the per-group partials (no combine_groups)
+        soa_direct = launch.group_layout is not None and len(starts) == len(lay.rows) and \
+            lay.max_kept == meta["mko"]
+        assert launch.group_layout is None or soa_direct, "merged kept runs need one row per group"
         out = [meta["fetch"]] if meta.get("fetch") is not None else []
         out.append(DistPiecesLaunch(self, launch, np.array(starts + [len(lay.rows)], dtype=np.int64),
-                                    table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys]))
+                                    table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys],
+                                    soa_direct=soa_direct))
         return out
 
     def _lower_local(self, program, cfg, target, keys):
@@ -927,7 +940,7 @@ class GpuDagExecutor(DagExecutor):
         if self.check_memory:
             self._check_hbm(dag)
         targets = [d["target"] for _, d in dag.nodes(data=True) if isinstance(d.get("target"), DeviceArray)]
-        state = tuple(t.written for t in targets)
+        state = target_state(targets)
         gen_of = {}
         if parallel:
             for g, names in enumerate(nx.topological_generations(dag)):
@@ -1159,6 +1172,12 @@ class _Schedule:
         self.epoch = alloc_epoch()
 
 
+def target_state(targets):
+    """What a recorded schedule depends on: which targets are written (in
+    HBM) or complete in their Zarr store (resume)."""
+    return tuple((t.written, bool(getattr(t, "zarr_complete", False))) for t in targets)
+
+
 class _Schedules:
     """The recorded schedules of one (plan DAG, array names, resume) by the
     written state of the plan's targets they start from.  A schedule is
@@ -1173,7 +1192,7 @@ class _Schedules:
     def lookup(self):
         from ...storage import alloc_epoch
 
-        sched = self.by_state.get(tuple(t.written for t in self.targets))
+        sched = self.by_state.get(target_state(self.targets))
         if sched is not None and sched.epoch == alloc_epoch():
             return sched
         return None

@@ -6,8 +6,11 @@ import networkx as nx
 
 
 def _target_complete(target) -> bool:
-    written = getattr(target, "written", None)
-    return bool(written)
+    """An HBM target written by an earlier compute (and still resident), or
+    one whose Zarr store holds every chunk (``zarr_complete``, set for a
+    resumed reference DAG: the reference's nchunks_initialized check,
+    cubed/runtime/pipeline.py:25-33)."""
+    return bool(getattr(target, "written", None)) or bool(getattr(target, "zarr_complete", False))
 
 
 def already_computed(name, dag, nodes: Dict[str, Any], resume: Optional[bool] = None) -> bool:

@@ -618,23 +618,62 @@ def convert_reference_dag(dag) -> ConvertedDag:
 def execute_reference_dag(executor, dag, callbacks=None, array_names=None, resume=None, spec=None,
                           **kwargs):
     """Run a reference-built DAG on ``executor`` and write the requested
-    arrays to their Zarr stores."""
+    arrays to their Zarr stores.  With ``resume``, an array whose Zarr store
+    already holds every chunk counts as computed (cubed/runtime/pipeline.py
+    :25-33, whatever process wrote it); one that an op still to run reads is
+    uploaded from its store first.  Afterwards the converted arrays' HBM is
+    released: the results live in their Zarr stores, which is where the
+    reference reads them from (and the reference keeps finalized DAGs -- so
+    this conversion -- alive in an lru_cache, core/plan.py:178)."""
     conv = convert_reference_dag(dag)
-    executor.execute_dag(conv.dag, callbacks=callbacks, array_names=array_names, resume=resume,
-                         spec=spec, **kwargs)
-    write_back(conv, array_names)
+    _mark_zarr_complete(executor, conv, resume)
+    try:
+        executor.execute_dag(conv.dag, callbacks=callbacks, array_names=array_names, resume=resume,
+                             spec=spec, **kwargs)
+        write_back(conv, array_names)
+    finally:
+        for d in conv.targets.values():
+            d.zarr_complete = False
+            if d.allocated:
+                d.release()
     return conv
+
+
+def _mark_zarr_complete(executor, conv: ConvertedDag, resume):
+    """resume: flag the arrays whose Zarr sink is complete on disk (the
+    pipeline walk skips their ops), and upload those an op still to run
+    reads."""
+    from ..zarr_io import ZarrV2Array, upload_zarr, zarr_complete
+    from .pipeline import already_computed
+
+    for name, d in conv.targets.items():
+        t = conv.sinks.get(name)
+        d.zarr_complete = bool(resume) and t is not None and not d.written and zarr_complete(_store_path(t))
+    if not resume:
+        return
+    dag = conv.dag
+    nodes = dict(dag.nodes(data=True))
+    for n, nd in nodes.items():
+        if "pipeline" not in nd or already_computed(n, dag, nodes, resume=True):
+            continue
+        for a in dag.predecessors(n):
+            d = nodes[a].get("target")
+            if isinstance(d, DeviceArray) and getattr(d, "zarr_complete", False) and not d.written:
+                executor.allocate(d)
+                upload_zarr(ZarrV2Array.open(_store_path(conv.sinks[a])), d)
+                d.written = True
 
 
 def write_back(conv: ConvertedDag, array_names):
     """The requested arrays, device -> their reference Zarr stores (created
-    here with the LazyZarrArray's shape, dtype, chunks and fill value)."""
+    here with the LazyZarrArray's shape, dtype, chunks and fill value);
+    arrays found complete on disk by a resume are not rewritten."""
     from ..zarr_io import ZarrV2Array, write_device_array
 
     for name in array_names or ():
         t = conv.sinks.get(name)
         d = conv.targets.get(name)
-        if t is None or d is None:
+        if t is None or d is None or getattr(d, "zarr_complete", False):
             continue
         dst = ZarrV2Array.create(_store_path(t), d.shape, d.dtype, d.chunks,
                                  fill_value=getattr(t, "fill_value", None), mode="a")

@@ -172,6 +172,15 @@ class ZarrV2Array:
     def chunk_path(self, coords) -> str:
         return os.path.join(self.path, *self.chunk_key(coords).split("/"))
 
+    @property
+    def nchunks_initialized(self) -> int:
+        """Chunks present in the store (zarr.Array.nchunks_initialized: the
+        resume check of cubed/runtime/pipeline.py:25-33)."""
+        if not self.shape:
+            return int(os.path.exists(self.chunk_path(())))
+        return sum(1 for c in itertools.product(*[range(n) for n in self.numblocks])
+                   if os.path.exists(self.chunk_path(c)))
+
     def edge_extent(self, coords):
         return tuple(min(c, s - b * c) for s, c, b in zip(self.shape, self.chunks, coords))
 
@@ -507,6 +516,14 @@ def _store_arrays(sources, targets, executor, **kwargs):
     if len(sources) != len(targets):
         raise ValueError(f"Different number of sources ({len(sources)}) and targets ({len(targets)})")
     targets = [open_array(t, mode="r+") if not isinstance(t, ZarrV2Array) else t for t in targets]
+    if kwargs.get("resume"):
+        # resume: a sink whose chunks are all in its store is already computed
+        # (cubed/runtime/pipeline.py:25-33 skips the store op writing it);
+        # only the sources of incomplete sinks are computed
+        keep = [(s, t) for s, t in zip(sources, targets) if not zarr_complete(t)]
+        if not keep:
+            return
+        sources, targets = [s for s, _ in keep], [t for _, t in keep]
     arrays = []
     for s, t in zip(sources, targets):
         if tuple(s.shape) != tuple(t.shape):
@@ -521,6 +538,16 @@ def _store_arrays(sources, targets, executor, **kwargs):
     compute(*arrays, executor=executor, _return_in_memory_array=False, **kwargs)
     for a, t in zip(arrays, targets):
         write_device_array(a.zarray_maybe_lazy, t)
+
+
+def zarr_complete(t) -> bool:
+    """Every chunk of the Zarr array ``t`` (a ZarrV2Array or a path) is in
+    its store; a 0-d array never counts as complete (as in the reference)."""
+    try:
+        z = t if isinstance(t, ZarrV2Array) else ZarrV2Array.open(t)
+    except (FileNotFoundError, ValueError, NotImplementedError):
+        return False
+    return z.ndim > 0 and z.nchunks_initialized == z.nchunks
 
 
 def _identity(x):
@@ -538,8 +565,18 @@ def to_zarr(x, store, executor=None, **kwargs):
     (core/ops.py:155-182)."""
     rank, world = _rank_world()
     if rank == 0:
-        target = open_array(store, mode="w-", shape=x.shape, dtype=x.dtype,
-                            chunks=x.chunksize if x.ndim else ())
+        # mode "a", as the reference's create-arrays step opens its lazy target
+        # (core/plan.py:430-432): an existing array is reopened (so a resumed
+        # to_zarr finds its chunks), otherwise created
+        chunks = x.chunksize if x.ndim else ()
+        if os.path.exists(os.path.join(str(store), ".zarray")):
+            target = open_array(store, mode="r+")
+            if tuple(target.shape) != tuple(x.shape) or target.dtype != np.dtype(x.dtype) or \
+                    tuple(target.chunks) != tuple(chunks):
+                raise ValueError(f"Zarr array at {store!r} has shape {target.shape}, dtype {target.dtype}, "
+                                 f"chunks {target.chunks}; to_zarr writes {x.shape} {x.dtype} {chunks}")
+        else:
+            target = open_array(store, mode="w-", shape=x.shape, dtype=x.dtype, chunks=chunks)
     if world > 1:
         import torch.distributed as dist
 

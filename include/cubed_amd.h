@@ -45,12 +45,12 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 11
+#define CUBED_ABI_VERSION 12
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
-#define CUBED_MAX_FIELDS 2 /* reduced fields (e.g. mean's n and total)      */
-#define CUBED_MAX_OUTS 2   /* output arrays written per task                */
+#define CUBED_MAX_FIELDS 3 /* reduced fields (mean: n, total; var: n, mu, M2) */
+#define CUBED_MAX_OUTS 3   /* output arrays written per task (var: n, mu, M2) */
 #define CUBED_MAX_INSNS 48 /* VM instructions in the prologue program       */
 #define CUBED_MAX_EPI 16   /* VM instructions in the epilogue program       */
 #define CUBED_MAX_CONSTS 16
@@ -96,12 +96,20 @@ enum cubed_leaf_kind {
  * (its partner, PAIR_INDEX / PAIR_IMAG): argmax/argmin reduce {value, index}
  * pairs (core/ops.py:1093-1153 _arg_func/_arg_combine), cprod the {re, im}
  * parts of a complex product (np.prod of complex chunks).  A program holding
- * a pair has exactly these two fields. */
+ * a pair has exactly these two fields.
+ * var triples couple field 0 (n, int64: VAR or VARC) with field 1 (mu,
+ * VAR_MEAN) and field 2 (M2, VAR_M2), f64: the count, mean and sum of
+ * squared deviations of Chan, Golub & LeVeque's pairwise update.  VAR folds
+ * element VALUES (field 0's source) by Welford's update; VARC folds partial
+ * {n, mu, M2} triples (the three fields' sources) -- the combine rounds of
+ * var's reduction; accumulators always combine by Chan's update.  A program
+ * holding a triple has exactly these three fields. */
 enum cubed_rop {
   CUBED_R_NONE = 0, CUBED_R_SUM, CUBED_R_NANSUM, CUBED_R_COUNT,
   CUBED_R_COUNT_NONNAN, CUBED_R_MAX, CUBED_R_MIN, CUBED_R_PROD,
   CUBED_R_NANMAX, CUBED_R_NANMIN, CUBED_R_ANY, CUBED_R_ALL, CUBED_R_NANPROD,
-  CUBED_R_ARGMAX, CUBED_R_ARGMIN, CUBED_R_CPROD, CUBED_R_PAIR_INDEX, CUBED_R_PAIR_IMAG
+  CUBED_R_ARGMAX, CUBED_R_ARGMIN, CUBED_R_CPROD, CUBED_R_PAIR_INDEX, CUBED_R_PAIR_IMAG,
+  CUBED_R_VAR, CUBED_R_VARC, CUBED_R_VAR_MEAN, CUBED_R_VAR_M2
 };
 
 /* VM opcodes (two-address: r[a] = op(r[a], r[b]); where: r[a] = r[c] ? r[a] : r[b]) */
@@ -170,10 +178,11 @@ typedef struct {
   uint8_t field_rop[CUBED_MAX_FIELDS];
   uint8_t field_acc[CUBED_MAX_FIELDS]; /* 0 = f64 accumulator, 1 = i64     */
   uint8_t field_src[CUBED_MAX_FIELDS]; /* register holding the field value  */
-  uint8_t pad0[2];
+  uint8_t pad0[3];
   int32_t nouts;
   uint8_t out_dtype[CUBED_MAX_OUTS];
   uint8_t out_src[CUBED_MAX_OUTS]; /* register (or field when no epilogue)  */
+  uint8_t pad1[2];
   int32_t ninsns;
   int32_t nepi;                  /* -1 = store fields directly              */
   cubed_insn_t insns[CUBED_MAX_INSNS];

@@ -245,3 +245,30 @@ def test_inverse_trigonometric_hyperbolic_and_logs(ex, dtype):
             exp = getattr(np, npname)(Z)
             close(got, exp, dtype, ulps=256 if name in ("atan", "atanh") else 64,
                   scale=np.maximum(np.abs(exp), 1.0))
+
+
+@pytest.mark.parametrize("dtype", ["complex64", "complex128"])
+def test_integer_powers_bit_exact(ex, dtype):
+    """npy_cpow multiplies out a constant integral exponent
+    (|n| < 100): z**2 == z*z exactly, (1j)**2 == -1 + 0j with a ZERO
+    imaginary part, (-2)**2 == 4 + 0j, z**-3 == 1 / z**3 (Smith's division),
+    0**n == 0 (n > 0) / nan (n < 0).  The executor takes the same branch,
+    so the results are bit-identical to numpy, signed zeros included."""
+    Z = cdata((5, 8), dtype, 13, specials=False)
+    f = Z.reshape(-1)
+    f[0], f[1], f[2], f[3], f[4] = 1j, -2, 0, complex(-0.0, 1.5), complex(3.0, -0.0)
+    spec = mkspec(ex)
+    z = cubed.from_array(Z, chunks=(3, 4), spec=spec)
+    pw = np.dtype(dtype).type
+    for n in (1, 2, 3, 5, 7, -1, -2, -3, 10, 99, 0):
+        with np.errstate(all="ignore"):
+            exp = np.power(Z, pw(n))
+        got = (z ** n).compute()
+        assert got.dtype == exp.dtype
+        for part in ("real", "imag"):
+            g, e = getattr(got, part), getattr(exp, part)
+            both_nan = np.isnan(g) & np.isnan(e)
+            bits = g.view(np.uint32 if dtype == "complex64" else np.uint64) == \
+                e.view(np.uint32 if dtype == "complex64" else np.uint64)
+            assert (bits | both_nan).all(), (n, part, g[~(bits | both_nan)][:4], e[~(bits | both_nan)][:4])
+    assert (z ** 2).compute().reshape(-1)[0].imag == 0.0

@@ -72,6 +72,13 @@ def _cases(rank, world, zdir):
     out["sum1"] = xp.sum(b, axis=1).compute()
     note("sum1")
 
+    # var / std: {n, mu, M2} triples are not an RCCL sum -- all-gathered and
+    # folded in rank order with Chan's update
+    out["var0"] = xp.var(b, axis=0).compute()
+    out["std_all"] = xp.std(b, correction=1.0).compute()
+    out["var_rechunk"] = xp.var(b.rechunk((33, 100)), axis=0).compute()
+    note("var")
+
     # rechunk: rows -> columns, and misaligned
     y = np.random.default_rng(9).random((60, 50)).astype(np.float32)
     c = cubed.from_array(y, chunks=(10, 50), spec=spec)
@@ -155,6 +162,9 @@ def test_distributed_executor_matches_oracle(world, tmp_path):
     assert np.array_equal(got["max0"], x.max(axis=0))
     assert got["min_all"] == x.min()
     assert np.allclose(got["sum1"], x.sum(axis=1), rtol=1e-12, atol=0)
+    assert np.allclose(got["var0"], x.var(axis=0), rtol=1e-12, atol=0)
+    assert np.isclose(got["std_all"], x.std(ddof=1), rtol=1e-12, atol=0)
+    assert np.allclose(got["var_rechunk"], x.var(axis=0), rtol=1e-12, atol=0)
 
     y = np.random.default_rng(9).random((60, 50)).astype(np.float32)
     assert np.array_equal(got["rechunk_cols"], y)

@@ -626,6 +626,51 @@ def test_task_end_events_and_resume(ex):
     assert c2.value == 0 or c2.value < c.value
 
 
+class TaskCounter(cubed.Callback):
+    """cubed/tests/utils.py TaskCounter: sums TaskEndEvent.num_tasks."""
+
+    def __init__(self):
+        self.value = 0
+
+    def on_task_end(self, event):
+        self.value += event.num_tasks
+
+
+def test_callbacks_exact_counts(ex):
+    """cubed/tests/test_executor_features.py:51-63 (test_callbacks): an
+    add of two 3x3 arrays in 2x2 chunks is 4 tasks plus one created array."""
+    spec = mkspec(ex, mem=100000, reserved=0)
+    a = xp.asarray([[1, 2, 3], [4, 5, 6], [7, 8, 9]], chunks=(2, 2), spec=spec)
+    b = xp.asarray([[1, 1, 1], [1, 1, 1], [1, 1, 1]], chunks=(2, 2), spec=spec)
+    c = xp.add(a, b)
+    tc = TaskCounter()
+    assert np.array_equal(c.compute(callbacks=[tc]), np.array([[2, 3, 4], [5, 6, 7], [8, 9, 10]]))
+    num_created_arrays = 1
+    assert tc.value == num_created_arrays + 4
+
+
+def test_resume_exact_counts(ex):
+    """cubed/tests/test_executor_features.py:121-150 (test_resume), restated
+    with its exact task counts: c computed, then d = -c with resume runs only
+    d's 4 tasks (the create-arrays task runs again, for both arrays)."""
+    spec = mkspec(ex, mem=100000, reserved=0)
+    a = xp.asarray([[1, 2, 3], [4, 5, 6], [7, 8, 9]], chunks=(2, 2), spec=spec)
+    b = xp.asarray([[1, 1, 1], [1, 1, 1], [1, 1, 1]], chunks=(2, 2), spec=spec)
+    c = xp.add(a, b)
+    d = xp.negative(c)
+    num_created_arrays = 2  # c, d
+    assert d.plan.num_tasks(optimize_graph=False) == num_created_arrays + 8
+    tc = TaskCounter()
+    c.compute(callbacks=[tc], optimize_graph=False)
+    num_created_arrays = 1  # c
+    assert tc.value == num_created_arrays + 4
+    tc = TaskCounter()
+    got = d.compute(callbacks=[tc], optimize_graph=False, resume=True)
+    num_created_arrays = 2  # c, d
+    assert tc.value == num_created_arrays + 4
+    assert np.array_equal(got, -np.array([[2, 3, 4], [5, 6, 7], [8, 9, 10]]))
+
+
 # ----------------------------------------------------- full-size properties
 
 

@@ -1,0 +1,83 @@
+"""Rank rehearsal on one GPU (``-m gpu``): every rank of an 8-rank job run in
+ONE process through ``runtime.comm.LoopbackComm`` -- each rank allocates
+only its block-cyclic share, lowers its own pieces (DistPiecesLaunch) and
+launches them for real; its collectives are local copies, and the reduce
+inputs it would hand to RCCL are recorded.  Folding the 8 recorded partials
+in rank order (the RCCL sum) and running the aggregate must give the
+single-GPU result: the rehearsed launch list is the one the 8-GPU bench runs
+(bench.py ``rechunk_mean_rehearsal``), so its timing rests on a correct path.
+
+Reference: the reduction rounds this distributes, cubed/core/ops.py:849-892;
+mean's combine/aggregate, cubed/array_api/statistical_functions.py:61-100.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _plan(ex, shape, chunks, cols):
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+    random.seed(2000)
+    x = xp.astype(crandom.random(shape, chunks=chunks, spec=spec), xp.float32)
+    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+    m = xp.mean(x.rechunk((shape[0], cols)), axis=0)
+    return x, m
+
+
+@pytest.mark.parametrize("shape,cols", [((4000, 3000), 100),    # uniform groups: merged kept runs
+                                        ((4050, 3050), 100)])   # ragged edge chunks: combine_groups
+def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols):
+    import torch
+
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.comm import LoopbackComm
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+    from cubed_amd.runtime.executors.dist import DistPiecesLaunch
+
+    chunks = (100, shape[1])
+    x1, m1 = _plan(gpu_executor, shape, chunks, cols)
+    want = m1.compute(resume=True)
+    host = x1.compute(resume=True).astype(np.float64)
+    np.testing.assert_allclose(want, host.mean(axis=0).astype(np.float32), rtol=1e-6)
+
+    world = 8
+    totals, counts = [], []
+    direct = []
+    for r in range(world):
+        comm = LoopbackComm(r, world, record=True)
+        ex = GpuDagExecutor("cuda:0", comm=comm)
+        x, m = _plan(ex, shape, chunks, cols)
+        assert x.zarray.world == world and x.zarray.rank == r
+        arrays_to_plan(m).execute(executor=ex, array_names=[m.name], resume=True)
+        torch.cuda.synchronize()
+        launches = [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistPiecesLaunch)]
+        assert len(launches) == 1
+        direct.append(launches[0].soa_direct)
+        recs = [t for kind, t in comm.records if kind == "all_reduce_sum"]
+        tot = [t for t in recs if t.dtype == torch.float64]
+        cnt = [t for t in recs if t.dtype == torch.int64]
+        assert len(tot) == 1 and len(cnt) == 1
+        totals.append(tot[0].cpu().numpy())
+        counts.append(cnt[0].cpu().numpy())
+        del x, m, ex
+    # uniform groups stream as merged kept runs (no combine_groups pass)
+    assert all(direct) == (shape[0] % chunks[0] == 0 and shape[1] % cols == 0)
+    total = totals[0].copy()
+    count = counts[0].copy()
+    for r in range(1, world):  # the RCCL sum, in rank order
+        total += totals[r]
+        count += counts[r]
+    ngroups = -(-shape[1] // cols)
+    assert count.shape == (ngroups,)
+    assert np.all(count == shape[0])
+    got = (total.reshape(ngroups, cols) / count[:, None]).reshape(-1)[:shape[1]].astype(np.float32)
+    np.testing.assert_allclose(got, want, rtol=1e-6)

@@ -107,3 +107,69 @@ def test_reference_quad_means_shape(tmp_path, spec):
     exp = R.mean(U * V, chunks, 0, allowed_mem=2_000_000_000, reserved_mem=100_000_000)
     assert np.allclose(res0, exp, rtol=1e-12, atol=0)
     assert np.allclose(res1, exp, rtol=1e-12, atol=0)
+
+
+_RESUME_SCRIPT = r"""
+import json, random, sys
+sys.path.insert(0, {root!r})
+import numpy as np
+import torch
+torch.cuda.set_device(0)
+import cubed_amd as cubed
+import cubed_amd.random as crandom
+from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+
+class Count(cubed.Callback):
+    def __init__(self):
+        self.value = 0
+
+    def on_task_end(self, event):
+        self.value += event.num_tasks
+
+
+ex = GpuDagExecutor("cuda:0")
+spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+random.seed(31)
+x = crandom.random((60, 40), chunks=(20, 10), spec=spec)
+cnt = Count()
+cubed.to_zarr((x + 1) * 2, {path!r}, callbacks=[cnt], resume={resume})
+print(json.dumps({{"tasks": cnt.value, "ran": ex.last_schedule is not None}}), flush=True)
+"""
+
+
+def _run_resume_proc(tmp_path, path, resume):
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _RESUME_SCRIPT.format(root=root, path=path, resume=resume)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240,
+                         cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_resume_at_complete_zarr_sink_in_a_new_process(tmp_path):
+    """cubed/runtime/pipeline.py:25-33: with resume, an op whose Zarr target
+    holds every chunk is already computed, whichever process wrote it.  A
+    first process writes (x + 1) * 2 with to_zarr; a second builds the same
+    plan and calls to_zarr(..., resume=True): nothing is launched and the
+    store is unchanged.  Removing one chunk file makes the next resume
+    compute again."""
+    import os
+
+    path = str(tmp_path / "r.zarr")
+    first = _run_resume_proc(tmp_path, path, False)
+    assert first["ran"] and first["tasks"] > 0
+    before = Z.open_array(path)[...]
+    second = _run_resume_proc(tmp_path, path, True)
+    assert second == {"tasks": 0, "ran": False}
+    assert np.array_equal(Z.open_array(path)[...], before)
+    os.remove(Z.open_array(path).chunk_path((1, 2)))
+    assert Z.open_array(path).nchunks_initialized == Z.open_array(path).nchunks - 1
+    third = _run_resume_proc(tmp_path, path, True)
+    assert third["ran"] and third["tasks"] > 0
+    assert np.array_equal(Z.open_array(path)[...], before)

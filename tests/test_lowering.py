@@ -6,6 +6,7 @@ performance: how many launches a pipeline becomes, whether the streaming
 fast path is taken, and that reduction chains are fused into one pass.
 """
 
+import ctypes
 import math
 import random
 
@@ -685,3 +686,39 @@ def test_complex_prod_is_one_pair_reduction(built, dry):
     assert P.nfields == 2
     assert (P.field_rop[0], P.field_rop[1]) == (ir.ROPS["cprod"], ir.ROPS["pair_imag"])
     assert P.field_acc[0] == P.field_acc[1] == 0
+
+
+def test_var_is_one_fused_triple_pass(built, dry):
+    """var(axis=0) over merge rounds: the per-chunk {n, mu, M2} program and
+    every varc combine round compose into ONE streaming pass of the var
+    triple (fields n / mu / M2 with the var / var_mean / var_m2 ops), the
+    aggregate M2 / max(n - correction, 0) in its epilogue."""
+    spec = cubed.Spec(allowed_mem=120_000, reserved_mem=0, executor=dry)
+    a = cubed.from_array(np.zeros((400, 64)), chunks=(5, 64), spec=spec)
+    arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+    dry.launched.clear()
+    v = xp.var(a, axis=0, correction=1.0)
+    plan = arrays_to_plan(v)
+    nops = sum(1 for _, d in plan._finalize_dag().nodes(data=True) if d.get("op_name") == "blockwise")
+    assert nops >= 3  # per-chunk + combine rounds + aggregate
+    plan.execute(executor=dry, resume=True, array_names=[v.name])
+    fused = _fused(dry)
+    assert len(dry.launched) == 1 and len(fused) == 1
+    P = fused[0].prog
+    assert P.mode & MODE_STREAM
+    assert P.nfields == 3
+    assert [P.field_rop[i] for i in range(3)] == [ir.ROPS["var"], ir.ROPS["var_mean"], ir.ROPS["var_m2"]]
+    assert [P.field_acc[i] for i in range(3)] == [1, 0, 0]
+    assert P.nepi > 0
+
+
+def test_var_triple_rejected_when_malformed(built):
+    """The library's program check refuses a var lead without its partners."""
+    P = nat.Program()
+    P.vtype, P.ndim, P.nred, P.mode, P.nleaves, P.nfields, P.nouts = 1, 2, 1, 4, 1, 2, 1
+    P.field_rop[0], P.field_acc[0] = ir.ROPS["var"], 1
+    P.field_rop[1] = ir.ROPS["var_mean"]
+    P.nepi = -1
+    h = ctypes.c_void_p()
+    rc = nat.lib().cubed_fused_compile(ctypes.byref(P), nat.INCLUDE_DIRS.encode(), ctypes.byref(h))
+    assert rc != 0 and b"triple" in nat.lib().cubed_last_error()
