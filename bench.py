@@ -568,7 +568,56 @@ def config1_extra(args, ex, rank, world):
         r["check"] = check_close(m.compute(resume=True), acc / A.shape[0], 1e-12,
                                  "oracle: f64 column sums of (a+1)*2 over the resident 20000^2 input")
         CHECKS.append(("config1", r["check"]))
+        if rank == 0 and not args.no_cpu_baseline:
+            r["cpu_baseline"] = cpu_config1_baseline(a, acc / A.shape[0])
     return r
+
+
+def cpu_config1_baseline(a, gpu_exp, row_blocks=2):
+    """BASELINE config 1 as the reference runs it: the sequential
+    PythonDagExecutor over the finalized plan (add; multiply + _mean_func;
+    merge + combine + aggregate) with every intermediate in a LOCAL ZARR
+    WORK_DIR (this repo's Zarr v2 writer/reader, blosc-lz4 with byte shuffle:
+    numcodecs' default compressor).  ``a`` (the random op's output) is first
+    written to the work_dir from HBM (untimed, as its generation is untimed
+    on the GPU); the timed sample is the first ``row_blocks`` row bands of
+    chunks (all four column chunks), bounded to ~10-30 s."""
+    import shutil
+    import tempfile
+
+    from oracle import cubed_ref as R
+    from cubed_amd.zarr_io import ZarrV2Array, write_device_array
+
+    A = a.zarray
+    work = tempfile.mkdtemp(prefix="cubed_cpu_work_")
+    try:
+        src = ZarrV2Array.create(os.path.join(work, "a"), A.shape, A.dtype, A.chunks)
+        write_device_array(A, src)
+        t0 = time.perf_counter()
+        got = R.config1_python_zarr(src, work, row_blocks=row_blocks)
+        dt = time.perf_counter() - t0
+        # the sample's mean over its rows, checked against the resident input
+        rows = row_blocks * A.chunks[0]
+        import itertools
+
+        acc = np.zeros(A.shape[1], dtype=np.float64)
+        for i, j in itertools.product(range(row_blocks), range(A.numblocks[1])):
+            c0 = A.chunk_start((i, j))[1]
+            blk = A.read_chunk((i, j))
+            acc[c0:c0 + blk.shape[1]] += np.sum((blk + 1) * 2, axis=0, dtype=np.float64)
+        ok = bool(np.allclose(got, acc / rows, rtol=1e-12, atol=0))
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    nbytes = rows * A.shape[1] * A.dtype.itemsize
+    return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"{row_blocks} of {A.numblocks[0]} row bands of config 1 ({rows}x{A.shape[1]} f64, "
+                      f"{row_blocks * A.numblocks[1]} chunk tasks per op): oracle restatement of the "
+                      f"sequential PythonDagExecutor over the reference's finalized plan (add; multiply + "
+                      f"_mean_func; merge + combine + aggregate), every intermediate written to and read "
+                      f"from a local Zarr v2 work_dir (blosc-lz4 + byte shuffle, this repo's host codec, "
+                      f"{{n, total}} partials as two arrays); input a already in the work_dir (untimed); "
+                      f"one timed pass; {_cpu_info(1)}",
+            "seconds": round(dt, 3), "values_match": ok}
 
 
 def vorticity_extra(args, ex, rank, world, T=1000):
@@ -617,7 +666,56 @@ def vorticity_extra(args, ex, rank, world, T=1000):
         r["check"] = check_close(m.compute(resume=True), exp, 1e-12,
                                  "oracle: chunked f64 sum over the resident (1000,900,800) inputs")
         CHECKS.append(("vorticity", r["check"]))
+        if rank == 0 and not args.no_cpu_baseline:
+            r["cpu_baseline"] = cpu_vorticity_baseline(A, B, X, Y)
     return r
+
+
+def cpu_vorticity_baseline(A, B, X, Y, t_blocks=2):
+    """BASELINE config 4 on the reference's finalized plan (map_direct a[1:],
+    b[1:]; multiply by x, y; add + _mean_func; combine + aggregate) restated
+    chunk by chunk with in-memory intermediates (no Zarr: optimistic), the
+    sequential and the threaded executor; sample = the first ``t_blocks``
+    time blocks of a[1:] (all 72 spatial chunks each)."""
+    import itertools
+
+    from threadpoolctl import threadpool_limits
+
+    from oracle import cubed_ref as R
+
+    c = A.chunks[0]
+    nrows = min(A.shape[0], (t_blocks + 1) * c)
+
+    def host(Z, rows):
+        out = np.empty((rows,) + tuple(Z.shape[1:]), dtype=Z.dtype)
+        for key in itertools.product(*[range(n) for n in Z.numblocks]):
+            st = Z.chunk_start(key)
+            if st[0] >= rows:
+                continue
+            blk = Z.read_chunk(key)
+            out[tuple(slice(s, s + e) for s, e in zip(st, blk.shape))] = blk[:rows - st[0]]
+        return out
+
+    a, b = host(A, nrows), host(B, nrows)
+    x, y = X.to_numpy(), Y.to_numpy()
+    threads = min(32, (os.cpu_count() or 1) + 4)
+    res = {}
+    with threadpool_limits(1):
+        for name, th in (("sequential", 1), ("threads", threads)):
+            R.vorticity_python(a, b, x, y, c, t_blocks=1, threads=th)  # warm-up
+            t0 = time.perf_counter()
+            got = R.vorticity_python(a, b, x, y, c, t_blocks=t_blocks, threads=th)
+            res[name] = time.perf_counter() - t0
+    exp = float(np.mean(a[1:1 + t_blocks * c] * x + b[1:1 + t_blocks * c] * y, dtype=np.float64))
+    nbytes = 2 * t_blocks * c * x.size * 8 + 2 * x.size * 8
+    return {"value": round(nbytes / res["threads"] / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{t_blocks} of {-(-(A.shape[0] - 1) // c)} time blocks of a[1:], b[1:] "
+                      f"({t_blocks * 72} chunk tasks per op): oracle restatement of the reference's finalized "
+                      f"plan (index a[1:], b[1:]; * x, * y; add + _mean_func; combine + aggregate) on the "
+                      f"threaded executor, in-memory intermediates (no Zarr/Blosc: optimistic), one timed "
+                      f"pass after a warm-up; {_cpu_info(threads)}",
+            "sequential": {"value": round(nbytes / res["sequential"] / 1e9, 3), "cores": 1},
+            "values_match": bool(abs(got - exp) <= 1e-12 * abs(exp))}
 
 
 def matmul_extra(args, ex, rank, world, dt_name):

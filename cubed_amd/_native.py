@@ -122,6 +122,8 @@ def lib():
     L.cubed_fused_chunks.restype = c_int
     L.cubed_fused_workspace_bytes.argtypes = [POINTER(Program), c_int64, c_int64, c_int64]
     L.cubed_fused_workspace_bytes.restype = c_int64
+    L.cubed_stream_split_target.argtypes = [c_int64]
+    L.cubed_stream_split_target.restype = c_int64
     L.cubed_random_chunks.argtypes = [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]
     L.cubed_random_chunks.restype = c_int
     L.cubed_copy_boxes.argtypes = [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32,
@@ -186,7 +188,7 @@ def check(rc: int, what: str):
 
 
 EXPORTED_SYMBOLS = (
-    "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_random_chunks",
+    "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_stream_split_target", "cubed_random_chunks",
     "cubed_copy_boxes", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",

@@ -74,17 +74,27 @@ def _const(v, dt):
     return ir.Const(np.array(v, dtype=dt).item(), np.dtype(dt))
 
 
-def _const_value(e):
-    """The value of a constant expression (a Const, possibly cast), else None."""
+def _const_value(e, const_args):
+    """The value of a constant expression (a Const, or an argument reading a
+    constant, possibly cast), else None."""
     while isinstance(e, ir.Cast):
         e = e.x
-    return e.value if isinstance(e, ir.Const) else None
+    if isinstance(e, ir.Const):
+        return e.value
+    if isinstance(e, ir.Arg) and e.index in const_args:
+        v = const_args[e.index]
+        if e.field == "real":
+            return np.real(v)
+        if e.field == "imag":
+            return np.imag(v)
+        return None if e.field is not None else v
+    return None
 
 
-def _integral_exponent(br, bi):
+def _integral_exponent(br, bi, const_args):
     """n when the exponent is the constant n + 0i with n integral and
     |n| < 100 (npy_cpow's ``(n = (npy_intp)br) == br`` test), else None."""
-    r, i = _const_value(br), _const_value(bi)
+    r, i = _const_value(br, const_args), _const_value(bi, const_args)
     if r is None or i is None:
         return None
     try:
@@ -391,7 +401,7 @@ class _Splitter:
         # z ** w = exp(w log z) (npy_cpow's general branch); w = 0 -> 1 + 0i,
         # z = 0 with real w > 0 -> 0 + 0i.  A constant integral w with |w| <
         # 100 takes numpy's multiplied-out branch (_ipow)
-        n = _integral_exponent(br, bi)
+        n = _integral_exponent(br, bi, getattr(self, "const_args", {}))
         if n is not None:
             return self._ipow(ar, ai, n, p)
         lr = _un("log", _bin("hypot", ar, ai, p), p)
@@ -502,12 +512,16 @@ def program_has_complex(p) -> bool:
     return p.reduce is not None and any(is_complex(f.dtype) for f in p.reduce.fields)
 
 
-def split_program(p: ir.ExprProgram) -> ir.ExprProgram:
+def split_program(p: ir.ExprProgram, const_args=None) -> ir.ExprProgram:
     """The program over real expressions that computes ``p``'s complex values
-    part by part (unchanged when ``p`` has no complex value)."""
+    part by part (unchanged when ``p`` has no complex value).
+    ``const_args``: {argument index: value} of arguments that read a
+    constant (a promoted scalar), so numpy's constant-exponent branches of
+    ``pow`` can be taken."""
     if not program_has_complex(p):
         return p
     s = _Splitter()
+    s.const_args = dict(const_args or {})
     reduce = p.reduce
     if reduce is not None:
         fields = []

@@ -168,7 +168,7 @@ int stream_groups(const cubed_program_t& P) {
 // split, profiles/r02_stream_ab.log); smaller grids split toward
 // 1024 workgroups (~4 per CU: config 1's stream 0.503 ms vs 0.542 at 2048,
 // 0.59-0.62 at 4096-8192, 1.10 at 256).
-static constexpr int64_t kStreamTarget = 1024;
+static int64_t g_stream_target = 1024;  // cubed_stream_split_target() (probes)
 
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red, int stream_w) {
@@ -193,7 +193,7 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     const int isz = P->vtype == CUBED_V_F32 ? 4 : 8;
     const int64_t inflight = (int64_t)kBlock * stream_unroll(isz, P->nleaves) * P->nleaves * W * 4 * isz;
     if (P->nfields > 0 && base * inflight < (int64_t)256 * 96 * 1024 && max_red >= 64)
-      L.nsplit = (int32_t)choose_split(base, max_red / 16, kStreamTarget);
+      L.nsplit = (int32_t)choose_split(base, max_red / 16, g_stream_target);
     // a multiple of 8 workgroups (the surplus exits at once): stream_body
     // maps them to XCD-contiguous runs
     L.blocks = (ntasks * L.nsplit * L.bpt + 7) / 8 * 8;
@@ -289,6 +289,10 @@ int check_program(const cubed_program_t& P) {
       ((P.mode & 3) != 0 || !(P.mode & 4) || P.nred > 2 || P.ndim != P.nred + 1 || P.nleaves < 1)) {
     set_err("cubed_fused_chunks: stream mode needs kernel A, VEC=4, one kept dim and <= 2 reduced dims");
     return CUBED_E_LAYOUT;
+  }
+  if ((P.mode & CUBED_MODE_HOST_COUNT) && !(P.mode & CUBED_MODE_PARTIALS)) {
+    set_err("cubed_fused_chunks: host-provided counts need partials mode");
+    return CUBED_E_ARG;
   }
   if ((P.mode & (CUBED_MODE_STREAM_W2 | CUBED_MODE_STREAM_W4)) &&
       (!(P.mode & CUBED_MODE_STREAM) || (P.mode & CUBED_MODE_STREAM_W2 && P.mode & CUBED_MODE_STREAM_W4))) {
@@ -475,6 +479,12 @@ extern "C" int cubed_combine_partials(const cubed_program_t* prog, const cubed_p
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   return 0;
+}
+
+extern "C" int64_t cubed_stream_split_target(int64_t workgroups) {
+  const int64_t prev = g_stream_target;
+  if (workgroups > 0) g_stream_target = workgroups;
+  return prev;
 }
 
 extern "C" const char* cubed_last_error(void) { return g_err; }

@@ -414,7 +414,8 @@ CUBED_DEV void collect_body(
   Acc x[CUBED_MAX_FIELDS];
   if (k < nk) fold_splits_of(P, ws, nsplit, ntasks, t, max_kept, k, x);
   for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f)
-    soa[f * n + i] = k < nk ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
+    if (!(P.mode & CUBED_MODE_HOST_COUNT) || P.field_rop[f] != CUBED_R_COUNT)
+      soa[f * n + i] = k < nk ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
 }
 
 // Epilogue + store from combined SoA partials (the last step of a reduction
@@ -964,7 +965,8 @@ CUBED_DEV void stream_body(
     if (el >= max_kept) return;
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-      if (f < nf) soa[f * nsoa + t * max_kept + el] = valid ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
+      if (f < nf && (!(P.mode & CUBED_MODE_HOST_COUNT) || P.field_rop[f] != CUBED_R_COUNT))
+        soa[f * nsoa + t * max_kept + el] = valid ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
   };
   // (block-uniform trip count: the arrival handshake below has barriers)
   for (int64_t bb = b * kBlock; bb < wslots; bb += bpt * kBlock) {
@@ -1010,13 +1012,18 @@ CUBED_DEV void stream_body(
             if (f < nf && P.field_rop[f] != CUBED_R_COUNT) store_through(&w[el * nf + f], acc[j][f][e]);
         }
       }
-      // Handshake without L2 maintenance: the accumulators above are
-      // write-through stores (agent scope) -- the 8 XCDs' L2s are not
+      // Handshake without L2 maintenance (MI355X_MICROARCH.md "Correctness
+      // boundaries", the sc1 form): the accumulators above are write-through
+      // stores (agent-scope relaxed atomics: sc1) -- the 8 XCDs' L2s are not
       // coherent with each other, and an agent-scope release/acquire fence
       // would write back and invalidate this XCD's whole L2 per workgroup
-      // (measured 2x slower on the per-rank share).  Waiting for the stores
-      // to complete before the barrier orders them before the arrival count.
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      // (measured 2x slower on the per-rank share).  Every storing wave
+      // drains its stores (vmcnt(0)) before the barrier, so they are complete
+      // before one lane counts the arrival; the fold reads them with sc1
+      // loads after the second barrier.
+      // (inline asm: the builtin form was dropped by the wait-count pass,
+      // which does not order stores before a barrier)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
         uint32_t* c = cnt + t * nblk + bb / kBlock;
@@ -1028,48 +1035,59 @@ CUBED_DEV void stream_body(
       __syncthreads();
       if (!last_arrival) continue;
       // the other splits' accumulators: read past this XCD's L2 (load_through)
-      // fold splits 0..nsplit-1 in order (this workgroup's own included)
+      // fold splits 0..nsplit-1 in order (this workgroup's own included).
+      // The loads are agent-scope atomics, which keep their program order:
+      // every load of a batch (4 splits x 4 elements) is issued before the
+      // first combine, so a batch costs one memory round trip
       const int64_t sstride = nsoa * nf;
+      auto stored = [&](int f) { return f < nf && P.field_rop[f] != CUBED_R_COUNT; };
 #pragma unroll
       for (int j = 0; j < W; ++j) {
         if (!gv[j]) continue;
+        const Acc* __restrict__ pe[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t el = go[j] + (e >> 1) * dk[j] + (e & 1);
-          const Acc* __restrict__ pp = ws + ((int64_t)t * max_kept + el) * nf;
-          Acc x[CUBED_MAX_FIELDS];
+        for (int e = 0; e < 4; ++e)
+          pe[e] = ws + ((int64_t)t * max_kept + go[j] + (e >> 1) * dk[j] + (e & 1)) * nf;
+        Acc x[4][CUBED_MAX_FIELDS];
 #pragma unroll
-          for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-            if (f < nf && P.field_rop[f] != CUBED_R_COUNT) x[f] = load_through(&pp[f]);
-            else x[f] = acc_init(P.field_rop[f], P.field_acc[f]);
-          }
-          int sp = 1;
-          for (; sp + 4 <= nsplit; sp += 4) {
-            Acc v[4][CUBED_MAX_FIELDS];
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+          for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+            x[e][f] = stored(f) ? load_through(pe[e] + f) : acc_init(P.field_rop[f], P.field_acc[f]);
+        int sp = 1;
+        for (; sp + 4 <= nsplit; sp += 4) {
+          Acc v[4][4][CUBED_MAX_FIELDS];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
 #pragma unroll
               for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-                v[u][f] = (f < nf && P.field_rop[f] != CUBED_R_COUNT)
-                              ? load_through(&pp[(int64_t)(sp + u) * sstride + f])
-                              : acc_init(P.field_rop[f], P.field_acc[f]);
+                v[u][e][f] = stored(f) ? load_through(pe[e] + (int64_t)(sp + u) * sstride + f)
+                                       : acc_init(P.field_rop[f], P.field_acc[f]);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) fields_combine(x, v[u], P);
-          }
-          for (; sp < nsplit; ++sp) {
-            Acc v[CUBED_MAX_FIELDS];
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) fields_combine(x[e], v[u][e], P);
+        }
+        for (; sp < nsplit; ++sp) {
+          Acc v[4][CUBED_MAX_FIELDS];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-              v[f] = (f < nf && P.field_rop[f] != CUBED_R_COUNT) ? load_through(&pp[(int64_t)sp * sstride + f])
-                                                                   : acc_init(P.field_rop[f], P.field_acc[f]);
-            fields_combine(x, v, P);
-          }
+              v[e][f] = stored(f) ? load_through(pe[e] + (int64_t)sp * sstride + f)
+                                  : acc_init(P.field_rop[f], P.field_acc[f]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) fields_combine(x[e], v[e], P);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
           for (int f = 0; f < CUBED_MAX_FIELDS; ++f) {
-            if (f < nf && P.field_rop[f] == CUBED_R_COUNT) x[f].i = nrd;
-            acc[j][f][e] = x[f];
+            if (f < nf && P.field_rop[f] == CUBED_R_COUNT) x[e][f].i = nrd;
+            acc[j][f][e] = x[e][f];
           }
-        }
       }
     } else {
 #pragma unroll

@@ -31,16 +31,19 @@ __global__ __launch_bounds__(kBlock) void k_stream(
   stream_body<V, NL, U, 1, SPLIT>(*Pd, tasks, ntasks, bpt, nsplit, ws, max_kept);
 }
 
+// The interpreted kernels are the fallback / cross-check of the JIT ones
+// (CUBED_AMD_JIT=0): two rows in flight instead of stream_unroll()'s 2-8
+// keeps each a few copies of the interpreter instead of up to 8 (build time);
+// the accumulation order per element -- and so every result bit -- is the same.
 template <typename V, bool SPLIT>
 static void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
                             const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
-  constexpr int S = (int)sizeof(V);
   const dim3 grid = grid_of(L.blocks);
   switch (P.nleaves) {
-    case 1: hipLaunchKernelGGL((k_stream<V, 1, stream_unroll(S, 1), SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 2: hipLaunchKernelGGL((k_stream<V, 2, stream_unroll(S, 2), SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 3: hipLaunchKernelGGL((k_stream<V, 3, stream_unroll(S, 3), SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    default: hipLaunchKernelGGL((k_stream<V, 4, stream_unroll(S, 4), SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 1: hipLaunchKernelGGL((k_stream<V, 1, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 2: hipLaunchKernelGGL((k_stream<V, 2, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 3: hipLaunchKernelGGL((k_stream<V, 3, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    default: hipLaunchKernelGGL((k_stream<V, 4, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
   }
 }
 

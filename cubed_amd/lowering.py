@@ -1029,6 +1029,11 @@ class Lowerer:
             if P.nfields == 0:
                 raise LoweringError("partials mode needs a reduction")
             P.mode |= MODE_PARTIALS
+            if group_layout is not None:
+                # per-group SoA straight from the kernel (DistPiecesLaunch):
+                # its plain COUNT fields are the groups' global row counts,
+                # filled by the host once, never reduced across the ranks
+                P.mode |= MODE_HOST_COUNT
         table = layout.table(self.ctx.device)
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)
         launch = FusedLaunch(P, table, len(rows), layout.max_kept, layout.max_red, ws,
@@ -1656,6 +1661,7 @@ _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64:
 
 MODE_STREAM_W2 = 32  # include/cubed_amd.h CUBED_MODE_STREAM_W2
 MODE_STREAM_W4 = 64  # include/cubed_amd.h CUBED_MODE_STREAM_W4
+MODE_HOST_COUNT = 128  # include/cubed_amd.h CUBED_MODE_HOST_COUNT
 
 
 def _stream_unroll(itemsize: int, nleaves: int) -> int:

@@ -190,6 +190,29 @@ def compose_rechunks(dag, array_names):
     return dag, elided
 
 
+def _constant_args(spec):
+    """{argument index: value} of a blockwise spec's arguments that read a
+    constant array (a promoted scalar: VirtualFullArray, or a one-element
+    in-memory array), resolved through the key function of block 0."""
+    from .storage import VirtualFullArray, VirtualInMemoryArray
+
+    out = {}
+    try:
+        nd = spec.write.array.ndim
+        args = spec.block_function(("out",) + (0,) * nd)
+    except Exception:  # noqa: BLE001 - no resolvable block: no constants
+        return out
+    for i, a in enumerate(args):
+        if not isinstance(a, tuple) or not a or a[0] not in spec.reads_map:
+            continue
+        arr = spec.reads_map[a[0]].array
+        if isinstance(arr, VirtualFullArray):
+            out[i] = arr.fill_value
+        elif isinstance(arr, VirtualInMemoryArray) and arr.array.size == 1:
+            out[i] = arr.array.reshape(-1)[0].item()
+    return out
+
+
 def split_complex(dag):
     """Every blockwise program that computes complex values rewritten into
     real expressions over the values' real / imaginary slabs
@@ -205,7 +228,7 @@ def split_complex(dag):
     for name in todo:
         nd = dag.nodes[name]
         spec = nd["pipeline"].config
-        spec = dataclasses.replace(spec, function=split_program(spec.function))
+        spec = dataclasses.replace(spec, function=split_program(spec.function, _constant_args(spec)))
         pipeline = dataclasses.replace(nd["pipeline"], config=spec)
         nd["pipeline"] = pipeline
         nd["primitive_op"] = dataclasses.replace(nd["primitive_op"], pipeline=pipeline)

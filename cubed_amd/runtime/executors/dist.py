@@ -291,7 +291,7 @@ class DistPiecesLaunch:
     (cubed_fused_finish over one row per group)."""
 
     def __init__(self, ctx, fused, group_start, group_table, max_kept_out, rops, acc_int, owners,
-                 soa_direct=False):
+                 soa_direct=False, host_counts=None):
         import torch
 
         self.ctx = ctx
@@ -315,6 +315,16 @@ class DistPiecesLaunch:
         # group: one int64 per group crosses the ranks (as in PartialsLaunch)
         self.uniform = [r == "count" for r in rops]
         self.sum_only = all(r in SUM_ROPS for r in rops)
+        # host_counts (CUBED_MODE_HOST_COUNT, soa_direct only): the kernel leaves
+        # the COUNT fields alone; they hold each group's global count, filled
+        # here once, and never cross the ranks
+        self.host_count = [r == "count" and host_counts is not None for r in rops]
+        if host_counts is not None:
+            assert soa_direct and len(host_counts) == self.ngroups
+            hc = torch.as_tensor(np.asarray(host_counts, dtype=np.int64), device=ctx.device)
+            for f in range(self.nf):
+                if self.host_count[f]:
+                    self.field_view(f).view(self.ngroups, self.mko).copy_(hc[:, None].expand(self.ngroups, self.mko))
         self.acc_int = acc_int
         uniq = sorted(set(owners))
         self.root = uniq[0] if len(uniq) == 1 else None
@@ -340,6 +350,8 @@ class DistPiecesLaunch:
         if self.sum_only:
             mk = self.mko
             for f in range(self.nf):
+                if self.host_count[f]:
+                    continue
                 v = self.field_view(f)
                 per_group = self.uniform[f] and mk > 1
                 if per_group:

@@ -165,6 +165,7 @@ class GpuDagExecutor(DagExecutor):
         self._scratch: List = []
         self._sink: List = self._scratch
         self._schedules: Dict = {}
+        self.last_schedule = None  # the schedule the last non-replayed execute_dag recorded
         self.replays = 0  # execute_dag calls served from a recorded schedule
         self.lowerer = Lowerer(self)
         self.comm = None
@@ -444,6 +445,7 @@ class GpuDagExecutor(DagExecutor):
         shape (the caller then fetches whole chunks instead)."""
         import dataclasses
 
+        from ...lowering import MODE_HOST_COUNT
         from ...storage import geometry_only
         from .dist import DistPiecesLaunch
 
@@ -480,6 +482,7 @@ class GpuDagExecutor(DagExecutor):
             # resolved); other ranks' pieces only give their group's shape
             rows, gkeys = [], []
             mko = 1
+            counts = {}
             with _remote_chunks(fetch, arrays), geometry_only():
                 for key in keys:
                     r, g = low.task_pieces(program, cfg, target, key, leaves, out_items,
@@ -489,6 +492,9 @@ class GpuDagExecutor(DagExecutor):
                     for i, (row, gk) in enumerate(zip(r, g)):
                         by_group.setdefault(gk, []).append((i, row))
                     for gk, items in by_group.items():
+                        # the group's global element count along the reduced
+                        # dims: its pieces on every rank together
+                        counts[(key, gk)] = sum(math.prod(row.extent[d] for d in red) for _, row in items)
                         first = items[0][1]
                         mko = max(mko, math.prod(first.extent[d] for d in range(len(first.extent))
                                                  if d not in red))
@@ -514,6 +520,7 @@ class GpuDagExecutor(DagExecutor):
             meta["kept_ok"] = all(math.prod(r.extent[d] for d in range(len(r.extent)) if d not in red) == mko
                                   for r in rows)
             meta["mko"] = mko
+            meta["counts"] = [counts[gkeys[i]] for i in meta["starts"]]
             return rows, red
 
         def one_row_per_group():
@@ -538,7 +545,8 @@ class GpuDagExecutor(DagExecutor):
         out = [meta["fetch"]] if meta.get("fetch") is not None else []
         out.append(DistPiecesLaunch(self, launch, np.array(starts + [len(lay.rows)], dtype=np.int64),
                                     table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys],
-                                    soa_direct=soa_direct))
+                                    soa_direct=soa_direct,
+                                    host_counts=meta["counts"] if launch.prog.mode & MODE_HOST_COUNT else None))
         return out
 
     def _lower_local(self, program, cfg, target, keys):
@@ -947,6 +955,28 @@ class GpuDagExecutor(DagExecutor):
                 for n in names:
                     gen_of[n] = g
         steps = []
+        try:
+            self._lower_steps(dag, nodes, chains, members, gen_of, resume, steps)
+        except LoweringError:
+            # the ops before the one that cannot be lowered run (and are marked
+            # written), as the reference's executor runs op by op: a resume
+            # then picks up after them
+            if steps:
+                self._run_schedule(_Schedule(steps, parallel), stream, callbacks)
+            raise
+        sched = _Schedule(steps, parallel)
+        self.last_schedule = sched
+        self._run_schedule(sched, stream, callbacks)
+        # later calls with the same plan, names, resume flag and written
+        # state replay the launch list without re-walking the DAG
+        if book is None or book.dag_ref() is not plan_dag:
+            book = self._schedules[key] = _Schedules(plan_dag, targets)
+            weakref.finalize(plan_dag, _drop_entry, weakref.ref(self), "_schedules", key)
+        book.add(state, sched)
+
+    def _lower_steps(self, dag, nodes, chains, members, gen_of, resume, steps):
+        """The recorded steps of one execute_dag, appended to ``steps`` op by
+        op (so a LoweringError leaves the lowered prefix in ``steps``)."""
         for name, node in visit_nodes(dag, resume=resume):
             gen = gen_of.get(name, 0)
             if name in members:
@@ -995,15 +1025,6 @@ class GpuDagExecutor(DagExecutor):
             op = node.get("primitive_op")
             events = list(node.get("fused_from", ())) + [(name, op.num_tasks if op is not None else 1)]
             steps.append((name, tuple(launches), tuple(marks), tuple(events), gen))
-        sched = _Schedule(steps, parallel)
-        self.last_schedule = sched
-        self._run_schedule(sched, stream, callbacks)
-        # later calls with the same plan, names, resume flag and written
-        # state replay the launch list without re-walking the DAG
-        if book is None or book.dag_ref() is not plan_dag:
-            book = self._schedules[key] = _Schedules(plan_dag, targets)
-            weakref.finalize(plan_dag, _drop_entry, weakref.ref(self), "_schedules", key)
-        book.add(state, sched)
 
     PARALLEL_STREAMS = 4  # GPU_MAX_HW_QUEUES on the box: one hardware queue each
 

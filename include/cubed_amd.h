@@ -61,6 +61,7 @@ extern "C" {
 #define CUBED_MODE_PARTIALS 16
 #define CUBED_MODE_STREAM_W2 32
 #define CUBED_MODE_STREAM_W4 64
+#define CUBED_MODE_HOST_COUNT 128 /* partials: COUNT fields are left to the host */
 
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)
@@ -171,6 +172,10 @@ typedef struct {
                                  /* streaming JIT kernels give each thread  */
                                  /* 2 / 4 groups of 4 kept elements         */
                                  /* (interpreted kernels ignore the bits)   */
+                                 /* +128 (CUBED_MODE_HOST_COUNT): partials  */
+                                 /* mode leaves plain COUNT fields unwritten*/
+                                 /* in the SoA block -- the host fills them */
+                                 /* with the (geometry-known) global count  */
   int32_t nleaves;
   uint8_t leaf_kind[CUBED_MAX_LEAVES];
   uint8_t leaf_dtype[CUBED_MAX_LEAVES];
@@ -236,6 +241,12 @@ int cubed_fused_chunks_compiled(void* handle, const cubed_program_t* prog,
 /* The generated source / code object size of a compiled program (diagnostics). */
 const char* cubed_fused_source(const void* handle);
 int64_t cubed_fused_code_bytes(const void* handle);
+
+/* Split target of streaming reductions: a grid too small to cover HBM
+ * latency unsplit is split toward this many workgroups (default 1024, ~4 per
+ * CU).  Process-wide tuning hook for probes (tools/); workgroups <= 0 only
+ * queries.  Returns the previous value. */
+int64_t cubed_stream_split_target(int64_t workgroups);
 
 /* Workspace the call above needs (split reductions keep partial
  * accumulators there).  Pure host function. */

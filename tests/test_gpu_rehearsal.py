@@ -50,7 +50,7 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
     np.testing.assert_allclose(want, host.mean(axis=0).astype(np.float32), rtol=1e-6)
 
     world = 8
-    totals, counts = [], []
+    totals, counts, host_counts = [], [], []
     direct = []
     for r in range(world):
         comm = LoopbackComm(r, world, record=True)
@@ -65,17 +65,29 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
         recs = [t for kind, t in comm.records if kind == "all_reduce_sum"]
         tot = [t for t in recs if t.dtype == torch.float64]
         cnt = [t for t in recs if t.dtype == torch.int64]
-        assert len(tot) == 1 and len(cnt) == 1
+        assert len(tot) == 1
         totals.append(tot[0].cpu().numpy())
-        counts.append(cnt[0].cpu().numpy())
+        if launches[0].soa_direct:
+            # the global counts are filled by the host (CUBED_MODE_HOST_COUNT):
+            # nothing crosses the ranks for them; every rank holds the totals
+            assert cnt == [] and any(launches[0].host_count)
+            host_counts.append(launches[0].field_view(0).view(-1, launches[0].mko)[:, 0].cpu().numpy())
+        else:
+            assert len(cnt) == 1
+            counts.append(cnt[0].cpu().numpy())
         del x, m, ex
     # uniform groups stream as merged kept runs (no combine_groups pass)
     assert all(direct) == (shape[0] % chunks[0] == 0 and shape[1] % cols == 0)
     total = totals[0].copy()
-    count = counts[0].copy()
     for r in range(1, world):  # the RCCL sum, in rank order
         total += totals[r]
-        count += counts[r]
+    if host_counts:
+        assert len(host_counts) == world and all(np.array_equal(h, host_counts[0]) for h in host_counts)
+        count = host_counts[0]
+    else:
+        count = counts[0].copy()
+        for r in range(1, world):
+            count += counts[r]
     ngroups = -(-shape[1] // cols)
     assert count.shape == (ngroups,)
     assert np.all(count == shape[0])

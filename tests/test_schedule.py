@@ -219,3 +219,32 @@ def test_parallel_chain_runs_with_its_last_member(built, dry):
     for head, ch in chains.items():
         (st,) = [st for st in sched.steps if st[0] == head]
         assert st[4] == max(gen_of[n] for n in ch.nodes)
+
+
+def test_lowering_failure_runs_the_lowered_prefix(built, dry):
+    """a plan whose later op cannot be lowered (an untraceable
+    chunk function) raises LoweringError after running the ops lowered
+    before it -- they are marked written, as the reference's op-by-op
+    executor would have completed them, so a resume picks up after them."""
+    import numpy as np
+    import pytest
+
+    import cubed_amd as cubed
+    from cubed_amd.core.ops import map_blocks
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.lowering import LoweringError
+
+    spec = cubed.Spec(allowed_mem="1GB", executor=dry)
+    a = cubed.from_array(np.arange(16.0).reshape(4, 4), chunks=(2, 2), spec=spec)
+    b = a + 1
+
+    def opaque(x):
+        return np.asarray(sorted(x.ravel())).reshape(x.shape)  # not traceable
+
+    c = map_blocks(opaque, b, dtype=b.dtype)
+    plan = arrays_to_plan(c)
+    dry.launched.clear()
+    with pytest.raises(LoweringError):
+        plan.execute(executor=dry, array_names=[c.name], optimize_graph=False)
+    assert dry.launched  # b's op ran
+    assert b.zarray.written and not c.zarray.written
