@@ -2,7 +2,8 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CSRC := cubed_amd/csrc
-SRCS := $(CSRC)/fused.hip $(CSRC)/stream_f32.hip $(CSRC)/stream_f64.hip $(CSRC)/stream_i64.hip $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm_chain.hip
+STREAMS := $(foreach v,f32 f64 i64,$(CSRC)/stream_$(v).hip $(CSRC)/stream_$(v)_split.hip)
+SRCS := $(CSRC)/fused.hip $(STREAMS) $(CSRC)/jit.hip $(CSRC)/copy_random.hip $(CSRC)/gemm_chain.hip
 CPPSRCS := $(CSRC)/codec.cpp
 OBJS := $(SRCS:.hip=.o) $(CPPSRCS:.cpp=.o)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \

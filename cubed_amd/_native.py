@@ -131,6 +131,11 @@ def lib():
     L.cubed_copy_boxes.restype = c_int
     L.cubed_gemm_chain_path.argtypes = [c_void_p, c_int64, c_void_p, c_int32, c_int32]
     L.cubed_gemm_chain_path.restype = c_int
+    L.cubed_gemm_grid_check.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_int32]
+    L.cubed_gemm_grid_check.restype = c_int
+    L.cubed_gemm_chain_grid.argtypes = [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                                        c_int32, c_int32, c_void_p, c_void_p]
+    L.cubed_gemm_chain_grid.restype = c_int
     L.cubed_gemm_chain.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                    c_void_p, c_int32, c_void_p]
     L.cubed_gemm_chain.restype = c_int
@@ -195,6 +200,7 @@ EXPORTED_SYMBOLS = (
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
     "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_zstd_decompress", "cubed_lz4_chunk_decompress", "cubed_gemm_chain", "cubed_gemm_chain_path",
+    "cubed_gemm_grid_check", "cubed_gemm_chain_grid",
 )
 
 

@@ -165,10 +165,14 @@ int stream_groups(const cubed_program_t& P) {
 // Streaming launches: a grid that fills the CUs without splitting the
 // reduced dim runs unsplit (a time split costs more than the occupancy it
 // adds: config 2 W = 2 unsplit 6.81 TB/s vs 6.02 for the round-2 3-way
-// split, profiles/r02_stream_ab.log); smaller grids split toward
-// 1024 workgroups (~4 per CU: config 1's stream 0.503 ms vs 0.542 at 2048,
-// 0.59-0.62 at 4096-8192, 1.10 at 256).
-static int64_t g_stream_target = 1024;  // cubed_stream_split_target() (probes)
+// split, profiles/r02_stream_ab.log); smaller grids split toward ONE
+// workgroup per CU (256): with the split fold in the last-arriving
+// workgroup (round 4) one long row walk per CU beats 2-12 shorter ones --
+// config 1 0.452 ms (256) / 0.479 (512) / 0.498 (1024) / 0.511 (2048), the
+// per-rank share of config 3 0.204 / 0.221 / 0.242 / 0.292, a grid of 384
+// or 160 (not whole rounds of 256) slower than either neighbour
+// (profiles/r04_split_sweep.log).
+static int64_t g_stream_target = 256;  // cubed_stream_split_target() (probes)
 
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red, int stream_w) {

@@ -102,10 +102,19 @@ struct LaunchPlan {
   int64_t blocks;
 };
 
-// stream.hip: the streaming fast path (mode bit CUBED_MODE_STREAM)
+// stream_impl.h: the streaming fast path (mode bit CUBED_MODE_STREAM), one
+// instantiation per (value type, split variant) in stream_*.hip
+template <typename V, bool SPLIT>
+void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
+                     const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st);
 template <typename V>
 void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L, const cubed_task_t* d_tasks,
-                   int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st);
+                   int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
+  if (L.nsplit > 1 && P.nfields > 0)
+    launch_stream_v<V, true>(P, dP, L, d_tasks, ntasks, max_kept, ws, st);
+  else
+    launch_stream_v<V, false>(P, dP, L, d_tasks, ntasks, max_kept, ws, st);
+}
 
 dim3 grid_of(int64_t blocks);
 // stream_w: kept VEC groups per thread of a streaming launch (1 for the

@@ -482,11 +482,23 @@ constexpr int HF_BM = 256, HF_BN = 256;
 // [256 rows][BK k] (BK*4-byte rows, CPR = BK/4 16-B chunks, chunk c of row
 // r at position c ^ swz(r): conflict-free b128 reads) + B [BK k][256 n]
 // (1 KiB rows, as in HBM).
-template <int BK, int NS, bool PP = false>
+// GRID: the output is one (M, N) matrix of ti x tj chunks (task I*tj + J =
+// chunk (I, J), every chunk cm x cn except the last row / column, the same
+// k segmentation in every task) and 256 x 256 tiles cover the WHOLE matrix:
+// a tile that straddles a chunk boundary takes each row's A from its chunk
+// row I0 or I0 + 1 and each column's B / C from chunk column J0 or J0 + 1
+// (cm, cn >= 256, so never more than two).  Per-chunk tiling pads every
+// 5000-wide chunk to 20 x 256 = 5120 (4.9 % of the MFMAs discarded); the grid
+// pads 40000 to 157 x 256 = 40192 (1 %).
+struct GemmGrid {
+  int64_t ti, tj, cm, cn, M, N;
+};
+
+template <int BK, int NS, bool PP = false, bool GRID = false>
 __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
                                                         int64_t tiles_m, int64_t tiles_n,
-                                                        const char* __restrict__ zero) {
+                                                        const char* __restrict__ zero, GemmGrid gg) {
   static_assert(BK == 16 || BK == 32, "K step of 16 or 32");
   constexpr int SA = HF_BM * BK * 4, SB = BK * HF_BN * 4, STAGE = SA + SB;
   constexpr int CPR = BK / 4;            // 16-B chunks per A row
@@ -501,10 +513,26 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
   tile_of<HF_BM, HF_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  // GRID: (m0, n0) in the whole matrix; chunk rows I0 (, I0 + 1) and columns
+  // J0 (, J0 + 1) of the tile; mb / nb: the first row / column of chunk I0+1 / J0+1
+  int64_t I0 = 0, J0 = 0, mb = 0, nb = 0;
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
-  const int64_t M = T->m, N = T->n, KT = T->ktot;
+  const cubed_gemm_chain_t* __restrict__ TI1 = T;  // chunk (I0 + 1, J0): A rows
+  const cubed_gemm_chain_t* __restrict__ TJ1 = T;  // chunk (I0, J0 + 1): B columns
+  if constexpr (GRID) {
+    I0 = m0 / gg.cm;
+    J0 = n0 / gg.cn;
+    mb = (I0 + 1) * gg.cm;
+    nb = (J0 + 1) * gg.cn;
+    T = tasks + I0 * gg.tj + J0;
+    TI1 = (I0 + 1 < gg.ti) ? T + gg.tj : T;
+    TJ1 = (J0 + 1 < gg.tj) ? T + 1 : T;
+  }
+  const int64_t M = GRID ? gg.M : T->m, N = GRID ? gg.N : T->n, KT = T->ktot;
   if (m0 >= M || n0 >= N) return;
   const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
+  // segment s of chunk (I0 + 1, J0) / (I0, J0 + 1): same index offset
+  const int64_t dsI = TI1->seg0 - T->seg0, dsJ = TJ1->seg0 - T->seg0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -513,47 +541,63 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
   // ---- staging geometry (constant over the K loop)
   // A: wave w instruction i stages rows RPI*(NA*w + i) + lane/CPR; LDS
   // position lane%CPR of the row holds global chunk (lane%CPR) ^ swz(row)
+  // (GRID: a lane's row / column is local to its chunk, hiA / hiB select
+  // chunk row I0 + 1 / column J0 + 1)
   int64_t gmA[NA];
   int kA[NA];
+  bool hiA[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int r = RPI * (NA * w + i) + lane / CPR;
-    gmA[i] = (m0 + r < M ? m0 + r : M - 1);
+    int64_t g = (m0 + r < M ? m0 + r : M - 1);
+    hiA[i] = GRID && g >= mb;
+    gmA[i] = GRID ? g - (hiA[i] ? mb : I0 * gg.cm) : g;
     kA[i] = 4 * ((lane % CPR) ^ ((r >> SWS) & (CPR - 1)));
   }
   // B: wave w instruction i stages k-row NB*w + i, columns n0 + 4*lane .. +3
   const int rB0 = NB * w;
-  const int64_t gnB = (n0 + 4 * lane + 4 <= N ? n0 + 4 * lane : N - 4);
+  int64_t gnB = (n0 + 4 * lane + 4 <= N ? n0 + 4 * lane : N - 4);
+  const bool hiB = GRID && gnB >= nb;
+  if constexpr (GRID) gnB -= hiB ? nb : J0 * gg.cn;
 
   int64_t s = seg0, ks = 0;
-  const char* a_cur = (const char*)(uintptr_t)segs[s].a;
-  const char* b_cur = (const char*)(uintptr_t)segs[s].b;
-  int64_t lda4 = segs[s].lda * 4, ldb4 = segs[s].ldb * 4;
+  // per segment: A of chunk rows I0 / I0+1, B (and its row pitch) of chunk
+  // columns J0 / J0+1 -- wave-uniform; a lane selects with hiA / hiB
+  auto ptr = [&](int64_t i) { return (const char*)(uintptr_t)segs[i].a; };
+  auto ptrb = [&](int64_t i) { return (const char*)(uintptr_t)segs[i].b; };
+  const char* a_cur = ptr(s);
+  const char* a_hi = ptr(s + dsI);
+  const char* b_cur = ptrb(s);
+  const char* b_hi = ptrb(s + dsJ);
+  int64_t lda4 = segs[s].lda * 4, ldb4 = segs[s].ldb * 4, ldb4h = segs[s + dsJ].ldb * 4;
   int64_t ke = segs[s].k;
 
   auto stage = [&](int64_t k0, CUBED_L char* buf) {
     const char* sa[NA];
     const char* sb[NB];
+    const char* bb = hiB ? b_hi : b_cur;
+    const int64_t lb = hiB ? ldb4h : ldb4;
 #pragma unroll
-    for (int i = 0; i < NA; ++i) sa[i] = a_cur + gmA[i] * lda4 + (k0 - ks + kA[i]) * 4;
+    for (int i = 0; i < NA; ++i) sa[i] = (hiA[i] ? a_hi : a_cur) + gmA[i] * lda4 + (k0 - ks + kA[i]) * 4;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) sb[i] = b_cur + (k0 - ks + rB0 + i) * ldb4 + gnB * 4;
+    for (int i = 0; i < NB; ++i) sb[i] = bb + (k0 - ks + rB0 + i) * lb + gnB * 4;
     if (k0 + BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
       const bool has_next = s + 1 < segN;
       const int64_t sn = has_next ? s + 1 : s;
-      const char* na = (const char*)(uintptr_t)segs[sn].a;
-      const char* nb = (const char*)(uintptr_t)segs[sn].b;
-      const int64_t nlda4 = segs[sn].lda * 4, nldb4 = segs[sn].ldb * 4;
+      const char* nal = ptr(sn);
+      const char* nah = ptr(sn + dsI);
+      const char* nbp = hiB ? ptrb(sn + dsJ) : ptrb(sn);
+      const int64_t nlda4 = segs[sn].lda * 4, nldb4 = (hiB ? segs[sn + dsJ].ldb : segs[sn].ldb) * 4;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         const int64_t ka = k0 + kA[i];
-        const char* pa = na + gmA[i] * nlda4 + (ka - ke) * 4;
+        const char* pa = (hiA[i] ? nah : nal) + gmA[i] * nlda4 + (ka - ke) * 4;
         sa[i] = ka < ke ? sa[i] : ((has_next && ka < KT) ? pa : zero);
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         const int64_t kb = k0 + rB0 + i;
-        const char* pb = nb + (kb - ke) * nldb4 + gnB * 4;
+        const char* pb = nbp + (kb - ke) * nldb4 + gnB * 4;
         sb[i] = kb < ke ? sb[i] : ((has_next && kb < KT) ? pb : zero);
       }
     }
@@ -564,10 +608,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
     if (k0 + BK >= ke && s + 1 < segN) {  // the next step starts in the next segment
       ks = ke;
       ++s;
-      a_cur = (const char*)(uintptr_t)segs[s].a;
-      b_cur = (const char*)(uintptr_t)segs[s].b;
+      a_cur = ptr(s);
+      a_hi = ptr(s + dsI);
+      b_cur = ptrb(s);
+      b_hi = ptrb(s + dsJ);
       lda4 = segs[s].lda * 4;
       ldb4 = segs[s].ldb * 4;
+      ldb4h = segs[s + dsJ].ldb * 4;
       ke = ks + segs[s].k;
     }
   };
@@ -690,18 +737,27 @@ __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chai
 
   // ---- epilogue: accumulator (rb, q) register r = row wm + 32 rb + (r&3) +
   // 8 (r>>2) + 4h, column wn + 4 r32 + q: one float4 per (rb, r)
-  char* C = (char*)(uintptr_t)T->c;
-  const int64_t ldc = T->ldc;
   const bool accum = T->accumulate != 0;
   const int64_t gn = n0 + wn + 4 * r32;
   if (gn < N) {
+    // GRID: this lane's 4 columns lie in chunk column J0 or J0 + 1 (cn % 4 == 0);
+    // each row in chunk row I0 or I0 + 1
+    const bool hn = GRID && gn >= nb;
+    const cubed_gemm_chain_t* __restrict__ TC0 = hn ? TJ1 : T;  // chunk (I0, J)
+    const cubed_gemm_chain_t* __restrict__ TC1 = TC0 + (TI1 - T);  // chunk (I0 + 1, J)
+    const int64_t ln = GRID ? gn - (hn ? nb : J0 * gg.cn) : gn;
+    char* C0 = (char*)(uintptr_t)TC0->c;
+    char* C1 = (char*)(uintptr_t)TC1->c;
+    const int64_t ldc0 = TC0->ldc, ldc1 = TC1->ldc;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t gm = m0 + wm + 32 * rb + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (gm < M) {
-          CUBED_G f32x4* c = (CUBED_G f32x4*)(uintptr_t)(C + (gm * ldc + gn) * 4);
+          const bool hm = GRID && gm >= mb;
+          const int64_t lm = GRID ? gm - (hm ? mb : I0 * gg.cm) : gm;
+          CUBED_G f32x4* c = (CUBED_G f32x4*)(uintptr_t)((hm ? C1 : C0) + (lm * (hm ? ldc1 : ldc0) + ln) * 4);
           f32x4 v = {acc[rb][0][r], acc[rb][1][r], acc[rb][2][r], acc[rb][3][r]};
           if (accum) v += *c;
           *c = v;
@@ -867,7 +923,7 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     const int64_t blocks = ntasks * tm * tn;
     if (blocks > 0x7fffffff) return fail("grid too large");
     hipLaunchKernelGGL((k_gemm_f32_chain<16, 4>), dim3((unsigned)blocks), dim3(512), 0, st, d_tasks, d_segs, tm,
-                       tn, (const char*)d_zero);
+                       tn, (const char*)d_zero, GemmGrid{});
   } else {
     const int64_t tm = (max_m + TM - 1) / TM, tn = (max_n + TN - 1) / TN;
     const int64_t blocks = ntasks * tm * tn;
@@ -891,6 +947,67 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
         return CUBED_E_DTYPE;
     }
   }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+// ---- grid tiling (f32 MFMA): the chain set is a ti x tj chunk grid of one
+// (M, N) output, task I*tj + J = chunk (I, J); see k_gemm_f32_chain<.., GRID>.
+extern "C" int cubed_gemm_grid_check(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                                     const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,
+                                     int32_t out_dtype) {
+  if (!tasks || !segs || ti < 1 || tj < 1) return fail("grid: bad argument");
+  if (in_dtype != CUBED_F32 || out_dtype != CUBED_F32) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: f32 only");
+    return CUBED_E_LAYOUT;
+  }
+  const int64_t n = ti * tj;
+  if (cubed_gemm_chain_path(tasks, n, segs, in_dtype, out_dtype) != CUBED_GEMM_MFMA) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: shapes do not fit the MFMA path");
+    return CUBED_E_LAYOUT;
+  }
+  const cubed_gemm_chain_t& T0 = tasks[0];
+  const int64_t cm = T0.m, cn = T0.n;
+  auto bad = [&](const char* why) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: %s", why);
+    return CUBED_E_LAYOUT;
+  };
+  if ((ti > 1 && cm < HF_BM) || (tj > 1 && cn < HF_BN) || cn % 4) return bad("chunks narrower than a tile");
+  for (int64_t I = 0; I < ti; ++I)
+    for (int64_t J = 0; J < tj; ++J) {
+      const cubed_gemm_chain_t& T = tasks[I * tj + J];
+      if (T.seg0 < 0 || T.seg0 + T.nseg > nsegs) return fail("task out of range");
+      if (T.nseg != T0.nseg || T.ktot != T0.ktot || T.accumulate != T0.accumulate) return bad("tasks differ in k");
+      if ((I + 1 < ti && T.m != cm) || (J + 1 < tj && T.n != cn) || T.m > cm || T.n > cn || T.m < 1 || T.n < 1)
+        return bad("not a regular chunk grid");
+      if (T.m != tasks[I * tj].m || T.n != tasks[J].n) return bad("not a regular chunk grid");
+      for (int64_t s = 0; s < T.nseg; ++s) {
+        const cubed_gemm_seg_t &a = segs[T.seg0 + s], &b = segs[T0.seg0 + s];
+        if (a.k != b.k || a.lda != segs[tasks[J].seg0 + s].lda) return bad("segments differ across the grid");
+        if (a.ldb != segs[tasks[J].seg0 + s].ldb) return bad("B row pitches differ down a chunk column");
+      }
+    }
+  return 0;
+}
+
+extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
+                                     int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs,
+                                     const cubed_gemm_seg_t* d_segs, int64_t nsegs, int32_t in_dtype,
+                                     int32_t out_dtype, const void* d_zero, void* stream) {
+  if (!d_tasks || !d_segs || !d_zero) return fail("grid: bad argument");
+  if (int rc = cubed_gemm_grid_check(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype)) return rc;
+  GemmGrid gg;
+  gg.ti = ti;
+  gg.tj = tj;
+  gg.cm = tasks[0].m;
+  gg.cn = tasks[0].n;
+  gg.M = (ti - 1) * gg.cm + tasks[(ti - 1) * tj].m;
+  gg.N = (tj - 1) * gg.cn + tasks[tj - 1].n;
+  const int64_t tm = (gg.M + HF_BM - 1) / HF_BM, tn = (gg.N + HF_BN - 1) / HF_BN;
+  if (tm * tn > 0x7fffffff) return fail("grid too large");
+  hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), dim3((unsigned)(tm * tn)), dim3(512), 0,
+                     (hipStream_t)stream, d_tasks, d_segs, tm, tn, (const char*)d_zero, gg);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
   return 0;

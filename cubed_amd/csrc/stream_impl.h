@@ -1,5 +1,5 @@
 // stream_impl.h -- streaming fast path of the fused chunk kernels (gfx950),
-// instantiated per value type by stream_f32.hip / stream_f64.hip / stream_i64.hip.
+// instantiated per value type and split variant by stream_{f32,f64,i64}{,_split}.hip.
 //
 // Covers the hot shape of Cubed's reduction path: after canonicalisation a
 // task is [one reduced dim] x [one packed kept dim] (or just the kept dim for
@@ -36,8 +36,8 @@ __global__ __launch_bounds__(kBlock) void k_stream(
 // keeps each a few copies of the interpreter instead of up to 8 (build time);
 // the accumulation order per element -- and so every result bit -- is the same.
 template <typename V, bool SPLIT>
-static void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
-                            const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
+void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
+                     const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
   const dim3 grid = grid_of(L.blocks);
   switch (P.nleaves) {
     case 1: hipLaunchKernelGGL((k_stream<V, 1, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
@@ -47,18 +47,10 @@ static void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP,
   }
 }
 
-template <typename V>
-void launch_stream(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L, const cubed_task_t* d_tasks,
-                   int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
-  if (L.nsplit > 1 && P.nfields > 0)
-    launch_stream_v<V, true>(P, dP, L, d_tasks, ntasks, max_kept, ws, st);
-  else
-    launch_stream_v<V, false>(P, dP, L, d_tasks, ntasks, max_kept, ws, st);
-}
-
-// one TU per value type (stream_f32.hip, stream_f64.hip, stream_i64.hip):
-// the three compile in parallel
-template void launch_stream<CUBED_STREAM_V>(const cubed_program_t&, const cubed_program_t*, const LaunchPlan&,
-                                            const cubed_task_t*, int64_t, int64_t, Acc*, hipStream_t);
+// one TU per (value type, split variant): stream_{f32,f64,i64}{,_split}.hip
+// compile in parallel; launch_stream (fused.hip) picks the variant
+template void launch_stream_v<CUBED_STREAM_V, CUBED_STREAM_SPLIT>(
+    const cubed_program_t&, const cubed_program_t*, const LaunchPlan&, const cubed_task_t*, int64_t, int64_t,
+    Acc*, hipStream_t);
 
 }  // namespace cubed

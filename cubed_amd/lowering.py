@@ -749,7 +749,9 @@ class GemmLaunch:
     loop (a per-chunk product is a chain of one segment).  The hand-written
     kernels of csrc/gemm_chain.hip run every dtype (MFMA for bf16 / f32)."""
 
-    def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None):
+    GRID = True  # probes set False to time the per-chunk tiling
+
+    def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None):
         import torch
 
         self.n = len(tasks)
@@ -758,6 +760,13 @@ class GemmLaunch:
         self.segs = np.ascontiguousarray(segs) if len(segs) else np.zeros(1, dtype=nat.SEG_DTYPE)
         self.zero = zero_ptr
         self.path = nat.GEMM_AUTO if path is None else path
+        # (ti, tj): the tasks are the C-order chunk grid of one output; the
+        # f32 MFMA kernel then tiles the whole matrix (cubed_gemm_chain_grid)
+        self.grid = None
+        if grid is not None and self.GRID and self.path == nat.GEMM_AUTO and grid[0] * grid[1] == self.n and \
+                nat.lib().cubed_gemm_grid_check(self.tasks.ctypes.data, grid[0], grid[1], self.segs.ctypes.data,
+                                                len(self.segs), in_code, out_code) == 0:
+            self.grid = tuple(grid)
         self.flops = 2.0 * float(sum(int(t["m"]) * int(t["n"]) * int(t["ktot"]) for t in self.tasks))
         if not self.n:
             return
@@ -775,6 +784,12 @@ class GemmLaunch:
         if not self.n:
             return
         L = nat.lib()
+        if self.grid is not None:
+            nat.check(L.cubed_gemm_chain_grid(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.grid[0],
+                                              self.grid[1], self.segs.ctypes.data, self.d_segs.data_ptr(),
+                                              len(self.segs), self.in_code, self.out_code, self.zero, stream),
+                      "cubed_gemm_chain_grid")
+            return
         nat.check(L.cubed_gemm_chain(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.n,
                                      self.segs.ctypes.data, self.d_segs.data_ptr(), len(self.segs),
                                      self.in_code, self.out_code, self.zero, self.path, stream),

@@ -315,6 +315,7 @@ class DistPiecesLaunch:
         # group: one int64 per group crosses the ranks (as in PartialsLaunch)
         self.uniform = [r == "count" for r in rops]
         self.sum_only = all(r in SUM_ROPS for r in rops)
+        self.acc_int = acc_int
         # host_counts (CUBED_MODE_HOST_COUNT, soa_direct only): the kernel leaves
         # the COUNT fields alone; they hold each group's global count, filled
         # here once, and never cross the ranks
@@ -325,7 +326,6 @@ class DistPiecesLaunch:
             for f in range(self.nf):
                 if self.host_count[f]:
                     self.field_view(f).view(self.ngroups, self.mko).copy_(hc[:, None].expand(self.ngroups, self.mko))
-        self.acc_int = acc_int
         uniq = sorted(set(owners))
         self.root = uniq[0] if len(uniq) == 1 else None
         self.finish_here = ctx.rank in uniq

@@ -833,8 +833,11 @@ class GpuDagExecutor(DagExecutor):
         in_dt = in_dt if in_dt is not None else out_dt
         if in_dt not in (np.float32, np.float64, np.int64, ir.bfloat16):
             raise LoweringError(f"matmul of {in_dt} is not lowered (f32, bf16, f64, int64)")
+        # one GPU, every output chunk in C order: tiles may cover the whole
+        # matrix (cubed_gemm_chain_grid checks the grid and the dtype)
+        grid = (F.numblocks[0], F.numblocks[-1]) if self.world == 1 and len(tasks) > 1 else None
         out.append(GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
-                              self.zero_page()))
+                              self.zero_page(), grid=grid))
         return out
 
     def _compiled_chain_dist(self, chain, target, keys):

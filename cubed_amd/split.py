@@ -106,7 +106,7 @@ def collect_leaves_nodes(e):
     return out
 
 
-def split_program(p: ir.ExprProgram, max_parts: int = 8):
+def split_program(p: ir.ExprProgram, max_parts: int = 32):
     """[(subexpression program, its dtype)], remainder program: the parts
     are computed first, in order; part i is read by the remainder (and by
     later parts) as Arg(p.nargs + i) with identity axes."""

@@ -243,7 +243,7 @@ const char* cubed_fused_source(const void* handle);
 int64_t cubed_fused_code_bytes(const void* handle);
 
 /* Split target of streaming reductions: a grid too small to cover HBM
- * latency unsplit is split toward this many workgroups (default 1024, ~4 per
+ * latency unsplit is split toward this many workgroups (default 256, one per
  * CU).  Process-wide tuning hook for probes (tools/); workgroups <= 0 only
  * queries.  Returns the previous value. */
 int64_t cubed_stream_split_target(int64_t workgroups);
@@ -382,6 +382,22 @@ int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* 
                      int64_t ntasks, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
                      int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
                      int32_t path, void* stream);
+
+/* Grid tiling (f32 MFMA): the ti x tj tasks are the C-order chunk grid of
+ * ONE (M, N) output (task I*tj + J = chunk (I, J); chunks cm x cn with cm,
+ * cn >= 256 and cn % 4 == 0 except the last row / column; every task the
+ * same k segmentation).  256 x 256 tiles then cover the whole matrix --
+ * a tile straddling chunk boundaries reads each row / column from its own
+ * chunk -- instead of padding every chunk to whole tiles.  Same results
+ * contract as cubed_gemm_chain (each element one f32 accumulation chain over
+ * K in the same order).  cubed_gemm_grid_check (host only): 0 when the
+ * tables fit, CUBED_E_LAYOUT (message set) otherwise. */
+int cubed_gemm_grid_check(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                          const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype, int32_t out_dtype);
+int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti,
+                          int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
+                          int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
+                          void* stream);
 
 /* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
  * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and

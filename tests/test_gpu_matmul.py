@@ -214,3 +214,50 @@ def test_bf16_astype_round_trip(ex):
     nan = np.isnan(exp)
     assert np.array_equal(np.isnan(got), nan)  # NaN payloads differ (torch: 0xFFFF), NaN-ness not
     assert np.array_equal(got[~nan].view(np.uint32), exp[~nan].view(np.uint32))
+
+
+@pytest.mark.parametrize("shapes", [((600, 1200), (1200, 704), (300, 400), (400, 352)),    # 2 x 2 regular grid
+                                    ((700, 1300), (1300, 1000), (300, 400), (400, 352))])  # ragged last row / column
+def test_grid_tiling_f32_bit_identical(gpu_executor, shapes, monkeypatch):
+    """f32 chains over a regular chunk grid run as ONE grid-tiled launch
+    (cubed_gemm_chain_grid: 256 x 256 tiles over the whole matrix, tiles
+    straddling chunk boundaries) -- bit-identical to the per-chunk tiling
+    (each output element is the same f32 chain over K), and within the
+    bound of the f64 product (K = 1300: four k chunks of 400 / 100)."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    sa, sb, ca, cb = shapes
+    x, y = _operands(sa, sb, 21)
+    res = {}
+    for grid in (True, False):
+        monkeypatch.setattr(L.GemmLaunch, "GRID", grid)
+        e = GpuDagExecutor("cuda:0")
+        spec = cubed.Spec(allowed_mem="2GB", executor=e)
+        a = cubed.from_array(x, chunks=ca, spec=spec)
+        b = cubed.from_array(y, chunks=cb, spec=spec)
+        res[grid] = xp.matmul(a, b).compute()
+        gl = _launches(e)
+        assert len(gl) == 1 and (gl[0].grid is not None) == grid
+        if grid:
+            assert gl[0].grid == (-(-sa[0] // ca[0]), -(-sb[1] // cb[1]))
+    assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
+    _check_bound(res[True], x.astype(np.float64), y.astype(np.float64), sa[1])
+
+
+def test_grid_check_refuses_irregular_tables(built):
+    """The host check: chunks narrower than a tile, bf16, or a task table
+    that is not a chunk grid stay on the per-chunk launch."""
+    tasks = np.zeros(4, dtype=nat.CHAIN_DTYPE)
+    segs = np.zeros(4, dtype=nat.SEG_DTYPE)
+    for t in range(4):
+        segs[t] = (4096 * (t + 1), 8192 * (t + 1), 64, 64, 128, 0)
+        tasks[t] = (65536 * (t + 1), 128, 128, 128, t, 1, 64, 0)
+    L_ = nat.lib()
+    args = (tasks.ctypes.data, 2, 2, segs.ctypes.data, 4)
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) != 0  # 128 < 256
+    tasks["m"], tasks["n"], tasks["ldc"] = 256, 256, 256
+    segs["ldb"] = 256
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) == 0
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)) != 0
+    tasks["ktot"][3] = 128
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) != 0

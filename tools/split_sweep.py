@@ -60,13 +60,30 @@ def main():
         arrays_to_plan(a).execute(executor=ex, array_names=[a.name])
         return a, xp.mean((a + 1) * 2, axis=0)
 
+    def quad(ex):
+        spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex)
+        random.seed(1000)
+        u = xp.astype(crandom.random((1000, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+        v = xp.astype(crandom.random((1000, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+        arrays_to_plan(u, v).execute(executor=ex, array_names=[u.name, v.name])
+        return (u, v), xp.mean(u * v, axis=0)
+
+    if os.environ.get("SWEEP_QUAD_W"):
+        import cubed_amd.lowering as Lw
+
+        for w in (1, 2, 4):
+            tgt = f"W{w}"
+            Lw.FORCE_STREAM_W = w
+            run("quad_means", GpuDagExecutor("cuda:0"), quad)
+        Lw.FORCE_STREAM_W = None
+
     for tgt in targets:
         L.cubed_stream_split_target(tgt)
         run("share7000", GpuDagExecutor("cuda:0"), share(7000))
         run("rehearsed_rank0_of_8", GpuDagExecutor("cuda:0", comm=LoopbackComm(0, 8)), share(50000))
         run("config1", GpuDagExecutor("cuda:0"), config1, steps=10)
         run("elided_full", GpuDagExecutor("cuda:0"), share(50000), steps=10)
-    L.cubed_stream_split_target(1024)
+    L.cubed_stream_split_target(256)
     print(json.dumps(out))
 
 
