@@ -83,6 +83,41 @@ __device__ __forceinline__ bool tile_of(int64_t g, int64_t tiles_m, int64_t tile
   return true;
 }
 
+// GRID: the output is one (M, N) matrix of ti x tj chunks (task I*tj + J =
+// chunk (I, J), every chunk cm x cn except the last row / column, the same
+// k segmentation in every task) and 256 x 256 tiles cover the WHOLE matrix:
+// a tile that straddles a chunk boundary takes each row's A from its chunk
+// row I0 or I0 + 1 and each column's B / C from chunk column J0 or J0 + 1
+// (cm, cn >= 256, so never more than two).  Per-chunk tiling pads every
+// 5000-wide chunk to 20 x 256 = 5120 (4.9 % of the MFMAs discarded); the grid
+// pads 40000 to 157 x 256 = 40192 (1 %).
+struct GemmGrid {
+  int64_t ti, tj, cm, cn, M, N;
+};
+
+// The tile's chunk rows / columns (GRID): T = chunk (I0, J0), TI1 = (I0+1, J0),
+// TJ1 = (I0, J0+1) (T itself past the last row / column); mb / nb = first row
+// / column of chunk row I0+1 / column J0+1.
+struct GridTile {
+  int64_t I0, J0, mb, nb;
+  const cubed_gemm_chain_t* T;
+  const cubed_gemm_chain_t* TI1;
+  const cubed_gemm_chain_t* TJ1;
+};
+
+__device__ __forceinline__ GridTile grid_tile(const cubed_gemm_chain_t* tasks, const GemmGrid& gg, int64_t m0,
+                                              int64_t n0) {
+  GridTile g;
+  g.I0 = m0 / gg.cm;
+  g.J0 = n0 / gg.cn;
+  g.mb = (g.I0 + 1) * gg.cm;
+  g.nb = (g.J0 + 1) * gg.cn;
+  g.T = tasks + g.I0 * gg.tj + g.J0;
+  g.TI1 = (g.I0 + 1 < gg.ti) ? g.T + gg.tj : g.T;
+  g.TJ1 = (g.J0 + 1 < gg.tj) ? g.T + 1 : g.T;
+  return g;
+}
+
 // ------------------------------------------------------------------ bf16 MFMA
 // LDS is a ring of HB_NS slots, each one 32-deep K step of the 256x256 tile:
 // A [256 rows][32 k] (64-B rows) + B [32 k-rows][256 n] (512-B rows).  The
@@ -124,19 +159,22 @@ __device__ __forceinline__ void glds16(const char* src, CUBED_L char* dst) {
 // with register staging (see the K loop).
 // NS: ring slots (each step p+NS-1 is staged while step p is consumed);
 // GM: tile rows per XCD tile group.
-template <bool OUT_BF16, int ABL = 0, int PP = 0, int NS = HB_NS, int GM = 4>
+template <bool OUT_BF16, int ABL = 0, int PP = 0, int NS = HB_NS, int GM = 4, bool GRID = false>
 __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                          const cubed_gemm_seg_t* __restrict__ segs,
                                                          int64_t tiles_m, int64_t tiles_n,
-                                                         const char* __restrict__ zero) {
+                                                         const char* __restrict__ zero, GemmGrid gg) {
   __shared__ __attribute__((aligned(1024))) char lds_[(PP == 2 ? 2 : NS) * HB_STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
   tile_of<HB_BM, HB_BN, GM>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
-  const cubed_gemm_chain_t* __restrict__ T = tasks + t;
-  const int64_t M = T->m, N = T->n, KT = T->ktot;
+  GridTile gt{0, 0, 0, 0, tasks + t, tasks + t, tasks + t};
+  if constexpr (GRID) gt = grid_tile(tasks, gg, m0, n0);
+  const cubed_gemm_chain_t* __restrict__ T = gt.T;
+  const int64_t M = GRID ? gg.M : T->m, N = GRID ? gg.N : T->n, KT = T->ktot;
   if (m0 >= M || n0 >= N) return;
   const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
+  const int64_t dsI = gt.TI1->seg0 - T->seg0, dsJ = gt.TJ1->seg0 - T->seg0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -146,29 +184,38 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   // A: wave w stages rows 16*(2w+i) + lane>>2 (i = 0, 1); 16-B chunk lane&3 of
   // the 64-B LDS row holds global chunk (lane&3) ^ 2*((row>>3)&1)
   // [(row>>3)&1 = (lane>>5)&1], which makes the fragment reads conflict-free.
+  // (GRID: rows / columns local to their chunk; hiA / hiB select chunk row
+  // I0 + 1 / column J0 + 1)
   int64_t gmA[2];
+  bool hiA[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int64_t r = 16 * (2 * w + i) + (lane >> 2);
-    gmA[i] = (m0 + r < M ? m0 + r : M - 1);
+    const int64_t g = (m0 + r < M ? m0 + r : M - 1);
+    hiA[i] = GRID && g >= gt.mb;
+    gmA[i] = GRID ? g - (hiA[i] ? gt.mb : gt.I0 * gg.cm) : g;
   }
   const int dA = 8 * ((lane & 3) ^ (2 * ((lane >> 5) & 1)));
   // B: wave w stages k-rows 2*(2w+i) + lane>>5; 16-B chunk c = lane&31 of the
   // LDS row holds global chunk c ^ swz(row), swz(r) = 2*((r&3) | ((r>>3)&1)<<2).
   int rB[2];
   int64_t gnB[2];
+  bool hiB[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = 2 * (2 * w + i) + (lane >> 5);
     rB[i] = r;
     const int swz = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
     int64_t n = n0 + 8 * ((lane & 31) ^ swz);
-    gnB[i] = (n + 8 <= N ? n : N - 8);
+    n = (n + 8 <= N ? n : N - 8);
+    hiB[i] = GRID && n >= gt.nb;
+    gnB[i] = GRID ? n - (hiB[i] ? gt.nb : gt.J0 * gg.cn) : n;
   }
 
   // ---- wave-uniform segment state (the segment containing the next step to stage)
   int64_t s = seg0, ks = 0;
   Seg cur = load_seg(segs, s);
+  Seg curI = load_seg(segs, s + dsI), curJ = load_seg(segs, s + dsJ);  // GRID: chunk row I0+1 / column J0+1
   int64_t ke = segs[s].k;
 
   // per-lane byte offsets of this lane's 4 pieces inside the current segment
@@ -178,7 +225,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       offSA[i] = gmA[i] * cur.lda2 + dA * 2;
-      offSB[i] = rB[i] * cur.ldb2 + gnB[i] * 2;
+      offSB[i] = rB[i] * (hiB[i] ? curJ.ldb2 : cur.ldb2) + gnB[i] * 2;
     }
   };
   seg_offsets();
@@ -188,25 +235,26 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   const char* st_src[4];
   CUBED_L char* st_dst[4];
   auto stage_addrs = [&](int64_t k0, CUBED_L char* buf) {
-    const char* a0 = cur.a + (k0 - ks) * 2;        // uniform
-    const char* b0 = cur.b + (k0 - ks) * cur.ldb2;  // uniform
     const char* sa[2];
     const char* sb[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      sa[i] = a0 + offSA[i];
-      sb[i] = b0 + offSB[i];
+      sa[i] = (hiA[i] ? curI.a : cur.a) + (k0 - ks) * 2 + offSA[i];
+      sb[i] = hiB[i] ? curJ.b + (k0 - ks) * curJ.ldb2 + offSB[i] : cur.b + (k0 - ks) * cur.ldb2 + offSB[i];
     }
     if (k0 + HB_BK > ke) {  // uniform: a segment boundary (or the chain's end) inside this step
       const bool has_next = s + 1 < segN;
-      const Seg nxt = load_seg(segs, has_next ? s + 1 : s);
+      const int64_t sn = has_next ? s + 1 : s;
+      const Seg nxt = load_seg(segs, sn);
+      const Seg nxtI = load_seg(segs, sn + dsI), nxtJ = load_seg(segs, sn + dsJ);
       const int64_t ka = k0 + dA;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const char* na = nxt.a + gmA[i] * nxt.lda2 + (ka - ke) * 2;
+        const char* na = (hiA[i] ? nxtI.a : nxt.a) + gmA[i] * nxt.lda2 + (ka - ke) * 2;
         sa[i] = ka < ke ? sa[i] : ((has_next && ka < KT) ? na : zero);
         const int64_t kb = k0 + rB[i];
-        const char* nbp = nxt.b + (kb - ke) * nxt.ldb2 + gnB[i] * 2;
+        const char* nbp = hiB[i] ? nxtJ.b + (kb - ke) * nxtJ.ldb2 + gnB[i] * 2
+                                 : nxt.b + (kb - ke) * nxt.ldb2 + gnB[i] * 2;
         sb[i] = kb < ke ? sb[i] : ((has_next && kb < KT) ? nbp : zero);
       }
     }
@@ -222,6 +270,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
       ks = ke;
       ++s;
       cur = load_seg(segs, s);
+      curI = load_seg(segs, s + dsI);
+      curJ = load_seg(segs, s + dsJ);
       ke = ks + segs[s].k;
       seg_offsets();
     }
@@ -429,8 +479,6 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
   }
 
   // ---- epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
-  char* C = (char*)(uintptr_t)T->c;
-  const int64_t ldc = T->ldc;
   const bool accum = T->accumulate != 0;
 #pragma unroll
   for (int mb = 0; mb < 8; ++mb)
@@ -441,13 +489,21 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
         const int64_t gm = m0 + wr * 128 + mb * 16 + (lane >> 4) * 4 + r;
         const int64_t gn = n0 + wc * 64 + nb * 16 + (lane & 15);
         if (gm < M && gn < N) {
+          // the element's chunk (GRID) and its offset inside it
+          const bool hm = GRID && gm >= gt.mb, hn = GRID && gn >= gt.nb;
+          const cubed_gemm_chain_t* TC = hn ? gt.TJ1 : T;
+          if (hm) TC += gt.TI1 - T;
+          const int64_t lm = GRID ? gm - (hm ? gt.mb : gt.I0 * gg.cm) : gm;
+          const int64_t ln = GRID ? gn - (hn ? gt.nb : gt.J0 * gg.cn) : gn;
+          char* C = (char*)(uintptr_t)TC->c;
+          const int64_t ldc = TC->ldc;
           float v = acc[mb][nb][r];
           if constexpr (OUT_BF16) {
-            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (gm * ldc + gn) * 2);
+            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (lm * ldc + ln) * 2);
             if (accum) v += bf16_to_f32(*c);
             *c = f32_to_bf16(v);
           } else {
-            CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (gm * ldc + gn) * 4);
+            CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (lm * ldc + ln) * 4);
             if (accum) v += *c;
             *c = v;
           }
@@ -482,18 +538,6 @@ constexpr int HF_BM = 256, HF_BN = 256;
 // [256 rows][BK k] (BK*4-byte rows, CPR = BK/4 16-B chunks, chunk c of row
 // r at position c ^ swz(r): conflict-free b128 reads) + B [BK k][256 n]
 // (1 KiB rows, as in HBM).
-// GRID: the output is one (M, N) matrix of ti x tj chunks (task I*tj + J =
-// chunk (I, J), every chunk cm x cn except the last row / column, the same
-// k segmentation in every task) and 256 x 256 tiles cover the WHOLE matrix:
-// a tile that straddles a chunk boundary takes each row's A from its chunk
-// row I0 or I0 + 1 and each column's B / C from chunk column J0 or J0 + 1
-// (cm, cn >= 256, so never more than two).  Per-chunk tiling pads every
-// 5000-wide chunk to 20 x 256 = 5120 (4.9 % of the MFMAs discarded); the grid
-// pads 40000 to 157 x 256 = 40192 (1 %).
-struct GemmGrid {
-  int64_t ti, tj, cm, cn, M, N;
-};
-
 template <int BK, int NS, bool PP = false, bool GRID = false>
 __global__ __launch_bounds__(512, 2) void k_gemm_f32_chain(const cubed_gemm_chain_t* __restrict__ tasks,
                                                         const cubed_gemm_seg_t* __restrict__ segs,
@@ -914,9 +958,9 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     // one-wave-per-SIMD experiments in tools/gemm_bf16_probe.hip measured
     // slower (profiles/r02_gemm_bf16_q4_w4.log)
     if (out_dtype == CUBED_BF16)
-      hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
+      hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{});
     else
-      hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z);
+      hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{});
   } else if (path == CUBED_GEMM_MFMA && in_dtype == CUBED_F32) {
     if (!d_zero) return fail("the f32 path needs a zero page");
     const int64_t tm = (max_m + HF_BM - 1) / HF_BM, tn = (max_n + HF_BN - 1) / HF_BN;
@@ -958,8 +1002,10 @@ extern "C" int cubed_gemm_grid_check(const cubed_gemm_chain_t* tasks, int64_t ti
                                      const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,
                                      int32_t out_dtype) {
   if (!tasks || !segs || ti < 1 || tj < 1) return fail("grid: bad argument");
-  if (in_dtype != CUBED_F32 || out_dtype != CUBED_F32) {
-    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: f32 only");
+  const bool bf = in_dtype == CUBED_BF16;
+  if (!(in_dtype == CUBED_F32 && out_dtype == CUBED_F32) &&
+      !(bf && (out_dtype == CUBED_F32 || out_dtype == CUBED_BF16))) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: f32 or bf16 inputs only");
     return CUBED_E_LAYOUT;
   }
   const int64_t n = ti * tj;
@@ -973,7 +1019,9 @@ extern "C" int cubed_gemm_grid_check(const cubed_gemm_chain_t* tasks, int64_t ti
     snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_grid: %s", why);
     return CUBED_E_LAYOUT;
   };
-  if ((ti > 1 && cm < HF_BM) || (tj > 1 && cn < HF_BN) || cn % 4) return bad("chunks narrower than a tile");
+  // a tile spans at most two chunks per dim; a lane's 16-B column group
+  // (4 f32 / 8 bf16) never straddles a chunk column
+  if ((ti > 1 && cm < HF_BM) || (tj > 1 && cn < HF_BN) || cn % (bf ? 8 : 4)) return bad("chunks narrower than a tile");
   for (int64_t I = 0; I < ti; ++I)
     for (int64_t J = 0; J < tj; ++J) {
       const cubed_gemm_chain_t& T = tasks[I * tj + J];
@@ -1006,8 +1054,16 @@ extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cube
   gg.N = (tj - 1) * gg.cn + tasks[tj - 1].n;
   const int64_t tm = (gg.M + HF_BM - 1) / HF_BM, tn = (gg.N + HF_BN - 1) / HF_BN;
   if (tm * tn > 0x7fffffff) return fail("grid too large");
-  hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), dim3((unsigned)(tm * tn)), dim3(512), 0,
-                     (hipStream_t)stream, d_tasks, d_segs, tm, tn, (const char*)d_zero, gg);
+  const dim3 grid((unsigned)(tm * tn)), blk(512);
+  hipStream_t st = (hipStream_t)stream;
+  const char* z = (const char*)d_zero;
+  static_assert(HB_BM == HF_BM && HB_BN == HF_BN, "one tile size");
+  if (in_dtype == CUBED_BF16 && out_dtype == CUBED_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, 1, HB_NS, 4, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
+  else if (in_dtype == CUBED_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1, HB_NS, 4, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
+  else
+    hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
   return 0;

@@ -383,9 +383,9 @@ int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* 
                      int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
                      int32_t path, void* stream);
 
-/* Grid tiling (f32 MFMA): the ti x tj tasks are the C-order chunk grid of
- * ONE (M, N) output (task I*tj + J = chunk (I, J); chunks cm x cn with cm,
- * cn >= 256 and cn % 4 == 0 except the last row / column; every task the
+/* Grid tiling (f32 / bf16 MFMA): the ti x tj tasks are the C-order chunk grid
+ * of ONE (M, N) output (task I*tj + J = chunk (I, J); chunks cm x cn with cm,
+ * cn >= 256 and cn % 4 (f32) / 8 (bf16) == 0 except the last row / column; every task the
  * same k segmentation).  256 x 256 tiles then cover the whole matrix --
  * a tile straddling chunk boundaries reads each row / column from its own
  * chunk -- instead of padding every chunk to whole tiles.  Same results

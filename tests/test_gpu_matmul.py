@@ -218,7 +218,8 @@ def test_bf16_astype_round_trip(ex):
 
 @pytest.mark.parametrize("shapes", [((600, 1200), (1200, 704), (300, 400), (400, 352)),    # 2 x 2 regular grid
                                     ((700, 1300), (1300, 1000), (300, 400), (400, 352))])  # ragged last row / column
-def test_grid_tiling_f32_bit_identical(gpu_executor, shapes, monkeypatch):
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_grid_tiling_bit_identical(gpu_executor, shapes, dt, monkeypatch):
     """f32 chains over a regular chunk grid run as ONE grid-tiled launch
     (cubed_gemm_chain_grid: 256 x 256 tiles over the whole matrix, tiles
     straddling chunk boundaries) -- bit-identical to the per-chunk tiling
@@ -235,13 +236,19 @@ def test_grid_tiling_f32_bit_identical(gpu_executor, shapes, monkeypatch):
         spec = cubed.Spec(allowed_mem="2GB", executor=e)
         a = cubed.from_array(x, chunks=ca, spec=spec)
         b = cubed.from_array(y, chunks=cb, spec=spec)
+        if dt == "bf16":
+            a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
         res[grid] = xp.matmul(a, b).compute()
         gl = _launches(e)
         assert len(gl) == 1 and (gl[0].grid is not None) == grid
         if grid:
             assert gl[0].grid == (-(-sa[0] // ca[0]), -(-sb[1] // cb[1]))
     assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
-    _check_bound(res[True], x.astype(np.float64), y.astype(np.float64), sa[1])
+    if dt == "bf16":
+        x64, y64 = _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64)
+    else:
+        x64, y64 = x.astype(np.float64), y.astype(np.float64)
+    _check_bound(res[True], x64, y64, sa[1], out_bf16=(dt == "bf16"))
 
 
 def test_grid_check_refuses_irregular_tables(built):
@@ -258,6 +265,7 @@ def test_grid_check_refuses_irregular_tables(built):
     tasks["m"], tasks["n"], tasks["ldc"] = 256, 256, 256
     segs["ldb"] = 256
     assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) == 0
-    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)) != 0
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)) == 0
+    assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float64), ir.dtype_code(np.float64)) != 0
     tasks["ktot"][3] = 128
     assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) != 0
