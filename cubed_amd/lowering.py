@@ -750,6 +750,11 @@ class GemmLaunch:
     kernels of csrc/gemm_chain.hip run every dtype (MFMA for bf16 / f32)."""
 
     GRID = True  # probes set False to time the per-chunk tiling
+    # input dtypes that take the grid tiling by default: f32 measured 133.6 TF
+    # grid vs 129-130 per chunk; bf16 1038 vs 1085-1097 (its M slot -- the
+    # fragment reads + staging issue, DESIGN.md -- gets the per-lane chunk
+    # selects), so bf16 keeps per-chunk tiles unless a test opts in
+    GRID_INPUTS = {ir.dtype_code(np.float32)}
 
     def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None):
         import torch
@@ -763,7 +768,8 @@ class GemmLaunch:
         # (ti, tj): the tasks are the C-order chunk grid of one output; the
         # f32 MFMA kernel then tiles the whole matrix (cubed_gemm_chain_grid)
         self.grid = None
-        if grid is not None and self.GRID and self.path == nat.GEMM_AUTO and grid[0] * grid[1] == self.n and \
+        if grid is not None and self.GRID and in_code in self.GRID_INPUTS and self.path == nat.GEMM_AUTO and \
+                grid[0] * grid[1] == self.n and \
                 nat.lib().cubed_gemm_grid_check(self.tasks.ctypes.data, grid[0], grid[1], self.segs.ctypes.data,
                                                 len(self.segs), in_code, out_code) == 0:
             self.grid = tuple(grid)

@@ -276,9 +276,21 @@ class GpuDagExecutor(DagExecutor):
 
     def _cache_put(self, key, obj, launches, owned):
         """Cache ``launches`` (and the buffers they own) for ``obj``; the
-        entry goes when ``obj`` is collected (its id may then be reused)."""
-        self._cache[key] = (weakref.ref(obj), launches, owned)
+        entry goes when ``obj`` is collected (its id may then be reused).
+        The launches hold device addresses: an entry recorded before an
+        array was released or moved (storage.alloc_epoch) is not reused."""
+        from ...storage import alloc_epoch
+
+        self._cache[key] = (weakref.ref(obj), launches, owned, alloc_epoch())
         weakref.finalize(obj, _drop_entry, weakref.ref(self), "_cache", key)
+
+    def _cache_hit(self, key, obj):
+        from ...storage import alloc_epoch
+
+        entry = self._cache.get(key)
+        if entry is not None and entry[0]() is obj and entry[3] == alloc_epoch():
+            return entry
+        return None
 
     class _Collect:
         def __init__(self, ex):
@@ -703,8 +715,8 @@ class GpuDagExecutor(DagExecutor):
     # -- execution -------------------------------------------------------------
     def compiled(self, name, node):
         pipeline = node["pipeline"]
-        entry = self._cache.get(id(pipeline))
-        if entry is not None and entry[0]() is pipeline:
+        entry = self._cache_hit(id(pipeline), pipeline)
+        if entry is not None:
             return entry[1]
         err = None
         with self._Collect(self) as owned:
@@ -756,8 +768,8 @@ class GpuDagExecutor(DagExecutor):
         from ...gemm_chains import GemmChain
 
         key = ("gemm" if isinstance(chain, GemmChain) else "chain", id(chain.first_spec))
-        entry = self._cache.get(key)
-        if entry is not None and entry[0]() is chain.first_spec:
+        entry = self._cache_hit(key, chain.first_spec)
+        if entry is not None:
             return entry[1]
         with self._Collect(self) as owned:
             if isinstance(chain, GemmChain):

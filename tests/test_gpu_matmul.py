@@ -131,7 +131,7 @@ _orig_init = L.GemmLaunch.__init__
 
 
 def _forced_path_init(path):
-    def init(self, tasks, segs, in_code, out_code, device, zero_ptr, path_=None):
+    def init(self, tasks, segs, in_code, out_code, device, zero_ptr, path_=None, grid=None):
         _orig_init(self, tasks, segs, in_code, out_code, device, zero_ptr, path=path)
     return init
 
@@ -217,19 +217,20 @@ def test_bf16_astype_round_trip(ex):
 
 
 @pytest.mark.parametrize("shapes", [((600, 1200), (1200, 704), (300, 400), (400, 352)),    # 2 x 2 regular grid
-                                    ((700, 1300), (1300, 1000), (300, 400), (400, 352))])  # ragged last row / column
+                                    ((700, 1304), (1304, 1000), (300, 400), (400, 352))])  # ragged last row / column
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_grid_tiling_bit_identical(gpu_executor, shapes, dt, monkeypatch):
     """f32 chains over a regular chunk grid run as ONE grid-tiled launch
     (cubed_gemm_chain_grid: 256 x 256 tiles over the whole matrix, tiles
     straddling chunk boundaries) -- bit-identical to the per-chunk tiling
     (each output element is the same f32 chain over K), and within the
-    bound of the f64 product (K = 1300: four k chunks of 400 / 100)."""
+    bound of the f64 product (K = 1304: four k chunks of 400 / 104)."""
     from cubed_amd.runtime.executors.gpu import GpuDagExecutor
 
     sa, sb, ca, cb = shapes
     x, y = _operands(sa, sb, 21)
     res = {}
+    monkeypatch.setattr(L.GemmLaunch, "GRID_INPUTS", {ir.dtype_code(np.float32), ir.dtype_code(ir.bfloat16)})
     for grid in (True, False):
         monkeypatch.setattr(L.GemmLaunch, "GRID", grid)
         e = GpuDagExecutor("cuda:0")
