@@ -120,6 +120,38 @@ def test_mean_rounds_match_numpy():
     assert np.allclose(got32, f.astype(np.float64).mean(axis=0), rtol=1e-6, atol=0)
 
 
+@pytest.mark.parametrize("axis", [0, 1, (0, 1), None])
+@pytest.mark.parametrize("correction", [0.0, 1.0])
+def test_var_restatement_matches_numpy(axis, correction):
+    """The oracle's var (parity unpinned: no reference var) against numpy's
+    f64 var over merge rounds (small allowed_mem) and one round; std = sqrt."""
+    rng = np.random.default_rng(3)
+    x = rng.random((90, 70)) * 5 + 1e3  # offset mean: cancellation-sensitive
+    want = x.var(axis=axis, ddof=correction)
+    for mem in (30_000, 2_000_000_000):
+        got = R.var(x, (7, 9), axis, allowed_mem=mem, correction=correction)
+        assert np.allclose(got, want, rtol=1e-12, atol=0)
+    s = R.var(x, (7, 9), axis, allowed_mem=30_000, correction=correction, sqrt=True)
+    assert np.allclose(s, x.std(axis=axis, ddof=correction), rtol=1e-12, atol=0)
+
+
+def test_var_restatement_edge_cases():
+    x = np.arange(12.0).reshape(3, 4)
+    x[1, 2] = np.nan
+    got = R.var(x, (2, 2), 0, allowed_mem=10**9)
+    want = x.var(axis=0)
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    assert np.allclose(got[~np.isnan(got)], want[~np.isnan(want)], rtol=1e-12)
+    # reduced extent <= correction: numpy's rcount clamp gives inf / nan
+    y = np.array([[2.0, 3.0]])
+    with np.errstate(invalid="ignore", divide="ignore"):
+        assert np.array_equal(R.var(y, (1, 1), 0, 10**9, correction=1.0), y.var(axis=0, ddof=1), equal_nan=True)
+    f = x[[0, 2]].astype(np.float32)
+    g = R.var(f, (1, 3), 0, allowed_mem=10**9)
+    assert g.dtype == np.float32
+    assert np.allclose(g, f.astype(np.float64).var(axis=0), rtol=1e-6)
+
+
 def test_reference_cases_through_oracle():
     c = load("reference_cases.json")
     a = np.array(c["mean_axis_0"]["a"])
