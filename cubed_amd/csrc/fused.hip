@@ -180,6 +180,7 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
   L.kernel = P->mode & 3;
   L.vec = (P->mode & 4) ? 4 : 1;
   L.nsplit = 1;
+  L.balanced = 0;
   L.bpt = 1;
   const int64_t target = 2048;  // ~8 workgroups per CU
   if (P->mode & CUBED_MODE_STREAM) {
@@ -201,6 +202,19 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     // a multiple of 8 workgroups (the surplus exits at once): stream_body
     // maps them to XCD-contiguous runs
     L.blocks = (ntasks * L.nsplit * L.bpt + 7) / 8 * 8;
+    // every task the same reduced extent (the host's CUBED_MODE_STREAM_EVEN):
+    // exactly the target's workgroups, each an equal run of (task, column
+    // block, row) units (stream_body's balanced split) -- a uniform split
+    // of 49 column blocks x 5 keeps 245 of 256 CUs busy
+    const int64_t G = g_stream_target / 8 * 8;
+    const int64_t units = base * max_red;
+    if (L.nsplit > 1 && (P->mode & CUBED_MODE_STREAM_EVEN) && G >= 8 && units / G >= 64 &&
+        L.bpt * kBlock >= slots) {
+      const int64_t minlen = units / G;
+      L.nsplit = (int32_t)((max_red + minlen - 1) / minlen + 1);
+      L.balanced = 1;
+      L.blocks = G;
+    }
   } else if (L.kernel == 0) {
     const int64_t items = (max_kept + L.vec - 1) / L.vec;
     L.bpt = (items + kBlock - 1) / kBlock;

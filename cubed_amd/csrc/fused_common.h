@@ -96,7 +96,8 @@ struct LaunchPlan {
   int kernel;     // 0 = A, 1 = B
   int vec;        // 1 or 4
   int64_t bpt;    // A: blocks per task per split
-  int32_t nsplit;
+  int32_t nsplit;  // split slots (balanced: the most contributors of one column block)
+  int32_t balanced;  // stream: CUBED_MODE_STREAM_EVEN's balanced split (kernel gets -nsplit)
   int64_t soa_elems;  // partials mode: SoA per-field partials at the workspace start
   int64_t ws_bytes;
   int64_t blocks;

@@ -852,22 +852,26 @@ CUBED_DEV void stream_body(
   const int64_t G = (int64_t)gridDim.x * gridDim.y;
   int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   if ((G & 7) == 0) g = (g & 7) * (G >> 3) + (g >> 3);
-  const int64_t b = g % bpt;
-  const int64_t rest = g / bpt;
-  const int s = (int)(rest % nsplit);
-  const int64_t t = rest / nsplit;
-  if (t >= ntasks) return;
-  const cubed_task_t* __restrict__ T = tasks + t;
   // nr = 0 (map), 1 (rows) or 2 (chunks x rows: a reduction chain whose
   // chunks sit at a slot stride that is not the rows' own continuation)
   const int nr = P.nred;
+  auto nrd_of = [&](const cubed_task_t* T) {
+    return (nr == 2 ? T->extent[0] : 1) * (nr ? T->extent[nr - 1] : 1);
+  };
+  // One segment: rows [lo, hi) of column block b of task t, split slot s of
+  // nsp (lo < 0: the uniform split's range of slot s).
+  auto segment = [&](int64_t t, int64_t b, int s, int nsp, int64_t lo, int64_t hi) {
+  const cubed_task_t* __restrict__ T = tasks + t;
   const int64_t nk = T->extent[nr];
   const int64_t nrow = nr ? T->extent[nr - 1] : 1;
   const int64_t nq = nr == 2 ? T->extent[0] : 1;
   const int64_t nrd = nq * nrow;
   // thread slots: whole waves of W groups each
   const int64_t slots = ((nk + 256 * W - 1) / (256 * W)) * 64;
-  const int64_t r0 = nrd * s / nsplit, r1 = nrd * (s + 1) / nsplit;
+  // (a balanced run is clamped to the task's own extent: the host promises
+  // equal extents, the clamp keeps a broken promise inside the task)
+  const int64_t r0 = lo < 0 ? nrd * s / nsp : (lo < nrd ? lo : nrd);
+  const int64_t r1 = lo < 0 ? nrd * (s + 1) / nsp : (hi < nrd ? hi : nrd);
 
   const CUBED_G V* base[NL];
   int64_t rs[NL], qs[NL];
@@ -953,10 +957,11 @@ CUBED_DEV void stream_body(
   const bool partials = (P.mode & CUBED_MODE_PARTIALS) != 0;
   const int nf = P.nfields;
   const int64_t nsoa = ntasks * max_kept;
+  const int64_t nslots = nsplit < 0 ? -nsplit : nsplit;  // split slots in the workspace
   Acc* __restrict__ soa = ws - (int64_t)nf * nsoa;
   const int64_t slots_max = ((max_kept + 256 * W - 1) / (256 * W)) * 64;
   const int64_t nblk = (slots_max + kBlock - 1) / kBlock;
-  uint32_t* __restrict__ cnt = (uint32_t*)(ws + (int64_t)nsplit * nsoa * nf);
+  uint32_t* __restrict__ cnt = (uint32_t*)(ws + (int64_t)nslots * nsoa * nf);
   __shared__ int last_arrival;
   // partials mode writes every element < max_kept (the identity past an
   // edge task's extent), so every column block of max_kept takes part
@@ -1028,7 +1033,7 @@ CUBED_DEV void stream_body(
       if (threadIdx.x == 0) {
         uint32_t* c = cnt + t * nblk + bb / kBlock;
         const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int lastv = old == (uint32_t)(nsplit - 1);
+        const int lastv = old == (uint32_t)(nsp - 1);
         if (lastv) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_arrival = lastv;
       }
@@ -1055,7 +1060,7 @@ CUBED_DEV void stream_body(
           for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
             x[e][f] = stored(f) ? load_through(pe[e] + f) : acc_init(P.field_rop[f], P.field_acc[f]);
         int sp = 1;
-        for (; sp + 4 <= nsplit; sp += 4) {
+        for (; sp + 4 <= nsp; sp += 4) {
           Acc v[4][4][CUBED_MAX_FIELDS];
 #pragma unroll
           for (int u = 0; u < 4; ++u)
@@ -1070,7 +1075,7 @@ CUBED_DEV void stream_body(
 #pragma unroll
             for (int u = 0; u < 4; ++u) fields_combine(x[e], v[u][e], P);
         }
-        for (; sp < nsplit; ++sp) {
+        for (; sp < nsp; ++sp) {
           Acc v[4][CUBED_MAX_FIELDS];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -1132,6 +1137,50 @@ CUBED_DEV void stream_body(
         finish<4>(P, T, acc[j], ooff);
       }
     }
+  }
+  };
+
+  // Balanced split (SPLIT variant, nsplit < 0 = -slots; the host's
+  // CUBED_MODE_STREAM_EVEN: every task the same reduced extent): the (task,
+  // column block, row) units of the launch, in that order, are cut into G
+  // equal runs, one per workgroup -- a run may end in one column block and
+  // continue in the next, so every CU streams the same number of rows (a
+  // uniform split leaves G mod blocks CUs idle: 11 of 256 for 49 column
+  // blocks).  Column block c's contributors are the workgroups whose runs
+  // meet it, in row order: slot g - owner(first row); the last to arrive
+  // folds them in that order.  One call site of segment() (it is inlined).
+  const bool bal = SPLIT && nsplit < 0;
+  int64_t nru = 1, Ut = 1, u = 0, S1 = 0;
+  if (bal) {
+    nru = nrd_of(tasks);
+    Ut = ntasks * bpt * nru;
+    u = g * Ut / G;
+    S1 = (g + 1) * Ut / G;
+    if (u >= S1) return;
+  } else if (g / bpt / nsplit >= ntasks) {
+    return;
+  }
+  for (;;) {
+    int64_t t, b, lo = -1, hi = -1;
+    int s, nsp = nsplit;
+    if (bal) {
+      const int64_t c = u / nru;
+      lo = u - c * nru;
+      hi = S1 - c * nru < nru ? S1 - c * nru : nru;
+      const int64_t first = ((c * nru + 1) * G - 1) / Ut, last = (((c + 1) * nru) * G - 1) / Ut;
+      t = c / bpt;
+      b = c % bpt;
+      s = (int)(g - first);
+      nsp = (int)(last - first + 1);
+      u = c * nru + hi;
+    } else {
+      b = g % bpt;
+      const int64_t rest = g / bpt;
+      s = (int)(rest % nsplit);
+      t = rest / nsplit;
+    }
+    segment(t, b, s, nsp, lo, hi);
+    if (!bal || u >= S1) break;
   }
 }
 

@@ -39,11 +39,12 @@ template <typename V, bool SPLIT>
 void launch_stream_v(const cubed_program_t& P, const cubed_program_t* dP, const LaunchPlan& L,
                      const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept, Acc* ws, hipStream_t st) {
   const dim3 grid = grid_of(L.blocks);
+  const int32_t ns = L.balanced ? -L.nsplit : L.nsplit;  // balanced split: -slots
   switch (P.nleaves) {
-    case 1: hipLaunchKernelGGL((k_stream<V, 1, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 2: hipLaunchKernelGGL((k_stream<V, 2, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    case 3: hipLaunchKernelGGL((k_stream<V, 3, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
-    default: hipLaunchKernelGGL((k_stream<V, 4, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, L.nsplit, ws, max_kept); break;
+    case 1: hipLaunchKernelGGL((k_stream<V, 1, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, ns, ws, max_kept); break;
+    case 2: hipLaunchKernelGGL((k_stream<V, 2, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, ns, ws, max_kept); break;
+    case 3: hipLaunchKernelGGL((k_stream<V, 3, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, ns, ws, max_kept); break;
+    default: hipLaunchKernelGGL((k_stream<V, 4, 2, SPLIT>), grid, dim3(kBlock), 0, st, dP, d_tasks, ntasks, L.bpt, ns, ws, max_kept); break;
   }
 }
 

@@ -1046,6 +1046,11 @@ class Lowerer:
                 rows = layout.rows
         if stream:
             P.mode |= MODE_STREAM | _stream_groups_mode(P, len(rows), layout.max_kept)
+            if P.nfields > 0 and len({_red_extent(r, layout) for r in rows}) == 1:
+                # every task the same reduced extent: a split launch may cut
+                # the (task, column block, row) units into equal runs per
+                # workgroup (stream_body's balanced split)
+                P.mode |= MODE_STREAM_EVEN
         if partials:
             if P.nfields == 0:
                 raise LoweringError("partials mode needs a reduction")
@@ -1683,6 +1688,13 @@ _VTYPE_DTYPE = {V_F32: np.dtype(np.float32), V_F64: np.dtype(np.float64), V_I64:
 MODE_STREAM_W2 = 32  # include/cubed_amd.h CUBED_MODE_STREAM_W2
 MODE_STREAM_W4 = 64  # include/cubed_amd.h CUBED_MODE_STREAM_W4
 MODE_HOST_COUNT = 128  # include/cubed_amd.h CUBED_MODE_HOST_COUNT
+MODE_STREAM_EVEN = 256  # include/cubed_amd.h CUBED_MODE_STREAM_EVEN
+
+
+def _red_extent(row, layout) -> int:
+    """Reduced extent of one streaming task (stream_body's nrd)."""
+    ext = _apply_groups(row, layout.groups)[0]
+    return int(np.prod(ext[:layout.nred], dtype=np.int64))
 
 
 def _stream_unroll(itemsize: int, nleaves: int) -> int:

@@ -62,6 +62,7 @@ extern "C" {
 #define CUBED_MODE_STREAM_W2 32
 #define CUBED_MODE_STREAM_W4 64
 #define CUBED_MODE_HOST_COUNT 128 /* partials: COUNT fields are left to the host */
+#define CUBED_MODE_STREAM_EVEN 256 /* stream: every task the same reduced extent */
 
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)

@@ -240,6 +240,43 @@ def test_config1_small(ex):
     assert np.allclose(got, exp, rtol=1e-12, atol=0)
 
 
+@pytest.mark.parametrize("even", [True, False])
+def test_balanced_split_streams(gpu_executor, monkeypatch, even):
+    """Split streaming reductions with the balanced split (every task the same
+    reduced extent: CUBED_MODE_STREAM_EVEN, equal row runs per workgroup that
+    cross column blocks) and with the uniform split (bit cleared): int64 sums
+    bit-exact, f64 means rtol 1e-12 and f32 means rtol 1e-6 against numpy,
+    ragged last column chunk included."""
+    from cubed_amd import _native as nat
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    if not even:
+        monkeypatch.setattr(L, "MODE_STREAM_EVEN", 0)
+    e = GpuDagExecutor("cuda:0")
+    spec = mkspec(e)
+    rng = np.random.default_rng(11)
+    xi = rng.integers(-2**40, 2**40, size=(1500, 19000), dtype=np.int64)
+    xf = rng.random((1500, 19000)) + 7.0
+    keep = []
+    a = cubed.from_array(xi, chunks=(500, 5000), spec=spec)
+    keep.append(xp.sum(a, axis=0))
+    np.testing.assert_array_equal(keep[-1].compute(), xi.sum(axis=0))
+    b = cubed.from_array(xf, chunks=(500, 5000), spec=spec)
+    keep.append(xp.mean(b, axis=0))
+    np.testing.assert_allclose(keep[-1].compute(), xf.mean(axis=0), rtol=1e-12, atol=0)
+    c = xp.astype(b, xp.float32)
+    keep.append(xp.mean(c, axis=0))
+    want32 = xf.astype(np.float32).astype(np.float64).mean(axis=0).astype(np.float32)
+    np.testing.assert_allclose(keep[-1].compute(), want32, rtol=1e-6, atol=0)
+    streams = [l for l in _fused_launches(e) if l.prog.mode & L.MODE_STREAM and l.prog.nfields]
+    assert streams
+    lib = nat.lib()
+    for l in streams:
+        assert bool(l.prog.mode & 256) == even
+        # the launch split (a workspace) -- balanced or not
+        assert lib.cubed_fused_workspace_bytes(l.prog, l.ntasks, l.max_kept, l.max_red) > 0
+
+
 def test_mean_of_unmaterialised_random(ex):
     """random -> elementwise -> mean with nothing materialised: the Philox
     map is fused into the reduction's first pass (one stream key per

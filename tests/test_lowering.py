@@ -722,3 +722,80 @@ def test_var_triple_rejected_when_malformed(built):
     h = ctypes.c_void_p()
     rc = nat.lib().cubed_fused_compile(ctypes.byref(P), nat.INCLUDE_DIRS.encode(), ctypes.byref(h))
     assert rc != 0 and b"triple" in nat.lib().cubed_last_error()
+
+
+def _balanced_runs(G, blocks, nru):
+    """stream_body's balanced split (kernels.h), restated: per workgroup g the
+    (column block c, rows [lo, hi), slot, contributors) segments of its run."""
+    Ut = blocks * nru
+
+    def owner(u):
+        return ((u + 1) * G - 1) // Ut
+    out = []
+    for g in range(G):
+        S0, S1 = g * Ut // G, (g + 1) * Ut // G
+        u = S0
+        while u < S1:
+            c = u // nru
+            lo = u - c * nru
+            hi = min(S1 - c * nru, nru)
+            first, last = owner(c * nru), owner((c + 1) * nru - 1)
+            out.append((g, c, lo, hi, g - first, last - first + 1))
+            u = c * nru + hi
+    return out
+
+
+@pytest.mark.parametrize("G,blocks,nru", [(256, 49, 7000), (256, 49, 50000), (256, 20, 20000),
+                                          (256, 3, 1000), (248, 7, 777), (8, 1, 513)])
+def test_balanced_split_partition(G, blocks, nru):
+    """Every (block, row) unit is covered once; each block's contributors take
+    slots 0..nsp-1 in row order, all agreeing on nsp, and nsp never exceeds
+    the host's slot count (fused.hip plan_launch); runs differ by <= 1 row."""
+    segs = _balanced_runs(G, blocks, nru)
+    minlen = blocks * nru // G
+    K = (nru + minlen - 1) // minlen + 1
+    per_block = {}
+    for g, c, lo, hi, slot, nsp in segs:
+        assert 0 <= lo < hi <= nru and 0 <= slot < nsp <= K
+        per_block.setdefault(c, []).append((lo, hi, slot, nsp))
+    assert sorted(per_block) == list(range(blocks))
+    for c, lst in per_block.items():
+        lst.sort()
+        assert lst[0][0] == 0 and lst[-1][1] == nru
+        assert all(a[1] == b[0] for a, b in zip(lst, lst[1:]))
+        assert [x[2] for x in lst] == list(range(len(lst)))
+        assert {x[3] for x in lst} == {len(lst)}
+    run = {}
+    for g, c, lo, hi, *_ in segs:
+        run[g] = run.get(g, 0) + hi - lo
+    assert max(run.values()) - min(run.values()) <= 1 and len(run) == G
+
+
+def test_even_streams_mark_uniform_tasks(built, dry):
+    """Tasks of one reduced extent carry CUBED_MODE_STREAM_EVEN, and the
+    library sizes a balanced split's workspace for its slot count."""
+    from cubed_amd import _native as nat
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(1)
+    u = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=dry, array_names=[u.name, v.name])
+    dry.launched.clear()
+    m = xp.mean(u * v, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    (L,) = _fused(dry)
+    P = L.prog
+    assert P.mode & Lw.MODE_STREAM_EVEN
+    # the per-rank share of config 3: one task, 50000 kept, 7000 rows
+    P.mode &= ~(Lw.MODE_STREAM_W2 | Lw.MODE_STREAM_W4)
+    lib = nat.lib()
+    nf, ntasks, kept, red = P.nfields, 1, 50000, 7000
+    bpt = -(-(-(-kept // 256) * 64) // 256)  # column blocks: 64 lanes x 4 elements x 4 waves
+    even = lib.cubed_fused_workspace_bytes(P, ntasks, kept, red)
+    P.mode &= ~Lw.MODE_STREAM_EVEN
+    plain = lib.cubed_fused_workspace_bytes(P, ntasks, kept, red)
+    minlen = ntasks * bpt * red // 256
+    K = -(-red // minlen) + 1
+    assert even == K * ntasks * kept * nf * 8 + ntasks * bpt * 4
+    assert plain == 5 * ntasks * kept * nf * 8 + ntasks * bpt * 4  # uniform split: 49 x 5 workgroups
