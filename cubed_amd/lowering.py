@@ -1046,7 +1046,7 @@ class Lowerer:
                 rows = layout.rows
         if stream:
             P.mode |= MODE_STREAM | _stream_groups_mode(P, len(rows), layout.max_kept)
-            if P.nfields > 0 and len({_red_extent(r, layout) for r in rows}) == 1:
+            if STREAM_EVEN and P.nfields > 0 and len({_red_extent(r, layout) for r in rows}) == 1:
                 # every task the same reduced extent: a split launch may cut
                 # the (task, column block, row) units into equal runs per
                 # workgroup (stream_body's balanced split)
@@ -1689,6 +1689,14 @@ MODE_STREAM_W2 = 32  # include/cubed_amd.h CUBED_MODE_STREAM_W2
 MODE_STREAM_W4 = 64  # include/cubed_amd.h CUBED_MODE_STREAM_W4
 MODE_HOST_COUNT = 128  # include/cubed_amd.h CUBED_MODE_HOST_COUNT
 MODE_STREAM_EVEN = 256  # include/cubed_amd.h CUBED_MODE_STREAM_EVEN
+# The balanced split keeps all 256 CUs streaming where the uniform split of
+# 49 column blocks x 5 leaves 11 idle, but measured 4-8 % SLOWER on every
+# split workload (per-rank share 0.221 vs 0.203 ms, config 1 0.464 vs 0.456,
+# elided rechunk + mean 1.459 vs 1.404; profiles/r04_even_ab.log): 245 CUs
+# already saturate HBM, and 256 runs at 256 different row offsets read HBM
+# less sequentially than 49 column blocks x 5 row bands.  Off by default;
+# probes and tests set it.
+STREAM_EVEN = False
 
 
 def _red_extent(row, layout) -> int:

@@ -250,8 +250,7 @@ def test_balanced_split_streams(gpu_executor, monkeypatch, even):
     from cubed_amd import _native as nat
     from cubed_amd.runtime.executors.gpu import GpuDagExecutor
 
-    if not even:
-        monkeypatch.setattr(L, "MODE_STREAM_EVEN", 0)
+    monkeypatch.setattr(L, "STREAM_EVEN", even)
     e = GpuDagExecutor("cuda:0")
     spec = mkspec(e)
     rng = np.random.default_rng(11)

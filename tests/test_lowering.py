@@ -771,10 +771,13 @@ def test_balanced_split_partition(G, blocks, nru):
     assert max(run.values()) - min(run.values()) <= 1 and len(run) == G
 
 
-def test_even_streams_mark_uniform_tasks(built, dry):
-    """Tasks of one reduced extent carry CUBED_MODE_STREAM_EVEN, and the
-    library sizes a balanced split's workspace for its slot count."""
+def test_even_streams_mark_uniform_tasks(built, dry, monkeypatch):
+    """With the balanced split enabled (lowering.STREAM_EVEN, off by default)
+    tasks of one reduced extent carry CUBED_MODE_STREAM_EVEN, and the library
+    sizes a balanced split's workspace for its slot count."""
     from cubed_amd import _native as nat
+
+    monkeypatch.setattr(Lw, "STREAM_EVEN", True)
 
     spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
     random.seed(1)

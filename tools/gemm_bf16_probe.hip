@@ -5,6 +5,9 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude \
 //          -o tools/gemm_bf16_probe tools/gemm_bf16_probe.hip
 // Run:   tools/gemm_bf16_probe [reps]
+// (Rounds 2-3.  The library kernels gained a GemmGrid argument in round 4;
+// the experiment kernels here keep the 5-argument form, so this probe builds
+// against gemm_chain.hip as of commit 1cdef52^ -- its logs are in profiles/.)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

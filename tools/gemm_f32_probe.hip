@@ -33,7 +33,7 @@ __global__ void k_diff(const float* a, const float* b, int64_t n, float* out) {
   atomicMax((int*)out, __float_as_int(m));
 }
 
-typedef void (*kfn)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*);
+typedef void (*kfn)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*, GemmGrid);
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 1;
@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(v.f, grid, blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z);
+      hipLaunchKernelGGL(v.f, grid, blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z, GemmGrid{});
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));

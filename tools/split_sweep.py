@@ -77,6 +77,21 @@ def main():
             run("quad_means", GpuDagExecutor("cuda:0"), quad)
         Lw.FORCE_STREAM_W = None
 
+    if os.environ.get("SWEEP_EVEN_AB"):
+        # balanced split (CUBED_MODE_STREAM_EVEN) against the uniform split,
+        # interleaved twice, at the default target
+        import cubed_amd.lowering as Lw
+
+        for rep in range(2):
+            for even in (False, True):
+                tgt = f"{'even' if even else 'uniform'}{rep}"
+                Lw.STREAM_EVEN = even
+                run("share7000", GpuDagExecutor("cuda:0"), share(7000))
+                run("rehearsed_rank0_of_8", GpuDagExecutor("cuda:0", comm=LoopbackComm(0, 8)), share(50000))
+                run("config1", GpuDagExecutor("cuda:0"), config1, steps=10)
+                run("elided_full", GpuDagExecutor("cuda:0"), share(50000), steps=10)
+        Lw.STREAM_EVEN = False
+        targets = [t for t in targets if os.environ.get("SWEEP_TARGETS")]
     for tgt in targets:
         L.cubed_stream_split_target(tgt)
         run("share7000", GpuDagExecutor("cuda:0"), share(7000))
