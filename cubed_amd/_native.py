@@ -151,6 +151,9 @@ def lib():
     L.cubed_fused_finish.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                      c_void_p]
     L.cubed_fused_finish.restype = c_int
+    L.cubed_fused_finish_compiled.argtypes = [c_void_p, POINTER(Program), c_void_p, c_int64, c_int64,
+                                              c_void_p, c_void_p]
+    L.cubed_fused_finish_compiled.restype = c_int
     L.cubed_fused_finish_groups.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64,
                                             c_void_p, c_void_p, c_int64, c_void_p]
     L.cubed_fused_finish_groups.restype = c_int
@@ -196,7 +199,7 @@ EXPORTED_SYMBOLS = (
     "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_stream_split_target", "cubed_random_chunks",
     "cubed_copy_boxes", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
-    "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_combine_partials",
+    "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_fused_finish_compiled", "cubed_combine_partials",
     "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
     "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_zstd_decompress", "cubed_lz4_chunk_decompress", "cubed_gemm_chain", "cubed_gemm_chain_path",

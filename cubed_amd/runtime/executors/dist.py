@@ -235,10 +235,21 @@ class PartialsLaunch:
                                                    self.fused.ws.data_ptr(), stream),
                           "cubed_combine_partials")
         if self.finish_here:
-            nat.check(L.cubed_fused_finish(self.fused.prog, self.fused.d_prog.data_ptr(),
-                                           self.fused.table.data_ptr(), self.fused.ntasks,
-                                           self.fused.max_kept, self.fused.ws.data_ptr(), stream),
-                      "cubed_fused_finish")
+            fused_finish(self.fused, self.fused.table, self.fused.ntasks, self.fused.max_kept,
+                         self.fused.ws, stream)
+
+
+def fused_finish(F, table, ntasks, max_kept, partials, stream):
+    """The epilogue over combined SoA partials of ``F``'s program: the JIT
+    module's specialised finish when the program was compiled, else the
+    interpreted kernel (CUBED_AMD_JIT=0)."""
+    L = nat.lib()
+    if F.handle is not None:
+        nat.check(L.cubed_fused_finish_compiled(F.handle, F.prog, table.data_ptr(), ntasks, max_kept,
+                                                partials.data_ptr(), stream), "cubed_fused_finish_compiled")
+    else:
+        nat.check(L.cubed_fused_finish(F.prog, F.d_prog.data_ptr(), table.data_ptr(), ntasks, max_kept,
+                                       partials.data_ptr(), stream), "cubed_fused_finish")
 
 
 def gather_distributed(arr: DeviceArray) -> np.ndarray:
@@ -370,6 +381,4 @@ class DistPiecesLaunch:
                                                    comm.world, self.n, self.gsoa.data_ptr(), stream),
                           "cubed_combine_partials")
         if self.finish_here:
-            nat.check(L.cubed_fused_finish(F.prog, F.d_prog.data_ptr(), self.group_table.data_ptr(),
-                                           self.ngroups, self.mko, self.gsoa.data_ptr(), stream),
-                      "cubed_fused_finish")
+            fused_finish(F, self.group_table, self.ngroups, self.mko, self.gsoa, stream)

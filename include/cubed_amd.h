@@ -272,6 +272,10 @@ int64_t cubed_fused_workspace_bytes(const cubed_program_t* prog, int64_t ntasks,
 int cubed_fused_finish(const cubed_program_t* prog, const cubed_program_t* d_prog,
                        const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                        const void* d_partials, void* stream);
+/* The same finish, specialised: the JIT module of `handle` (cubed_fused_compile
+ * of a CUBED_MODE_PARTIALS program) carries it; CUBED_E_JIT if it does not. */
+int cubed_fused_finish_compiled(void* handle, const cubed_program_t* prog, const cubed_task_t* d_tasks,
+                                int64_t ntasks, int64_t max_kept, const void* d_partials, void* stream);
 /* Grouped finish (partials mode): tasks [group_start[g], group_start[g+1]) are
  * pieces of ONE output box -- a task split where its inputs straddle source
  * chunks along a reduced dim (e.g. the a[1:] regions of index/map_direct,

@@ -802,3 +802,27 @@ def test_even_streams_mark_uniform_tasks(built, dry, monkeypatch):
     K = -(-red // minlen) + 1
     assert even == K * ntasks * kept * nf * 8 + ntasks * bpt * 4
     assert plain == 5 * ntasks * kept * nf * 8 + ntasks * bpt * 4  # uniform split: 49 x 5 workgroups
+
+
+def test_partials_programs_compile_a_specialised_finish(built, dry):
+    """A partials-mode program's JIT module carries the SoA finish
+    (cubed_fused_finish_compiled) next to its main / split kernels; other
+    programs do not."""
+    import ctypes as C
+
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+    random.seed(1)
+    u = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((200, 16, 32), chunks=(10, 16, 32), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=dry, array_names=[u.name, v.name])
+    dry.launched.clear()
+    m = xp.mean(u * v, axis=0)
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    (L,) = _fused(dry)
+    assert "finish_soa_body" not in nat.program_source(L.handle)
+    P = nat.Program()
+    C.memmove(C.addressof(P), C.addressof(L.prog), C.sizeof(P))
+    P.mode |= Lw.MODE_PARTIALS
+    src = nat.program_source(nat.compile_program(P))
+    assert "_partials_finish(" in src and "cubed::finish_soa_body(JP," in src
+    assert "cubed_fused_finish_compiled" in nat.EXPORTED_SYMBOLS
