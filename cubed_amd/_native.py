@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 12  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 13  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -161,9 +161,10 @@ def lib():
                                        c_void_p, c_int64, c_int64, c_void_p, c_void_p]
     L.cubed_combine_groups.restype = c_int
     L.cubed_fold_groups.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
-                                    c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]
+                                    c_void_p, c_int64, c_void_p, c_int64, c_void_p, POINTER(Program),
+                                    c_void_p, c_void_p, c_void_p]
     L.cubed_fold_groups.restype = c_int
-    L.cubed_fold_groups_splits.argtypes = [c_int64, c_int64]
+    L.cubed_fold_groups_splits.argtypes = [c_int64, c_int64, c_int64]
     L.cubed_fold_groups_splits.restype = c_int64
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
                                          c_void_p]

@@ -83,21 +83,18 @@ __global__ __launch_bounds__(kBlock) void k_combine_groups(
 __global__ __launch_bounds__(kBlock) void k_fold_groups(
     const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
-    Acc* __restrict__ out, int kd0, int kd1) {
-  fold_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1);
+    Acc* __restrict__ out, int kd0, int kd1, const cubed_program_t* __restrict__ Pfin,
+    const cubed_task_t* __restrict__ fin_tasks) {
+  fold_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1, Pfin, fin_tasks);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fold_groups_split(
     const cubed_program_t* __restrict__ Pd, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
-    int64_t nsplit, Acc* __restrict__ out_split, int kd0, int kd1) {
-  fold_groups_split_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, nsplit, out_split, kd0, kd1);
-}
-
-__global__ __launch_bounds__(kBlock) void k_fold_splits(const cubed_program_t* __restrict__ Pd,
-                                                        const Acc* __restrict__ in_split, int64_t ngroups,
-                                                        int64_t nsplit, Acc* __restrict__ out) {
-  fold_splits_body(*Pd, in_split, ngroups, nsplit, out);
+    int64_t nsplit, Acc* __restrict__ out_split, Acc* __restrict__ out, int kd0, int kd1,
+    const cubed_program_t* __restrict__ Pfin, const cubed_task_t* __restrict__ fin_tasks) {
+  fold_groups_split_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, nsplit, out_split, out, kd0, kd1, Pfin,
+                         fin_tasks);
 }
 
 __global__ __launch_bounds__(kBlock) void k_combine_parts(
@@ -448,38 +445,47 @@ extern "C" int cubed_combine_groups(const cubed_program_t* prog, const cubed_pro
   return 0;
 }
 
-extern "C" int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group) {
-  // fewer groups than ~2 per CU: spread each group's rows over workgroups
-  if (ngroups <= 0 || max_rows_per_group <= 1 || ngroups >= 512) return 1;
-  int64_t s = (1024 + ngroups - 1) / ngroups;
-  return s < max_rows_per_group ? s : max_rows_per_group;
+extern "C" int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group, int64_t max_kept) {
+  // fewer groups than ~2 per CU: cut each group's rows x max_kept SoA
+  // entries into runs of >= 2048 (8 per thread), toward 1024 workgroups
+  if (ngroups <= 0 || max_rows_per_group < 1 || max_kept < 1 || ngroups >= 512) return 1;
+  const int64_t per_group = (1024 + ngroups - 1) / ngroups;
+  const int64_t by_size = max_rows_per_group * max_kept / 2048;
+  const int64_t s = per_group < by_size ? per_group : by_size;
+  return s > 1 ? s : 1;
 }
 
 extern "C" int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
                                  const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                                  const void* d_row_partials, const int64_t* d_group_start,
                                  int64_t ngroups, void* d_group_partials, int64_t nsplit,
-                                 void* d_split_ws, void* stream) {
+                                 void* d_split_ws, const cubed_program_t* fin, const cubed_program_t* d_fin,
+                                 const cubed_task_t* d_fin_tasks, void* stream) {
   if (!prog || !d_prog || !d_row_partials || !d_group_start || !d_group_partials ||
-      (!d_tasks && ntasks > 0) || (nsplit > 1 && !d_split_ws)) {
+      (!d_tasks && ntasks > 0) || (nsplit > 1 && !d_split_ws) || (!fin != !d_fin) || (fin && !d_fin_tasks)) {
     set_err("cubed_fold_groups: null argument");
     return CUBED_E_ARG;
   }
   if (ngroups == 0) return 0;
   if (int rc = check_program(*prog)) return rc;
+  if (fin) {
+    if (int rc = check_program(*fin)) return rc;
+    if (fin->nfields != prog->nfields || fin->nred != fin->ndim) {
+      set_err("cubed_fold_groups: the epilogue program must reduce every dim over the same fields");
+      return CUBED_E_ARG;
+    }
+  }
   if (prog->nfields == 0 || max_kept <= 0 || ngroups > ntasks || nsplit < 1) { set_err("cubed_fold_groups: bad shape"); return CUBED_E_ARG; }
   int kd0, kd1;
   kept_dims(*prog, kd0, kd1);
   if (nsplit > 1) {
     hipLaunchKernelGGL(k_fold_groups_split, grid_of(ngroups * nsplit), dim3(kBlock), 0, (hipStream_t)stream,
                        d_prog, d_tasks, ntasks, max_kept, (const Acc*)d_row_partials, d_group_start, ngroups,
-                       nsplit, (Acc*)d_split_ws, kd0, kd1);
-    hipLaunchKernelGGL(k_fold_splits, grid_of(ngroups), dim3(kBlock), 0, (hipStream_t)stream, d_prog,
-                       (const Acc*)d_split_ws, ngroups, nsplit, (Acc*)d_group_partials);
+                       nsplit, (Acc*)d_split_ws, (Acc*)d_group_partials, kd0, kd1, d_fin, d_fin_tasks);
   } else {
     hipLaunchKernelGGL(k_fold_groups, grid_of(ngroups), dim3(kBlock), 0, (hipStream_t)stream, d_prog, d_tasks,
                        ntasks, max_kept, (const Acc*)d_row_partials, d_group_start, ngroups,
-                       (Acc*)d_group_partials, kd0, kd1);
+                       (Acc*)d_group_partials, kd0, kd1, d_fin, d_fin_tasks);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }

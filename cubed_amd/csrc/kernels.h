@@ -514,11 +514,22 @@ CUBED_DEV void combine_groups_body(
   for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * no + i] = x[f];
 }
 
+// Split accumulators shared between workgroups (a column block's splits, a
+// fold group's runs): agent-scope relaxed atomics, i.e. stores written
+// through to memory and loads that miss the (per-XCD, non-coherent) L2.
+CUBED_DEV void store_through(Acc* p, Acc v) {
+  __hip_atomic_store(&p->i, v.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+CUBED_DEV Acc load_through(const Acc* p) {
+  Acc v;
+  v.i = __hip_atomic_load(&p->i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
 // Workgroup fold of per-thread accumulators (64-wide shuffle tree, then the
-// waves in order through LDS); thread 0 stores out[f * stride + idx].
-CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIELDS],
-                                Acc (&red)[kBlock / 64][CUBED_MAX_FIELDS], Acc* __restrict__ out,
-                                int64_t stride, int64_t idx) {
+// waves in order through LDS); the result lands in thread 0's x.
+CUBED_DEV void block_fold(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIELDS],
+                          Acc (&red)[kBlock / 64][CUBED_MAX_FIELDS], Acc (&x)[CUBED_MAX_FIELDS]) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     Acc b[CUBED_MAX_FIELDS];
@@ -533,11 +544,25 @@ CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIE
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    Acc x[CUBED_MAX_FIELDS];
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f) x[f] = red[0][f];
     for (int w = 1; w < kBlock / 64; ++w) fields_combine(x, red[w], P);
-    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * stride + idx] = x[f];
+  }
+}
+
+// A fold group's result (thread 0): stored to out[f][g] and, with an
+// epilogue program (the lifted reduction's, nred = ndim), finished into the
+// group's output (fin_tasks[g], one element) right here.
+CUBED_DEV void fold_group_done(const cubed_program_t& P, Acc (&x)[CUBED_MAX_FIELDS], Acc* __restrict__ out,
+                               int64_t ngroups, int64_t g, const cubed_program_t* __restrict__ Pfin,
+                               const cubed_task_t* __restrict__ fin_tasks) {
+  for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * ngroups + g] = x[f];
+  if (Pfin) {
+    Acc fin[CUBED_MAX_FIELDS][1];
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f) fin[f][0] = x[f];
+    int64_t ooff[CUBED_MAX_OUTS] = {};
+    finish<1>(*Pfin, fin_tasks + g, fin, ooff);
   }
 }
 
@@ -549,7 +574,8 @@ CUBED_DEV void block_fold_store(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIE
 CUBED_DEV void fold_groups_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
-    Acc* __restrict__ out, int kd0, int kd1) {
+    Acc* __restrict__ out, int kd0, int kd1, const cubed_program_t* __restrict__ Pfin,
+    const cubed_task_t* __restrict__ fin_tasks) {
   __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
   const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   if (g >= ngroups) return;
@@ -567,53 +593,75 @@ CUBED_DEV void fold_groups_body(
       fields_combine(a, y, P);
     }
   }
-  block_fold_store(P, a, red, out, ngroups, g);
+  Acc x[CUBED_MAX_FIELDS];
+  block_fold(P, a, red, x);
+  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin, fin_tasks);
 }
 
-// Split fold for few groups of many rows (e.g. one scalar over 720 source
-// chunks): workgroup b = (group g, split s) folds rows gs[g] + s, + nsplit,
-// ... into out_split[f][b]; fold_splits_body then folds the nsplit values of
-// each group.  Same combine operators, a fixed (shape-determined) order.
+// Split fold for few groups of many elements (e.g. one scalar over 720
+// source chunks x 720000 per-element partials): a group's SoA entries are the
+// flat run [gs[g], gs[g+1]) x max_kept (kept index < the task's extent), cut
+// into nsplit equal runs; workgroup (g, s) folds run s and leaves its result
+// in out_split[f][g][s] (write-through), and the LAST of the group's nsplit
+// workgroups to arrive (arrival counter per group, self-resetting) folds the
+// nsplit results and finishes the group: one launch.  A fixed
+// (shape-determined) order, so deterministic.
 CUBED_DEV void fold_groups_split_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
-    int64_t nsplit, Acc* __restrict__ out_split, int kd0, int kd1) {
+    int64_t nsplit, Acc* __restrict__ out_split, Acc* __restrict__ out, int kd0, int kd1,
+    const cubed_program_t* __restrict__ Pfin, const cubed_task_t* __restrict__ fin_tasks) {
   __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
+  __shared__ int last_arrival;
   const int64_t b = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   if (b >= ngroups * nsplit) return;
   const int64_t g = b / nsplit, sp = b - g * nsplit;
   const int64_t n = ntasks * max_kept;
+  const int64_t base = gs[g] * max_kept, E = (gs[g + 1] - gs[g]) * max_kept;
+  const int64_t e0 = base + E * sp / nsplit, e1 = base + E * (sp + 1) / nsplit;
   Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
-  for (int64_t t = gs[g] + sp; t < gs[g + 1]; t += nsplit) {
+  for (int64_t t = e0 / max_kept; t * max_kept < e1; ++t) {
     const cubed_task_t* __restrict__ T = tasks + t;
     int64_t nk = 1;
     for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
-    for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
+    const int64_t k0 = e0 > t * max_kept ? e0 - t * max_kept : 0;
+    const int64_t k1r = e1 - t * max_kept, k1 = k1r < nk ? k1r : nk;
+    for (int64_t k = k0 + threadIdx.x; k < k1; k += kBlock) {
       Acc y[CUBED_MAX_FIELDS];
       soa_load(P, soa, n, t * max_kept + k, y);
       fields_combine(a, y, P);
     }
   }
-  block_fold_store(P, a, red, out_split, ngroups * nsplit, b);
-}
-
-CUBED_DEV void fold_splits_body(const cubed_program_t& P, const Acc* __restrict__ in_split,
-                                int64_t ngroups, int64_t nsplit, Acc* __restrict__ out) {
-  __shared__ Acc red[kBlock / 64][CUBED_MAX_FIELDS];
-  const int64_t g = blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  if (g >= ngroups) return;
+  Acc x[CUBED_MAX_FIELDS];
+  block_fold(P, a, red, x);
   const int64_t ns = ngroups * nsplit;
-  Acc a[CUBED_MAX_FIELDS];
+  uint32_t* cnt = (uint32_t*)(out_split + (int64_t)P.nfields * ns);
+  if (threadIdx.x == 0) {
+    for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) store_through(&out_split[f * ns + b], x[f]);
+    // the stores complete before the arrival counts (MI355X_MICROARCH.md
+    // "Correctness boundaries": write-through stores, drained, then the count)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(cnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int lastv = old == (uint32_t)(nsplit - 1);
+    if (lastv) __hip_atomic_store(cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_arrival = lastv;
+  }
+  __syncthreads();
+  if (!last_arrival) return;
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
   for (int64_t s = threadIdx.x; s < nsplit; s += kBlock) {
     Acc y[CUBED_MAX_FIELDS];
-    soa_load(P, in_split, ns, g * nsplit + s, y);
+#pragma unroll
+    for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+      y[f] = f < P.nfields ? load_through(&out_split[f * ns + g * nsplit + s]) : acc_init(P.field_rop[f], P.field_acc[f]);
     fields_combine(a, y, P);
   }
-  block_fold_store(P, a, red, out, ngroups, g);
+  __syncthreads();  // red is reused
+  block_fold(P, a, red, x);
+  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin, fin_tasks);
 }
 
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in
@@ -816,18 +864,6 @@ CUBED_DEV void stream_rows(Acc (&acc)[W][CUBED_MAX_FIELDS][4], Regs<V, 4>& regs,
 #pragma unroll
     for (int l = 0; l < NL; ++l) p[l] += rs[l];
   }
-}
-
-// Split accumulators shared between the workgroups of one column block:
-// agent-scope relaxed atomics, i.e. stores written through to memory and
-// loads that miss the (per-XCD, non-coherent) L2.
-CUBED_DEV void store_through(Acc* p, Acc v) {
-  __hip_atomic_store(&p->i, v.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-CUBED_DEV Acc load_through(const Acc* p) {
-  Acc v;
-  v.i = __hip_atomic_load(&p->i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return v;
 }
 
 // W: kept VEC groups per thread (stream_groups()).  The 64 lanes of a wave

@@ -699,11 +699,14 @@ class FusedLaunch:
             raw = np.frombuffer(ctypes.string_at(ctypes.addressof(prog_fin), ctypes.sizeof(prog_fin)),
                                 dtype=np.uint8)
             rows_per_group = int(np.max(np.diff(group_start))) if self.ngroups else 1
-            self.fold_split = int(nat.lib().cubed_fold_groups_splits(self.ngroups, rows_per_group))
+            self.fold_split = int(nat.lib().cubed_fold_groups_splits(self.ngroups, rows_per_group,
+                                                                     self.max_kept))
             split_ws = None
             if self.fold_split > 1:
-                split_ws = torch.empty(8 * self.prog.nfields * self.ngroups * self.fold_split,
-                                       dtype=torch.uint8, device=self.d_prog.device)
+                # split accumulators + one arrival counter per group, zeroed
+                # once (the kernel leaves the counters at zero)
+                split_ws = torch.zeros(8 * self.prog.nfields * self.ngroups * self.fold_split
+                                       + 4 * self.ngroups, dtype=torch.uint8, device=self.d_prog.device)
             self.fold = (prog_fin, torch.from_numpy(raw.copy()).to(self.d_prog.device), table,
                          torch.empty(max(8 * self.prog.nfields * self.ngroups, 16), dtype=torch.uint8,
                                      device=self.d_prog.device), split_ws)
@@ -713,14 +716,15 @@ class FusedLaunch:
         if self.fold is not None:
             prog_fin, d_fin, table, gsoa, split_ws = self.fold
             L = nat.lib()
+            # the fold and the epilogue in one launch (the group's last
+            # workgroup finishes it)
             nat.check(L.cubed_fold_groups(self.prog, self.d_prog.data_ptr(), self.table.data_ptr(),
                                           self.ntasks, self.max_kept, self.ws.data_ptr(),
                                           self.groups.data_ptr(), self.ngroups, gsoa.data_ptr(),
                                           self.fold_split,
-                                          split_ws.data_ptr() if split_ws is not None else None, stream),
+                                          split_ws.data_ptr() if split_ws is not None else None,
+                                          prog_fin, d_fin.data_ptr(), table.data_ptr(), stream),
                       "cubed_fold_groups")
-            nat.check(L.cubed_fused_finish(prog_fin, d_fin.data_ptr(), table.data_ptr(), self.ngroups, 1,
-                                           gsoa.data_ptr(), stream), "cubed_fused_finish")
         elif self.groups is not None:
             nat.check(nat.lib().cubed_fused_finish_groups(
                 self.prog, self.d_prog.data_ptr(), self.table.data_ptr(), self.ntasks, self.max_kept,

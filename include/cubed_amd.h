@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 12
+#define CUBED_ABI_VERSION 13
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -299,17 +299,22 @@ int cubed_combine_groups(const cubed_program_t* prog, const cubed_program_t* d_p
 /* Fold each group's rows AND their kept elements into one accumulator per
  * field: d_group_partials[f][g].  For full reductions run "lifted" (the
  * innermost reduced dims walked as kept dims so every lane streams, e.g.
- * mean(a[1:] * x + b[1:] * y) of the vorticity example); the epilogue then
- * runs through cubed_fused_finish with the program's nred = ndim. */
+ * mean(a[1:] * x + b[1:] * y) of the vorticity example).  With an epilogue
+ * program (fin / d_fin: the same program with nred = ndim) the kernel also
+ * finishes each group into d_fin_tasks[g] (one launch); without it the caller
+ * runs cubed_fused_finish over d_group_partials.  ABI 13. */
 int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog,
                       const cubed_task_t* d_tasks, int64_t ntasks, int64_t max_kept,
                       const void* d_row_partials, const int64_t* d_group_start,
                       int64_t ngroups, void* d_group_partials, int64_t nsplit,
-                      void* d_split_ws, void* stream);
-/* Splits per group cubed_fold_groups should use (few groups of many rows:
- * each group's rows spread over nsplit workgroups, then folded); d_split_ws
- * then holds nfields x ngroups x nsplit 8-byte accumulators. */
-int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group);
+                      void* d_split_ws, const cubed_program_t* fin, const cubed_program_t* d_fin,
+                      const cubed_task_t* d_fin_tasks, void* stream);
+/* Splits per group cubed_fold_groups should use (few groups of many
+ * elements: each group's rows x max_kept SoA entries cut into nsplit equal
+ * runs, the last run to finish folds them); d_split_ws then holds
+ * nfields x ngroups x nsplit 8-byte accumulators followed by ngroups uint32
+ * arrival counters -- zero it once, the kernel leaves the counters at zero. */
+int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group, int64_t max_kept);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);
