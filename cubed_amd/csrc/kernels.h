@@ -553,8 +553,18 @@ CUBED_DEV void block_fold(const cubed_program_t& P, Acc (&a)[CUBED_MAX_FIELDS],
 // A fold group's result (thread 0): stored to out[f][g] and, with an
 // epilogue program (the lifted reduction's, nred = ndim), finished into the
 // group's output (fin_tasks[g], one element) right here.
+// The epilogue program is first copied into LDS by the whole workgroup (one
+// round trip): the interpreter's chain of dependent program reads then costs
+// LDS latency instead of a global-memory trip each (the separate finish
+// launch this replaces took 7 us for ONE element).
+CUBED_DEV void stage_program(cubed_program_t& dst, const cubed_program_t* __restrict__ src) {
+  static_assert(sizeof(cubed_program_t) % 16 == 0, "program struct in 16-byte units");
+  for (int i = threadIdx.x; i < (int)(sizeof(cubed_program_t) / 16); i += kBlock)
+    reinterpret_cast<uint4*>(&dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  __syncthreads();
+}
 CUBED_DEV void fold_group_done(const cubed_program_t& P, Acc (&x)[CUBED_MAX_FIELDS], Acc* __restrict__ out,
-                               int64_t ngroups, int64_t g, const cubed_program_t* __restrict__ Pfin,
+                               int64_t ngroups, int64_t g, const cubed_program_t* Pfin,
                                const cubed_task_t* __restrict__ fin_tasks) {
   for (int f = 0; f < P.nfields && f < CUBED_MAX_FIELDS; ++f) out[f * ngroups + g] = x[f];
   if (Pfin) {
@@ -583,24 +593,23 @@ CUBED_DEV void fold_groups_body(
   Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
-  for (int64_t t = gs[g]; t < gs[g + 1]; ++t) {
-    const cubed_task_t* __restrict__ T = tasks + t;
-    int64_t nk = 1;
-    for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
-    for (int64_t k = threadIdx.x; k < nk; k += kBlock) {
-      Acc y[CUBED_MAX_FIELDS];
-      soa_load(P, soa, n, t * max_kept + k, y);
-      fields_combine(a, y, P);
-    }
+  // the group's rows are one flat run of SoA entries: partials mode leaves
+  // the identity past every task's kept extent (collect_body, stream_body)
+  for (int64_t e = gs[g] * max_kept + threadIdx.x; e < gs[g + 1] * max_kept; e += kBlock) {
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, soa, n, e, y);
+    fields_combine(a, y, P);
   }
   Acc x[CUBED_MAX_FIELDS];
   block_fold(P, a, red, x);
-  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin, fin_tasks);
+  __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
+  if (Pfin) stage_program(pfin, Pfin);
+  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
 }
 
 // Split fold for few groups of many elements (e.g. one scalar over 720
-// source chunks x 720000 per-element partials): a group's SoA entries are the
-// flat run [gs[g], gs[g+1]) x max_kept (kept index < the task's extent), cut
+// source chunks' per-element partials): a group's SoA entries are the flat
+// run [gs[g], gs[g+1]) x max_kept, cut
 // into nsplit equal runs; workgroup (g, s) folds run s and leaves its result
 // in out_split[f][g][s] (write-through), and the LAST of the group's nsplit
 // workgroups to arrive (arrival counter per group, self-resetting) folds the
@@ -622,17 +631,11 @@ CUBED_DEV void fold_groups_split_body(
   Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
-  for (int64_t t = e0 / max_kept; t * max_kept < e1; ++t) {
-    const cubed_task_t* __restrict__ T = tasks + t;
-    int64_t nk = 1;
-    for (int d = kd0; d < kd1; ++d) nk *= T->extent[d];
-    const int64_t k0 = e0 > t * max_kept ? e0 - t * max_kept : 0;
-    const int64_t k1r = e1 - t * max_kept, k1 = k1r < nk ? k1r : nk;
-    for (int64_t k = k0 + threadIdx.x; k < k1; k += kBlock) {
-      Acc y[CUBED_MAX_FIELDS];
-      soa_load(P, soa, n, t * max_kept + k, y);
-      fields_combine(a, y, P);
-    }
+  // (a flat run: the identity past every task's kept extent, see above)
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, soa, n, e, y);
+    fields_combine(a, y, P);
   }
   Acc x[CUBED_MAX_FIELDS];
   block_fold(P, a, red, x);
@@ -661,7 +664,9 @@ CUBED_DEV void fold_groups_split_body(
   }
   __syncthreads();  // red is reused
   block_fold(P, a, red, x);
-  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin, fin_tasks);
+  __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
+  if (Pfin) stage_program(pfin, Pfin);
+  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
 }
 
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in
