@@ -151,6 +151,8 @@ def lib():
     L.cubed_fused_finish.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                      c_void_p]
     L.cubed_fused_finish.restype = c_int
+    L.cubed_stream_force_split.argtypes = [c_int64]
+    L.cubed_stream_force_split.restype = c_int64
     L.cubed_fused_finish_compiled.argtypes = [c_void_p, POINTER(Program), c_void_p, c_int64, c_int64,
                                               c_void_p, c_void_p]
     L.cubed_fused_finish_compiled.restype = c_int
@@ -197,7 +199,7 @@ def check(rc: int, what: str):
 
 
 EXPORTED_SYMBOLS = (
-    "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_stream_split_target", "cubed_random_chunks",
+    "cubed_fused_chunks", "cubed_fused_workspace_bytes", "cubed_stream_split_target", "cubed_stream_force_split", "cubed_random_chunks",
     "cubed_copy_boxes", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_fused_finish_compiled", "cubed_combine_partials",

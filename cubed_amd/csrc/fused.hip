@@ -170,6 +170,7 @@ int stream_groups(const cubed_program_t& P) {
 // or 160 (not whole rounds of 256) slower than either neighbour
 // (profiles/r04_split_sweep.log).
 static int64_t g_stream_target = 256;  // cubed_stream_split_target() (probes)
+static int64_t g_stream_force_split = 0;  // cubed_stream_force_split() (probes: split full grids too)
 
 LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kept,
                               int64_t max_red, int stream_w) {
@@ -196,6 +197,8 @@ LaunchPlan plan_launch(const cubed_program_t* P, int64_t ntasks, int64_t max_kep
     const int64_t inflight = (int64_t)kBlock * stream_unroll(isz, P->nleaves) * P->nleaves * W * 4 * isz;
     if (P->nfields > 0 && base * inflight < (int64_t)256 * 96 * 1024 && max_red >= 64)
       L.nsplit = (int32_t)choose_split(base, max_red / 16, g_stream_target);
+    else if (P->nfields > 0 && g_stream_force_split > 1 && max_red >= 16 * g_stream_force_split)
+      L.nsplit = (int32_t)g_stream_force_split;  // probes only (cubed_stream_force_split)
     // a multiple of 8 workgroups (the surplus exits at once): stream_body
     // maps them to XCD-contiguous runs
     L.blocks = (ntasks * L.nsplit * L.bpt + 7) / 8 * 8;
@@ -505,6 +508,12 @@ extern "C" int cubed_combine_partials(const cubed_program_t* prog, const cubed_p
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { set_err(hipGetErrorString(e)); return (int)e; }
   return 0;
+}
+
+extern "C" int64_t cubed_stream_force_split(int64_t nsplit) {
+  const int64_t prev = g_stream_force_split;
+  if (nsplit >= 0) g_stream_force_split = nsplit;
+  return prev;
 }
 
 extern "C" int64_t cubed_stream_split_target(int64_t workgroups) {

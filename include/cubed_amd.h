@@ -248,6 +248,9 @@ int64_t cubed_fused_code_bytes(const void* handle);
  * CU).  Process-wide tuning hook for probes (tools/); workgroups <= 0 only
  * queries.  Returns the previous value. */
 int64_t cubed_stream_split_target(int64_t workgroups);
+/* Probe hook: split streaming reductions whose grid already fills the chip
+ * into nsplit row ranges too (0 = off, the default; < 0 queries). */
+int64_t cubed_stream_force_split(int64_t nsplit);
 
 /* Workspace the call above needs (split reductions keep partial
  * accumulators there).  Pure host function. */

@@ -77,6 +77,21 @@ def main():
             run("quad_means", GpuDagExecutor("cuda:0"), quad)
         Lw.FORCE_STREAM_W = None
 
+    if os.environ.get("SWEEP_QUAD_SPLIT"):
+        # quad-means (grid already fills the chip: unsplit by default) with
+        # its time range forced into 2-4 splits folded in-kernel, at W = 1 / 2
+        import cubed_amd.lowering as Lw
+
+        for rep in range(2):
+            for w in (2, 1):
+                for ns in (0, 2, 3, 4):
+                    tgt = f"W{w}_split{ns}_{rep}"
+                    Lw.FORCE_STREAM_W = w
+                    L.cubed_stream_force_split(ns)
+                    run("quad_means", GpuDagExecutor("cuda:0"), quad)
+        L.cubed_stream_force_split(0)
+        Lw.FORCE_STREAM_W = None
+        targets = []
     if os.environ.get("SWEEP_EVEN_AB"):
         # balanced split (CUBED_MODE_STREAM_EVEN) against the uniform split,
         # interleaved twice, at the default target
