@@ -45,6 +45,17 @@ class Comm:
         self.world = dist.get_world_size(group)
         self.backend = str(dist.get_backend(group)).lower()
         self.staged = self.backend == "gloo"
+        # control-plane agreements (all_ok) go over a host-side gloo group:
+        # a device all-reduce + .item() would wait for every kernel queued on
+        # the stream, serialising the first step of each new plan across the
+        # ranks.  Created here (collectively: every rank builds its Comm at
+        # the same point), for the world group only.
+        self.ctrl = None
+        if not self.staged and group is None:
+            try:
+                self.ctrl = dist.new_group(backend="gloo")
+            except Exception:  # no gloo: fall back to the device group
+                self.ctrl = None
 
     # -- helpers --------------------------------------------------------------
     def _stage(self, t):
@@ -120,6 +131,10 @@ class Comm:
         a reduction chain could be fused on all ranks)."""
         import torch
 
+        if self.ctrl is not None:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.ctrl)
+            return bool(t.item())
         dev = "cpu" if self.staged else "cuda"
         t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)

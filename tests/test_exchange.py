@@ -248,3 +248,24 @@ def test_partials_collectives_over_gloo():
     assert all(r[1] == [2 + 3 + 4] * 10 for r in res)
     assert parts0 == [[i * (r + 1) for i in range(10)] for r in range(world)]
     assert all(r[3] == 7.0 for r in res)
+
+
+def _agree_rank(rank, world):
+    import torch.distributed as dist
+
+    from cubed_amd.runtime.comm import Comm
+
+    comm = Comm()
+    assert comm.ctrl is None  # a gloo world needs no separate control group
+    # the control-plane path (a host-side gloo group beside a device group)
+    comm.ctrl = dist.new_group(backend="gloo")
+    comm.staged = False
+    return comm.all_ok(True), comm.all_ok(rank != 1), comm.all_ok(True)
+
+
+def test_agreement_over_the_control_group():
+    """Comm.all_ok: plan-time agreements (MIN over ranks) run on the host-side
+    gloo group when the data group is RCCL, so they never wait on the GPU
+    stream; every rank gets the same answers, in call order."""
+    res = run_ranks(_agree_rank, 3)
+    assert res == [(True, False, True)] * 3
