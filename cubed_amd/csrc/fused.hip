@@ -450,13 +450,15 @@ extern "C" int cubed_combine_groups(const cubed_program_t* prog, const cubed_pro
 
 extern "C" int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group, int64_t max_kept) {
   // fewer groups than ~2 per CU: cut each group's rows x max_kept SoA
-  // entries into runs of >= 512 (2 per thread: the fold is a chain of
-  // dependent round trips, not bandwidth -- 48 runs of 2048 took 37 us for
-  // the vorticity's 98K entries), toward 1024 workgroups
+  // entries into runs of >= 2048 (8 loads in flight per thread), at most 32
+  // per group -- every run's arrival is an atomic on the group's counter, and
+  // 195 arrivals on one counter serialised to ~39 us for the vorticity's 98K
+  // entries (PMC: every wave ~25 us alive, mostly waiting)
   if (ngroups <= 0 || max_rows_per_group < 1 || max_kept < 1 || ngroups >= 512) return 1;
-  const int64_t per_group = (1024 + ngroups - 1) / ngroups;
-  const int64_t by_size = max_rows_per_group * max_kept / 512;
-  const int64_t s = per_group < by_size ? per_group : by_size;
+  int64_t s = (1024 + ngroups - 1) / ngroups;
+  if (s > 32) s = 32;
+  const int64_t by_size = max_rows_per_group * max_kept / 2048;
+  if (s > by_size) s = by_size;
   return s > 1 ? s : 1;
 }
 
