@@ -450,15 +450,14 @@ extern "C" int cubed_combine_groups(const cubed_program_t* prog, const cubed_pro
 
 extern "C" int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group, int64_t max_kept) {
   // fewer groups than ~2 per CU: cut each group's rows x max_kept SoA
-  // entries into runs of >= 2048 (8 loads in flight per thread), at most 32
-  // per group -- every run's arrival is an atomic on the group's counter, and
-  // 195 arrivals on one counter serialised to ~39 us for the vorticity's 98K
-  // entries (PMC: every wave ~25 us alive, mostly waiting)
+  // entries into runs of >= 512 (2 per thread), toward 1024 workgroups.
+  // (The vorticity's one-group fold of 98K entries takes 39 us with 195 runs,
+  // 49 with 32, 40 with 10: a fixed chain of dependent first touches --
+  // tables, partials, counter, epilogue program, output -- not the entries.)
   if (ngroups <= 0 || max_rows_per_group < 1 || max_kept < 1 || ngroups >= 512) return 1;
-  int64_t s = (1024 + ngroups - 1) / ngroups;
-  if (s > 32) s = 32;
-  const int64_t by_size = max_rows_per_group * max_kept / 2048;
-  if (s > by_size) s = by_size;
+  const int64_t per_group = (1024 + ngroups - 1) / ngroups;
+  const int64_t by_size = max_rows_per_group * max_kept / 512;
+  const int64_t s = per_group < by_size ? per_group : by_size;
   return s > 1 ? s : 1;
 }
 

@@ -59,14 +59,14 @@ def test_workspace_query_is_host_only(built):
 
 def test_fold_split_counts_are_host_only(built):
     """cubed_fold_groups_splits (ABI 13): few groups of many elements are cut
-    into runs of >= 2048 SoA entries, at most 32 per group and toward 1024 workgroups; many groups or
+    into runs of >= 512 SoA entries, toward 1024 workgroups; many groups or
     small ones are not split."""
     from cubed_amd import _native as nat
 
     f = nat.lib().cubed_fold_groups_splits
-    assert f(1, 10, 72000) == 32           # at most 32 arrivals per group counter
-    assert f(1, 720, 136) == 32            # the vorticity fold: 97920 entries
-    assert f(1, 40, 136) == 2              # runs of >= 2048 entries
+    assert f(1, 10, 72000) == 1024         # 720000 entries: 1024 runs
+    assert f(1, 720, 136) == 191           # the vorticity fold: 97920 entries, runs of >= 512
+    assert f(1, 8, 136) == 2
     assert f(100, 1000, 1000) == 11        # ~1024 workgroups over 100 groups
     assert f(600, 1000, 1000) == 1         # >= 512 groups: one workgroup each
     assert f(1, 1, 1000) == 1              # one short row
