@@ -18,11 +18,14 @@
 //   Byte shuffle transposes each block as a (blocksize/typesize, typesize)
 //   byte matrix; the trailing blocksize % typesize bytes stay in place.
 //
-// Decoding supports lz4, zlib and zstd streams with byte or no shuffle
-// (what zarr's defaults, the zlib codec and Blosc(cname="zstd") write); zstd
-// streams go to the system's libzstd (dlopen'ed on first use: it is the
-// reference implementation of the zstd format, only the Blosc container is
-// restated here).  blosclz / snappy streams and bit shuffle are refused.
+// Decoding supports blosclz, lz4, snappy, zlib and zstd streams with byte or
+// no shuffle (zarr's defaults, the zlib codec, Blosc(cname="zstd" |
+// "blosclz" | "snappy")); zstd streams go to the system's libzstd (dlopen'ed
+// on first use: it is the reference implementation of the zstd format, only
+// the Blosc container is restated here).  blosclz and snappy are restated
+// from their published stream formats (below); no fixture written by
+// numcodecs exists in this image, so their parity is unpinned.  Bit shuffle
+// is refused.
 // The encoder writes lz4 with byte shuffle and unsplit blocks (flag 0x10),
 // which every Blosc >= 1.x decoder reads.  Also the standalone numcodecs
 // "zstd" (one zstd frame) and "lz4" (a 4-byte size + one LZ4 block) chunks.
@@ -186,6 +189,116 @@ void lz4_encode(const uint8_t* src, int64_t n, std::vector<uint8_t>& out) {
     put_seq(out, src + anchor, n - anchor, 0, 0);
 }
 
+// ---------------------------------------------------------------- snappy (raw format)
+// A varint of the uncompressed length, then elements by the low two bits of
+// the tag byte: 0 literal (length - 1 in tag >> 2, or for 60..63 in the next
+// 1..4 little-endian bytes), 1 copy of 4 + ((tag >> 2) & 7) bytes at offset
+// ((tag >> 5) << 8) | next byte, 2 / 3 copy of 1 + (tag >> 2) bytes at a
+// 2- / 4-byte little-endian offset.  Copies may overlap their output.
+int64_t snappy_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+    uint64_t len = 0;
+    int64_t ip = 0;
+    for (int shift = 0;; shift += 7) {
+        if (ip >= n || shift > 35) return -1;
+        const uint8_t b = src[ip++];
+        len |= uint64_t(b & 0x7f) << shift;
+        if (!(b & 0x80)) break;
+    }
+    if (int64_t(len) != cap) return -1;
+    int64_t op = 0;
+    while (ip < n) {
+        const uint8_t tag = src[ip++];
+        const int type = tag & 3;
+        if (type == 0) {
+            int64_t l = tag >> 2;
+            if (l >= 60) {
+                const int nb = int(l) - 59;
+                if (ip + nb > n) return -1;
+                l = 0;
+                for (int k = 0; k < nb; ++k) l |= int64_t(src[ip + k]) << (8 * k);
+                ip += nb;
+            }
+            l += 1;
+            if (ip + l > n || op + l > cap) return -1;
+            std::memcpy(dst + op, src + ip, size_t(l));
+            ip += l;
+            op += l;
+            continue;
+        }
+        int64_t l, off;
+        if (type == 1) {
+            if (ip >= n) return -1;
+            l = 4 + ((tag >> 2) & 7);
+            off = (int64_t(tag >> 5) << 8) | src[ip++];
+        } else if (type == 2) {
+            if (ip + 2 > n) return -1;
+            l = 1 + (tag >> 2);
+            off = int64_t(src[ip]) | int64_t(src[ip + 1]) << 8;
+            ip += 2;
+        } else {
+            if (ip + 4 > n) return -1;
+            l = 1 + (tag >> 2);
+            off = rd32(src + ip);
+            ip += 4;
+        }
+        if (off == 0 || off > op || op + l > cap) return -1;
+        for (int64_t k = 0; k < l; ++k) dst[op + k] = dst[op - off + k];
+        op += l;
+    }
+    return op;
+}
+
+// ---------------------------------------------------------------- blosclz
+// Blosc's own LZ77 stream (FastLZ level-2 layout).  The first byte's low 5
+// bits open a literal run; then each control byte c is
+//   c < 32: a literal run of c + 1 bytes;
+//   c >= 32: a match of length (c >> 5) + 2 (c >> 5 == 7: plus extension
+//     bytes, each added, until one is not 255) at distance
+//     ((c & 31) << 8 | next byte) + 1 -- or, when that is (31 << 8 | 255),
+//     at distance 8191 + 1 + the next two bytes (big-endian).
+// Matches copy byte by byte (distance 1 repeats the last byte).
+int64_t blosclz_decode(const uint8_t* src, int64_t n, uint8_t* dst, int64_t cap) {
+    if (n <= 0) return cap == 0 ? 0 : -1;
+    int64_t ip = 0, op = 0;
+    uint32_t ctrl = src[ip++] & 31u;
+    for (;;) {
+        if (ctrl >= 32) {
+            int64_t len = int64_t(ctrl >> 5) - 1;
+            const int64_t hi = int64_t(ctrl & 31) << 8;
+            if (len == 6) {
+                uint8_t c;
+                do {
+                    if (ip >= n) return -1;
+                    c = src[ip++];
+                    len += c;
+                } while (c == 255);
+            }
+            if (ip >= n) return -1;
+            const uint8_t code = src[ip++];
+            int64_t dist = hi + code;
+            if (code == 255 && hi == (31 << 8)) {
+                if (ip + 2 > n) return -1;
+                dist = ((int64_t(src[ip]) << 8) | src[ip + 1]) + 8191;
+                ip += 2;
+            }
+            dist += 1;
+            len += 3;
+            if (dist > op || op + len > cap) return -1;
+            for (int64_t k = 0; k < len; ++k) dst[op + k] = dst[op - dist + k];
+            op += len;
+        } else {
+            const int64_t l = int64_t(ctrl) + 1;
+            if (ip + l > n || op + l > cap) return -1;
+            std::memcpy(dst + op, src + ip, size_t(l));
+            ip += l;
+            op += l;
+        }
+        if (ip >= n) break;
+        ctrl = src[ip++];
+    }
+    return op;
+}
+
 // ---------------------------------------------------------------- zstd (libzstd)
 
 typedef size_t (*zstd_decompress_fn)(void*, size_t, const void*, size_t);
@@ -219,7 +332,9 @@ int decode_stream(int codec, const uint8_t* src, int64_t csize, uint8_t* dst, in
         std::memcpy(dst, src, size_t(size));
         return 0;
     }
+    if (codec == 0) return blosclz_decode(src, csize, dst, size) == size ? 0 : CUBED_E_CODEC;
     if (codec == 1) return lz4_decode(src, csize, dst, size) == size ? 0 : CUBED_E_CODEC;
+    if (codec == 2) return snappy_decode(src, csize, dst, size) == size ? 0 : CUBED_E_CODEC;
     if (codec == 3) {
         uLongf got = uLongf(size);
         if (uncompress(dst, &got, src, uLong(csize)) != Z_OK || int64_t(got) != size) return CUBED_E_CODEC;

@@ -323,8 +323,8 @@ def _blosc_decompress(data: bytes, out_u8: np.ndarray):
     L = nat.lib()
     rc = L.cubed_blosc_decompress(data, len(data), out_u8.ctypes.data, out_u8.size)
     if rc != 0:
-        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec/shuffle (lz4/zlib/zstd with byte or no shuffle; "
-                                                 "blosclz, snappy and bit shuffle are not decoded)",
+        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec/shuffle (blosclz/lz4/snappy/zlib/zstd "
+                                                 "with byte or no shuffle; bit shuffle is not decoded)",
                 -1: "size mismatch"}.get(rc, f"error {rc}")
         raise ValueError(f"blosc decode failed: {what}")
 

@@ -63,14 +63,17 @@ def py_lz4_decode(src: bytes, size: int) -> bytes:
     return bytes(out)
 
 
-def py_blosc_decode(frame: bytes) -> bytes:
-    """Blosc 1.x frame reader over py_lz4_decode (test oracle for the encoder)."""
+def py_blosc_decode(frame: bytes, dec=None) -> bytes:
+    """Blosc 1.x frame reader over py_lz4_decode (test oracle for the encoder),
+    or over another stream decoder ``dec``."""
     ver, verlz, flags, ts = frame[0], frame[1], frame[2], frame[3]
     nbytes, bsize, cbytes = struct.unpack("<iii", frame[4:16])
     assert cbytes == len(frame)
     if flags & 2:
         return frame[16:16 + nbytes]
-    assert flags >> 5 == 1
+    if dec is None:
+        assert flags >> 5 == 1
+        dec = py_lz4_decode
     nblocks = -(-nbytes // bsize)
     starts = struct.unpack(f"<{nblocks}i", frame[16:16 + 4 * nblocks])
     out = bytearray()
@@ -85,7 +88,7 @@ def py_blosc_decode(frame: bytes) -> bytes:
             st += 4
             data = frame[st:st + cs]
             st += cs
-            blk += data if cs == n // ns else py_lz4_decode(data, n // ns)
+            blk += data if cs == n // ns else dec(data, n // ns)
         if flags & 1 and ts > 1:
             rows = n // ts
             a = np.frombuffer(bytes(blk[:rows * ts]), np.uint8).reshape(ts, rows).T.reshape(-1)
@@ -280,12 +283,242 @@ def test_zarr_refuses_what_it_cannot_decode(tmp_path, built):
     json.dump(meta, open(tmp_path / "q.zarr" / ".zarray", "w"))
     with pytest.raises(NotImplementedError, match="snappy"):
         Z.open_array(str(tmp_path / "q.zarr"))
-    # blosclz streams inside a blosc frame: refused with a clear error
+    # bit-shuffled blosc frames: refused with a clear error
     data = patterned(4096)
     fr = bytearray(frame(data, 4, 4096, 3, True, True, lambda b: zlib.compress(b, 5)))
-    fr[2] = (fr[2] & 0x1F) | (0 << 5)  # codec 0 = blosclz (the streams are compressed)
-    with pytest.raises(ValueError, match="blosclz"):
+    fr[2] |= 0x04  # bit shuffle
+    with pytest.raises(ValueError, match="bit shuffle"):
         native_decode(bytes(fr), len(data))
+    # a corrupt blosclz stream (match before any output): malformed, not wrong data
+    bad = bytes([0x00, 0x41, 0x20, 0x05])  # literal "A", then a match at distance 6
+    fr = bytearray(frame(b"A" * 64, 1, 64, 0, False, True, lambda b: bad))
+    with pytest.raises(ValueError, match="malformed"):
+        native_decode(bytes(fr), 64)
+
+
+# ----------------------------------------------------------------- blosclz / snappy streams
+# Restated from the published stream formats (codec.cpp); parity with
+# numcodecs-written frames is unpinned (no such fixture in this image).  The
+# encoders below write every element kind the decoders accept (short, long
+# and 60+ literals; short, extended and far matches; overlapping runs), and
+# an independent Python decoder checks them alongside the C library.
+
+
+def _matches(data: bytes, maxdist: int, minlen: int):
+    """Greedy (position, distance, length) matches via a 4-byte hash."""
+    table, out, i = {}, [], 0
+    while i + minlen <= len(data):
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is not None and 0 < i - j <= maxdist:
+            n = 0
+            while i + n < len(data) and data[j + n] == data[i + n]:
+                n += 1
+            if n >= minlen:
+                out.append((i, i - j, n))
+                for k in range(i + 1, min(i + n, len(data) - 3)):
+                    table[data[k:k + 4]] = k
+                i += n
+                continue
+        i += 1
+    return out
+
+
+def py_snappy_encode(data: bytes) -> bytes:
+    out = bytearray()
+    n = len(data)
+    while True:  # varint preamble
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            break
+
+    def literal(lit):
+        for a in range(0, len(lit), 65536):
+            piece = lit[a:a + 65536]
+            m = len(piece) - 1
+            if m < 60:
+                out.append(m << 2)
+            elif m < 256:
+                out.extend([60 << 2, m])
+            else:
+                out.extend([61 << 2, m & 255, m >> 8])
+            out.extend(piece)
+
+    pos = 0
+    for i, dist, ln in _matches(data, 65535, 4):
+        if i > pos:
+            literal(data[pos:i])
+        pos = i + ln
+        while ln > 0:
+            take = min(ln, 64)
+            if 4 <= take <= 11 and dist < 2048:
+                out.extend([((dist >> 8) << 5) | ((take - 4) << 2) | 1, dist & 255])
+            else:
+                out.extend([((take - 1) << 2) | 2, dist & 255, dist >> 8])
+            ln -= take
+    if pos < len(data):
+        literal(data[pos:])
+    return bytes(out)
+
+
+def py_snappy_decode(src: bytes, size: int) -> bytes:
+    n, shift, ip = 0, 0, 0
+    while True:
+        b = src[ip]
+        ip += 1
+        n |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            break
+    assert n == size
+    out = bytearray()
+    while ip < len(src):
+        tag = src[ip]
+        ip += 1
+        t = tag & 3
+        if t == 0:
+            ln = tag >> 2
+            if ln >= 60:
+                nb = ln - 59
+                ln = int.from_bytes(src[ip:ip + nb], "little")
+                ip += nb
+            ln += 1
+            out += src[ip:ip + ln]
+            ip += ln
+            continue
+        if t == 1:
+            ln, off = 4 + ((tag >> 2) & 7), ((tag >> 5) << 8) | src[ip]
+            ip += 1
+        elif t == 2:
+            ln, off = 1 + (tag >> 2), int.from_bytes(src[ip:ip + 2], "little")
+            ip += 2
+        else:
+            ln, off = 1 + (tag >> 2), int.from_bytes(src[ip:ip + 4], "little")
+            ip += 4
+        for _ in range(ln):
+            out.append(out[-off])
+    return bytes(out)
+
+
+def py_blosclz_encode(data: bytes) -> bytes:
+    out = bytearray()
+
+    def literal(lit):
+        for a in range(0, len(lit), 32):
+            piece = lit[a:a + 32]
+            out.append(len(piece) - 1)
+            out.extend(piece)
+
+    pos = 0
+    for i, dist, ln in _matches(data, 8191 + 65535 + 1, 3):
+        literal(data[pos:i])  # i >= 1 = pos at the first match: a stream opens with literals
+        d = dist - 1
+        field = ln - 2
+        hi, code, far = (d >> 8, d & 255, None) if d < 8191 else (31, 255, d - 8191)
+        out.append((min(field, 7) << 5) | hi)
+        if field >= 7:
+            e = field - 7
+            while e >= 255:
+                out.append(255)
+                e -= 255
+            out.append(e)
+        out.append(code)
+        if far is not None:
+            out.extend([far >> 8, far & 255])
+        pos = i + ln
+    if pos < len(data):
+        literal(data[pos:])
+    return bytes(out)
+
+
+def py_blosclz_decode(src: bytes, size: int) -> bytes:
+    out = bytearray()
+    ip = 1
+    ctrl = src[0] & 31
+    while True:
+        if ctrl >= 32:
+            ln = (ctrl >> 5) - 1
+            hi = (ctrl & 31) << 8
+            if ln == 6:
+                while True:
+                    c = src[ip]
+                    ip += 1
+                    ln += c
+                    if c != 255:
+                        break
+            code = src[ip]
+            ip += 1
+            dist = hi + code
+            if code == 255 and hi == 31 << 8:
+                dist = (src[ip] << 8 | src[ip + 1]) + 8191
+                ip += 2
+            dist += 1
+            for _ in range(ln + 3):
+                out.append(out[-dist])
+        else:
+            out += src[ip:ip + ctrl + 1]
+            ip += ctrl + 1
+        if ip >= len(src):
+            break
+        ctrl = src[ip]
+        ip += 1
+    assert len(out) == size
+    return bytes(out)
+
+
+def test_snappy_stream_by_hand(built):
+    """'abcd' + copy(len 8, off 4) + 'X' + a 2-byte-offset copy (len 5, off 13)."""
+    want = b"abcd" + b"abcdabcd" + b"X" + b"abcda"
+    st = bytes([len(want), (4 - 1) << 2]) + b"abcd" + bytes([(4 << 2) | 1, 4]) + bytes([0]) + b"X" + \
+        bytes([((5 - 1) << 2) | 2, 13, 0])
+    assert py_snappy_decode(st, len(want)) == want
+    fr = frame(want, 1, len(want), 2, False, True, lambda b: st)
+    assert native_decode(fr, len(want)) == want
+    # a 60+ literal (one length byte) and a 4-byte-offset copy
+    lit = bytes(range(100))
+    want = lit + lit[:20]
+    st = bytes([len(want), 60 << 2, 99]) + lit + bytes([((20 - 1) << 2) | 3, 100, 0, 0, 0])
+    fr = frame(want, 1, len(want), 2, False, True, lambda b: st)
+    assert native_decode(fr, len(want)) == want == py_snappy_decode(st, len(want))
+
+
+def test_blosclz_stream_by_hand(built):
+    """Literal 'ab', a run (distance 1, length 10), an extended match
+    (length 3 + 6 + 40) and a far match (distance 8191 + 1 + 300)."""
+    want = bytearray(b"ab" + b"b" * 10)
+    # length 10: field 10 - 2 = 8 >= 7, so (7 << 5) plus one extension byte 1; distance 1: code 0
+    st = bytearray([1]) + b"ab" + bytes([7 << 5, 8 - 7, 0])
+    assert py_blosclz_decode(bytes(st), len(want)) == bytes(want)
+    body = bytes((i * 7 + 3) & 255 for i in range(9000))
+    want2 = body + body[:49]
+    # literals of body (32 per run), then a far match at distance 9000 = 8191 + 1 + 808
+    st2 = bytearray()
+    for a in range(0, len(body), 32):
+        piece = body[a:a + 32]
+        st2.append(len(piece) - 1)
+        st2 += piece
+    st2 += bytes([(7 << 5) | 31, 49 - 9, 255, 808 >> 8, 808 & 255])
+    assert py_blosclz_decode(bytes(st2), len(want2)) == want2
+    for s_, w_ in ((bytes(st), bytes(want)), (bytes(st2), want2)):
+        fr = frame(w_, 1, len(w_), 0, False, True, lambda b, s_=s_: s_)
+        assert native_decode(fr, len(w_)) == w_
+
+
+@pytest.mark.parametrize("codec", [0, 2])
+@pytest.mark.parametrize("ts,shuf,dont_split", [(4, True, False), (8, True, True), (1, False, True)])
+def test_blosclz_snappy_frames_round_trip(built, codec, ts, shuf, dont_split):
+    enc = py_blosclz_encode if codec == 0 else py_snappy_encode
+    dec = py_blosclz_decode if codec == 0 else py_snappy_decode
+    data = patterned(3 * 8192 + 1000, seed=codec + ts) + bytes(70000) + bytes(range(256)) * 40
+    for blk in (data[:8192], data[-8192:], data[30000:38192]):
+        assert dec(enc(blk), len(blk)) == blk
+    fr = frame(data, ts, 8192, codec, shuf, dont_split, enc)
+    assert fr[2] >> 5 == codec
+    assert native_decode(fr, len(data)) == data
+    assert py_blosc_decode(fr, dec) == data
 
 
 def _zstd():
