@@ -922,9 +922,11 @@ class GpuDagExecutor(DagExecutor):
         ``runtime/executors/python_async.py:86-114``): the pipelines of one
         topological generation are independent, so each runs on its own HIP
         stream (up to ``PARALLEL_STREAMS``), joined back into the executor's
-        stream before the next generation.  Single GPU only: with several
-        ranks every collective must be issued in one order on one stream, so
-        the flag is accepted and the walk stays sequential."""
+        stream before the next generation.  With several ranks only ops made
+        of local kernel launches (copy / fused / GEMM) fork; every op that
+        holds a collective (partials, pieces, exchanges, fetches) stays on
+        the executor's stream, so each rank issues its collectives in one
+        order on one stream, as RCCL requires."""
         from ..reference_dag import execute_reference_dag, is_reference_dag
 
         if is_reference_dag(dag):
@@ -933,7 +935,7 @@ class GpuDagExecutor(DagExecutor):
             execute_reference_dag(self, dag, callbacks=callbacks, array_names=array_names, resume=resume,
                                   spec=spec, compute_arrays_in_parallel=compute_arrays_in_parallel, **kwargs)
             return
-        parallel = bool(compute_arrays_in_parallel) and self.world == 1
+        parallel = bool(compute_arrays_in_parallel)
         if self.world > 1 and self._stream is not None and self.device.type == "cuda":
             # collectives are issued on torch's current stream: make it the
             # executor's, so the pack / exchange / unpack sequence of a

@@ -127,6 +127,22 @@ def _cases(rank, world, zdir):
     out["reshape"] = xp.reshape(cubed.from_array(np.arange(24.0), chunks=4, spec=spec), (4, 6)).compute()
     note("manipulation")
 
+    # independent pipelines in parallel (compute_arrays_in_parallel): local
+    # kernel ops fork onto side streams, ops with collectives stay on the
+    # executor's stream in one order on every rank
+    pa = zc * 2 + 1
+    pb = xp.astype(zc, xp.float32) - 3
+    from cubed_amd.core.plan import arrays_to_plan as a2p
+    forks = getattr(ex, "parallel_forks", 0)
+    a2p(pa, pb).execute(executor=ex, array_names=[pa.name, pb.name], compute_arrays_in_parallel=True)
+    pm, ps = xp.mean(pa, axis=0), xp.sum(pb, axis=1)
+    a2p(pm, ps).execute(executor=ex, array_names=[pm.name, ps.name], resume=True,
+                        compute_arrays_in_parallel=True)
+    out["par_mean"] = pm.compute(resume=True)
+    out["par_sum"] = ps.compute(resume=True)
+    out["par_forked"] = np.array([getattr(ex, "parallel_forks", 0) > forks])
+    note("parallel")
+
     # Zarr sink written by every rank (its own chunks), read back as a source
     zpath = os.path.join(zdir, "w.zarr")
     cubed.to_zarr(zc * 3, zpath)
@@ -165,6 +181,12 @@ def test_distributed_executor_matches_oracle(world, tmp_path):
     assert np.allclose(got["var0"], x.var(axis=0), rtol=1e-12, atol=0)
     assert np.isclose(got["std_all"], x.std(ddof=1), rtol=1e-12, atol=0)
     assert np.allclose(got["var_rechunk"], x.var(axis=0), rtol=1e-12, atol=0)
+
+    z = np.random.default_rng(15).random((60, 50))
+    assert np.allclose(got["par_mean"], (z * 2 + 1).mean(axis=0), rtol=1e-12, atol=0)
+    assert np.allclose(got["par_sum"], (z.astype(np.float32) - np.float32(3)).astype(np.float64).sum(axis=1),
+                       rtol=1e-6, atol=0)
+    assert got["par_forked"].all()
 
     y = np.random.default_rng(9).random((60, 50)).astype(np.float32)
     assert np.array_equal(got["rechunk_cols"], y)
