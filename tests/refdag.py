@@ -397,7 +397,10 @@ def partial_reduce_mean_plan(work_dir, root_seed, shape=(40, 60), chunks=(10, 20
 
     fn = functools.partial(_partial_reduce,
                            reduce_func=functools.partial(_mean_combine, dtype=[("n", np.int64), ("total", np.float64)]),
-                           initial_func=functools.partial(_mean_func, dtype=[("n", np.int64), ("total", np.float64)]),
+                           # the reference's exact binding (core/ops.py:931-937): axis and
+                           # keepdims bound into initial_func, extra_func_kwargs (dtype) into both
+                           initial_func=functools.partial(_mean_func, axis=(0,), keepdims=True,
+                                                          dtype=[("n", np.int64), ("total", np.float64)]),
                            axis=(0,))
     spec = BlockwiseSpec(block_function, fn, 1, {rname: CubedArrayProxy(X, X.chunks)}, CubedArrayProxy(pt, pt.chunks))
     pop = PrimitiveOperation(CubedPipeline(apply_blockwise, p._name("apply_blockwise"), [], spec), pt,
