@@ -631,19 +631,13 @@ CUBED_DEV void fold_groups_split_body(
   Acc a[CUBED_MAX_FIELDS];
 #pragma unroll
   for (int f = 0; f < CUBED_MAX_FIELDS; ++f) a[f] = acc_init(P.field_rop[f], P.field_acc[f]);
-  // (a flat run: the identity past every task's kept extent, see above);
-  // 8 entries per thread in flight before the first combine
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += 8 * kBlock) {
-    Acc y[8][CUBED_MAX_FIELDS];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int64_t i = e + (int64_t)u * kBlock;
-#pragma unroll
-      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
-        y[u][f] = (i < e1 && f < P.nfields) ? soa[f * n + i] : acc_init(P.field_rop[f], P.field_acc[f]);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) fields_combine(a, y[u], P);
+  // (a flat run: the identity past every task's kept extent, see above;
+  // runs of ~2 entries per thread -- an 8-deep batched form measured 58 us
+  // against 39 for the vorticity fold)
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+    Acc y[CUBED_MAX_FIELDS];
+    soa_load(P, soa, n, e, y);
+    fields_combine(a, y, P);
   }
   Acc x[CUBED_MAX_FIELDS];
   block_fold(P, a, red, x);
