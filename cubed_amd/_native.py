@@ -166,6 +166,9 @@ def lib():
                                     c_void_p, c_int64, c_void_p, c_int64, c_void_p, POINTER(Program),
                                     c_void_p, c_void_p, c_void_p]
     L.cubed_fold_groups.restype = c_int
+    L.cubed_fold_groups_compiled.argtypes = [c_void_p, POINTER(Program), c_void_p, c_int64, c_int64, c_void_p,
+                                             c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]
+    L.cubed_fold_groups_compiled.restype = c_int
     L.cubed_fold_groups_splits.argtypes = [c_int64, c_int64, c_int64]
     L.cubed_fold_groups_splits.restype = c_int64
     L.cubed_combine_partials.argtypes = [POINTER(Program), c_void_p, c_void_p, c_int32, c_int64, c_void_p,
@@ -203,7 +206,7 @@ EXPORTED_SYMBOLS = (
     "cubed_copy_boxes", "cubed_abi_version", "cubed_last_error",
     "cubed_device_count", "cubed_fused_compile", "cubed_fused_chunks_compiled", "cubed_fused_source",
     "cubed_fused_code_bytes", "cubed_fused_finish", "cubed_fused_finish_compiled", "cubed_combine_partials",
-    "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits",
+    "cubed_fused_finish_groups", "cubed_combine_groups", "cubed_fold_groups", "cubed_fold_groups_splits", "cubed_fold_groups_compiled",
     "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_zstd_decompress", "cubed_lz4_chunk_decompress", "cubed_gemm_chain", "cubed_gemm_chain_path",
     "cubed_gemm_grid_check", "cubed_gemm_chain_grid",

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_groups(
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
     Acc* __restrict__ out, int kd0, int kd1, const cubed_program_t* __restrict__ Pfin,
     const cubed_task_t* __restrict__ fin_tasks) {
-  fold_groups_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1, Pfin, fin_tasks);
+  fold_groups_body<false>(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1, Pfin, fin_tasks);
 }
 
 __global__ __launch_bounds__(kBlock) void k_fold_groups_split(
@@ -93,8 +93,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_groups_split(
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
     int64_t nsplit, Acc* __restrict__ out_split, Acc* __restrict__ out, int kd0, int kd1,
     const cubed_program_t* __restrict__ Pfin, const cubed_task_t* __restrict__ fin_tasks) {
-  fold_groups_split_body(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, nsplit, out_split, out, kd0, kd1, Pfin,
-                         fin_tasks);
+  fold_groups_split_body<false>(*Pd, tasks, ntasks, max_kept, soa, gs, ngroups, nsplit, out_split, out, kd0, kd1,
+                                Pfin, fin_tasks);
 }
 
 __global__ __launch_bounds__(kBlock) void k_combine_parts(

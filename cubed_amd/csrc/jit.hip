@@ -26,12 +26,13 @@ namespace cubed {
 struct JitKernel {
   std::string main_name, fin_name;  // descriptive names (they show in rocprof traces)
   std::string finish_name;          // partials mode: the SoA finish (epilogue after the cross-GPU combine)
+  std::string fold_name;            // partials mode: the lifted fold + finish
   std::string source;
   std::string log;
   std::vector<char> code;
   std::mutex mu;
   std::unordered_map<int, hipModule_t> modules;  // per device
-  std::unordered_map<int, hipFunction_t> main_fn, fin_fn, finish_fn;
+  std::unordered_map<int, hipFunction_t> main_fn, fin_fn, finish_fn, fold_fn;
 };
 
 static std::mutex g_mu;
@@ -75,12 +76,27 @@ std::string jit_kernel_name(const cubed_program_t& P) {
 // kernel.  The interpreted k_finish_soa walks the program from device memory
 // and spent 15-16 us on the 50000 outputs of a rank's rechunk + mean share
 // (a short grid of long dependent load chains).
+// ... and the lifted fold (cubed_fold_groups_compiled): a full reduction's
+// per-element partials folded per group and finished with the program's own
+// epilogue -- the interpreted fold's generic combine and epilogue switches
+// are the latency chain that kept it at ~40 us for one scalar.
 static std::string jit_finish_source(const cubed_program_t& P, const std::string& name) {
   if (!(P.mode & CUBED_MODE_PARTIALS) || P.nfields == 0) return "";
   return "extern \"C\" __global__ __launch_bounds__(256) void " + name +
          "_finish(const cubed_task_t* __restrict__ tasks, int64_t ntasks, int64_t max_kept, "
          "const cubed::Acc* __restrict__ soa, int kd0, int kd1) {\n"
-         "  cubed::finish_soa_body(JP, tasks, ntasks, max_kept, soa, kd0, kd1);\n}\n";
+         "  cubed::finish_soa_body(JP, tasks, ntasks, max_kept, soa, kd0, kd1);\n}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void " + name +
+         "_fold(const cubed_task_t* __restrict__ tasks, int64_t ntasks, int64_t max_kept, "
+         "const cubed::Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups, int64_t nsplit, "
+         "cubed::Acc* __restrict__ out_split, cubed::Acc* __restrict__ out, int kd0, int kd1, "
+         "const cubed_task_t* __restrict__ fin_tasks) {\n"
+         "  if (nsplit > 1)\n"
+         "    cubed::fold_groups_split_body<true>(JP, tasks, ntasks, max_kept, soa, gs, ngroups, nsplit, out_split, "
+         "out, kd0, kd1, nullptr, fin_tasks);\n"
+         "  else\n"
+         "    cubed::fold_groups_body<true>(JP, tasks, ntasks, max_kept, soa, gs, ngroups, out, kd0, kd1, nullptr, "
+         "fin_tasks);\n}\n";
 }
 
 std::string jit_source(const cubed_program_t& P, const std::string& name) {
@@ -197,13 +213,15 @@ static int load(JitKernel* k, hipStream_t stream, hipFunction_t* main_fn, hipFun
     e = hipModuleGetFunction(&f0, m, k->main_name.c_str());
     if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
     if (hipModuleGetFunction(&f1, m, k->fin_name.c_str()) != hipSuccess) f1 = nullptr;
-    hipFunction_t f2 = nullptr;
+    hipFunction_t f2 = nullptr, f3 = nullptr;
     if (hipModuleGetFunction(&f2, m, k->finish_name.c_str()) != hipSuccess) f2 = nullptr;
+    if (hipModuleGetFunction(&f3, m, k->fold_name.c_str()) != hipSuccess) f3 = nullptr;
     (void)hipGetLastError();
     k->modules[dev] = m;
     k->main_fn[dev] = f0;
     k->fin_fn[dev] = f1;
     k->finish_fn[dev] = f2;
+    k->fold_fn[dev] = f3;
   }
   *main_fn = k->main_fn[dev];
   *fin_fn = k->fin_fn[dev];
@@ -228,6 +246,7 @@ extern "C" int cubed_fused_compile(const cubed_program_t* prog, const char* incl
   k->main_name = jit_kernel_name(*prog);
   k->fin_name = k->main_name + ((prog->mode & CUBED_MODE_STREAM) ? "_split" : "_finalize");
   k->finish_name = k->main_name + "_finish";
+  k->fold_name = k->main_name + "_fold";
   k->source = jit_source(*prog, k->main_name);
   if (int rc = compile(k, include_dirs)) { delete k; return rc; }
   std::lock_guard<std::mutex> g(g_mu);
@@ -343,6 +362,51 @@ extern "C" int cubed_fused_finish_compiled(void* handle, const cubed_program_t* 
   const Acc* soa = (const Acc*)d_partials;
   const cubed_task_t* tasks = d_tasks;
   void* args[] = {&tasks, &ntasks, &max_kept, &soa, &kd0, &kd1};
+  hipError_t e = hipModuleLaunchKernel(ff, grid.x, grid.y, 1, kBlock, 1, 1, 0, st, args, nullptr);
+  if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+extern "C" int cubed_fold_groups_compiled(void* handle, const cubed_program_t* prog, const cubed_task_t* d_tasks,
+                                          int64_t ntasks, int64_t max_kept, const void* d_row_partials,
+                                          const int64_t* d_group_start, int64_t ngroups, void* d_group_partials,
+                                          int64_t nsplit, void* d_split_ws, const cubed_task_t* d_fin_tasks,
+                                          void* stream) {
+  if (!handle || !prog || !d_row_partials || !d_group_start || !d_group_partials || !d_fin_tasks ||
+      (!d_tasks && ntasks > 0) || (nsplit > 1 && !d_split_ws)) {
+    set_error("cubed_fold_groups_compiled: null argument");
+    return CUBED_E_ARG;
+  }
+  if (ngroups == 0) return 0;
+  if (int rc = check_program(*prog)) return rc;
+  if (!(prog->mode & CUBED_MODE_PARTIALS) || prog->nfields == 0 || max_kept <= 0 || ngroups > ntasks ||
+      nsplit < 1) {
+    set_error("cubed_fold_groups_compiled: not a partials-mode reduction / bad shape");
+    return CUBED_E_ARG;
+  }
+  JitKernel* k = (JitKernel*)handle;
+  hipFunction_t fmain = nullptr, ffin = nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = load(k, st, &fmain, &ffin)) return rc;
+  hipFunction_t ff;
+  {
+    int dev = 0;
+    hipError_t e = st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev);
+    if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
+    std::lock_guard<std::mutex> g(k->mu);
+    ff = k->fold_fn[dev];
+  }
+  if (!ff) { set_error("cubed_fold_groups_compiled: the program has no fold kernel"); return CUBED_E_JIT; }
+  int kd0, kd1;
+  kept_dims(*prog, kd0, kd1);
+  const dim3 grid = grid_of(ngroups * nsplit);
+  const cubed_task_t* tasks = d_tasks;
+  const Acc* soa = (const Acc*)d_row_partials;
+  const int64_t* gs = d_group_start;
+  Acc* out_split = (Acc*)d_split_ws;
+  Acc* out = (Acc*)d_group_partials;
+  const cubed_task_t* fin_tasks = d_fin_tasks;
+  void* args[] = {&tasks, &ntasks, &max_kept, &soa, &gs, &ngroups, &nsplit, &out_split, &out, &kd0, &kd1, &fin_tasks};
   hipError_t e = hipModuleLaunchKernel(ff, grid.x, grid.y, 1, kBlock, 1, 1, 0, st, args, nullptr);
   if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
   return 0;

@@ -581,6 +581,10 @@ CUBED_DEV void fold_group_done(const cubed_program_t& P, Acc (&x)[CUBED_MAX_FIEL
 // per-element partials; this fold then reduces each group's rows AND kept
 // elements to one accumulator per field: one workgroup per group, a strided
 // pass per thread, then the 64-wide shuffle tree and LDS across the waves.
+// FIN_MAIN (the JIT fold, cubed_fold_groups_compiled): the epilogue is the
+// main program's own (constant-folded, no LDS staging); fin_tasks gives the
+// outputs.
+template <bool FIN_MAIN = false>
 CUBED_DEV void fold_groups_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
@@ -602,9 +606,13 @@ CUBED_DEV void fold_groups_body(
   }
   Acc x[CUBED_MAX_FIELDS];
   block_fold(P, a, red, x);
-  __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
-  if (Pfin) stage_program(pfin, Pfin);
-  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
+  if constexpr (FIN_MAIN) {
+    if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, &P, fin_tasks);
+  } else {
+    __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
+    if (Pfin) stage_program(pfin, Pfin);
+    if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
+  }
 }
 
 // Split fold for few groups of many elements (e.g. one scalar over 720
@@ -615,6 +623,7 @@ CUBED_DEV void fold_groups_body(
 // workgroups to arrive (arrival counter per group, self-resetting) folds the
 // nsplit results and finishes the group: one launch.  A fixed
 // (shape-determined) order, so deterministic.
+template <bool FIN_MAIN = false>
 CUBED_DEV void fold_groups_split_body(
     const cubed_program_t& P, const cubed_task_t* __restrict__ tasks, int64_t ntasks,
     int64_t max_kept, const Acc* __restrict__ soa, const int64_t* __restrict__ gs, int64_t ngroups,
@@ -666,9 +675,13 @@ CUBED_DEV void fold_groups_split_body(
   }
   __syncthreads();  // red is reused
   block_fold(P, a, red, x);
-  __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
-  if (Pfin) stage_program(pfin, Pfin);
-  if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
+  if constexpr (FIN_MAIN) {
+    if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, &P, fin_tasks);
+  } else {
+    __shared__ __attribute__((aligned(16))) cubed_program_t pfin;
+    if (Pfin) stage_program(pfin, Pfin);
+    if (threadIdx.x == 0) fold_group_done(P, x, out, ngroups, g, Pfin ? &pfin : nullptr, fin_tasks);
+  }
 }
 
 // Combine nparts SoA partial blocks (e.g. all-gathered from the ranks) in

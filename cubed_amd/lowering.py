@@ -717,7 +717,15 @@ class FusedLaunch:
             prog_fin, d_fin, table, gsoa, split_ws = self.fold
             L = nat.lib()
             # the fold and the epilogue in one launch (the group's last
-            # workgroup finishes it)
+            # workgroup finishes it); specialised from the program's JIT
+            # module when there is one
+            if self.handle is not None and self.prog.mode & MODE_PARTIALS:
+                nat.check(L.cubed_fold_groups_compiled(
+                    self.handle, self.prog, self.table.data_ptr(), self.ntasks, self.max_kept,
+                    self.ws.data_ptr(), self.groups.data_ptr(), self.ngroups, gsoa.data_ptr(), self.fold_split,
+                    split_ws.data_ptr() if split_ws is not None else None, table.data_ptr(), stream),
+                    "cubed_fold_groups_compiled")
+                return
             nat.check(L.cubed_fold_groups(self.prog, self.d_prog.data_ptr(), self.table.data_ptr(),
                                           self.ntasks, self.max_kept, self.ws.data_ptr(),
                                           self.groups.data_ptr(), self.ngroups, gsoa.data_ptr(),

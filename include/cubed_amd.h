@@ -318,6 +318,14 @@ int cubed_fold_groups(const cubed_program_t* prog, const cubed_program_t* d_prog
  * nfields x ngroups x nsplit 8-byte accumulators followed by ngroups uint32
  * arrival counters -- zero it once, the kernel leaves the counters at zero. */
 int64_t cubed_fold_groups_splits(int64_t ngroups, int64_t max_rows_per_group, int64_t max_kept);
+/* The same fold + finish from the JIT module of a CUBED_MODE_PARTIALS program
+ * (cubed_fused_compile): combine and epilogue specialised, the epilogue the
+ * program's own (its outputs through d_fin_tasks[g]); CUBED_E_JIT if the
+ * module has no fold kernel. */
+int cubed_fold_groups_compiled(void* handle, const cubed_program_t* prog, const cubed_task_t* d_tasks,
+                               int64_t ntasks, int64_t max_kept, const void* d_row_partials,
+                               const int64_t* d_group_start, int64_t ngroups, void* d_group_partials,
+                               int64_t nsplit, void* d_split_ws, const cubed_task_t* d_fin_tasks, void* stream);
 int cubed_combine_partials(const cubed_program_t* prog, const cubed_program_t* d_prog,
                            const void* d_parts, int32_t nparts, int64_t n, void* d_out,
                            void* stream);

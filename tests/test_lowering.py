@@ -825,4 +825,6 @@ def test_partials_programs_compile_a_specialised_finish(built, dry):
     P.mode |= Lw.MODE_PARTIALS
     src = nat.program_source(nat.compile_program(P))
     assert "_partials_finish(" in src and "cubed::finish_soa_body(JP," in src
-    assert "cubed_fused_finish_compiled" in nat.EXPORTED_SYMBOLS
+    # ... and the lifted fold with the program's own epilogue
+    assert "_partials_fold(" in src and "cubed::fold_groups_split_body<true>(JP," in src
+    assert {"cubed_fused_finish_compiled", "cubed_fold_groups_compiled"} <= set(nat.EXPORTED_SYMBOLS)
