@@ -830,7 +830,7 @@ class Lowerer:
 
     def lower_expr_pipeline(self, program: ir.ExprProgram, spec, target: DeviceArray, task_keys,
                             rows_fn=None, sample_key=None, partials=False, lift=True,
-                            merge_kept_groups=False):
+                            merge_kept_groups=False, host_count=False):
         """Build the FusedLaunch (or CopyLaunch) for a blockwise pipeline.
         ``rows_fn(leaves, kinds) -> (rows, reduced dims)`` overrides the
         per-task views (reduction-chain fusion, cubed_amd/chains.py)."""
@@ -1067,10 +1067,11 @@ class Lowerer:
             if P.nfields == 0:
                 raise LoweringError("partials mode needs a reduction")
             P.mode |= MODE_PARTIALS
-            if group_layout is not None:
-                # per-group SoA straight from the kernel (DistPiecesLaunch):
-                # its plain COUNT fields are the groups' global row counts,
-                # filled by the host once, never reduced across the ranks
+            if group_layout is not None or host_count:
+                # per-group SoA straight from the kernel (DistPiecesLaunch), or
+                # a chain whose global count the host knows (PartialsLaunch):
+                # its plain COUNT fields hold the global counts, filled by the
+                # host once, never reduced across the ranks
                 P.mode |= MODE_HOST_COUNT
         table = layout.table(self.ctx.device)
         ws = nat.lib().cubed_fused_workspace_bytes(P, len(rows), layout.max_kept, layout.max_red)

@@ -178,7 +178,7 @@ class PartialsLaunch:
     """Cross-rank combine + epilogue of a reduction chain run in partials
     mode (the FusedLaunch before it leaves SoA partials in its workspace)."""
 
-    def __init__(self, ctx, fused, rops: List[str], acc_int: List[bool], owners: List[int]):
+    def __init__(self, ctx, fused, rops: List[str], acc_int: List[bool], owners: List[int], host_count=None):
         import torch
 
         self.ctx = ctx
@@ -187,6 +187,15 @@ class PartialsLaunch:
         self.n = fused.ntasks * fused.max_kept
         self.sum_only = all(r in SUM_ROPS for r in rops)
         self.acc_int = acc_int
+        # host_count (CUBED_MODE_HOST_COUNT, sum-only chains): the kernel
+        # leaves the COUNT fields alone; they hold the global count (the whole
+        # reduced extent), filled here once -- one collective fewer per step
+        self.host_count = [r == "count" and host_count is not None for r in rops]
+        if host_count is not None:
+            assert self.sum_only and fused.prog.mode & 128
+            for f in range(self.nf):
+                if self.host_count[f]:
+                    self.field_view(f).fill_(int(host_count))
         # a plain COUNT field (mean's n) holds one value per output block --
         # every kept element of a task counts the same rows -- so only that
         # value crosses the ranks (8 B per block instead of 8 B per element:
@@ -216,6 +225,8 @@ class PartialsLaunch:
         if self.sum_only:
             mk = self.fused.max_kept
             for f in range(self.nf):
+                if self.host_count[f]:
+                    continue
                 v = self.field_view(f)
                 per_block = self.uniform[f] and mk > 1
                 if per_block:

@@ -875,18 +875,20 @@ class GpuDagExecutor(DagExecutor):
                                          lambda t: self._task_reads(p1, chain.first_spec, t))
         discard = self.scratch(max(target.slot_bytes(f) for f in target.fields))
         select = {K: [t for t in contrib[K] if first_owner(t) == rank] for K in keys}
+        rops = [f.rop for f in chain.program.reduce.fields]
+        count = _chain_global_count(chain, rops)
         with _remote_chunks(fetch, arrays):
             launch = self.lowerer.lower_expr_pipeline(
                 chain.program, chain.first_spec, target, keys,
                 rows_fn=lambda leaves, kinds: chain_rows(
                     self.lowerer, chain, leaves, kinds, keys, select=select,
                     out_owned=lambda K: target.owner(K) == rank, discard=discard),
-                sample_key=contrib[keys[0]][0], partials=True, lift=False)
+                sample_key=contrib[keys[0]][0], partials=True, lift=False, host_count=count is not None)
         launches = [fetch] if fetch is not None else []
         launches += _with_gathers(launch, self.device)
-        rops = [f.rop for f in chain.program.reduce.fields]
         acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
-        launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys]))
+        launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys],
+                                       host_count=count))
         return launches
 
     def exec_dag(self, dag, array_names):
@@ -1181,6 +1183,28 @@ class GpuDagExecutor(DagExecutor):
         if total > HBM_BYTES_PER_GPU:
             raise MemoryError(f"plan needs {total} bytes of HBM-resident arrays, more than one "
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")
+
+
+def _chain_global_count(chain, rops):
+    """The global COUNT of a chain run over several ranks, when the host
+    knows it: a plain ``count`` field of a sum-only chain (mean's ``n``)
+    counts every element of the reduced axes, which the chain covers whole --
+    the product of the reduced extents of the first op's full-rank inputs,
+    if they all agree (else None: the counts are reduced over RCCL)."""
+    from .dist import SUM_ROPS
+
+    if "count" not in rops or not all(r in SUM_ROPS for r in rops) or chain.regions:
+        return None
+    axes = tuple(chain.program.reduce.axes)
+    n = chain.program.ndim
+    exts = set()
+    for proxy in chain.first_spec.reads_map.values():
+        shape = getattr(getattr(proxy, "array", None), "shape", None)
+        if shape is not None and len(shape) == n:
+            exts.add(tuple(int(shape[a]) for a in axes))
+    if len(exts) != 1:
+        return None
+    return int(np.prod(exts.pop(), dtype=np.int64))
 
 
 class _Schedule:

@@ -48,6 +48,10 @@ def test_quad_means_partials_per_rank(built, world):
         assert fused.ntasks == 1 and fused.max_red == 10 * mine or (mine == 0 and fused.max_red == 1)
         assert part.sum_only and part.root == 0 and part.finish_here == (rank == 0)
         assert u.zarray.local_nslots() == mine
+        # mean's n is the whole reduced extent (T = 80): filled by the host
+        # (CUBED_MODE_HOST_COUNT), never reduced across the ranks
+        assert P.mode & 128 and part.host_count == [True, False]
+        assert (part.field_view(0) == 80).all()
 
 
 def test_rechunk_is_one_exchange_per_rank(built):
