@@ -29,8 +29,8 @@ dominates):
 Multi-GPU: ``python bench.py --gpus N`` (no torchrun around it) re-launches
 itself as N ranks under torch.distributed.run before touching the GPU; under
 torchrun, WORLD_SIZE must equal --gpus.  Quad-means weak-scales (each GPU
-holds 100 time chunks of u and v: one streaming launch + one RCCL reduce per
-field); the rechunk extras strong-scale (50000^2 total: pack -> one
+holds 100 time chunks of u and v: one streaming launch + one RCCL reduce of
+the f64 totals, the count host-provided); the rechunk extras strong-scale (50000^2 total: pack -> one
 all_to_all over xGMI -> unpack; rechunk+mean reduces before the exchange).
 
 CPU baseline (rank 0, N=1 only): the oracle's restatement of the reference's
