@@ -1067,7 +1067,7 @@ class Lowerer:
             if P.nfields == 0:
                 raise LoweringError("partials mode needs a reduction")
             P.mode |= MODE_PARTIALS
-            if group_layout is not None or host_count:
+            if group_layout is not None or (host_count() if callable(host_count) else host_count):
                 # per-group SoA straight from the kernel (DistPiecesLaunch), or
                 # a chain whose global count the host knows (PartialsLaunch):
                 # its plain COUNT fields hold the global counts, filled by the

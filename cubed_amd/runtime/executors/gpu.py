@@ -876,19 +876,25 @@ class GpuDagExecutor(DagExecutor):
         discard = self.scratch(max(target.slot_bytes(f) for f in target.fields))
         select = {K: [t for t in contrib[K] if first_owner(t) == rank] for K in keys}
         rops = [f.rop for f in chain.program.reduce.fields]
-        count = _chain_global_count(chain, rops)
+        meta = {}
+
+        def rows_fn(leaves, kinds):
+            rows = chain_rows(self.lowerer, chain, leaves, kinds, keys, select=select,
+                              out_owned=lambda K: target.owner(K) == rank, discard=discard)
+            # from geometry every rank derives alike (same decision everywhere)
+            meta["count"] = _chain_global_count(self.lowerer, chain, rops, keys, contrib, leaves)
+            return rows
+
         with _remote_chunks(fetch, arrays):
             launch = self.lowerer.lower_expr_pipeline(
-                chain.program, chain.first_spec, target, keys,
-                rows_fn=lambda leaves, kinds: chain_rows(
-                    self.lowerer, chain, leaves, kinds, keys, select=select,
-                    out_owned=lambda K: target.owner(K) == rank, discard=discard),
-                sample_key=contrib[keys[0]][0], partials=True, lift=False, host_count=count is not None)
+                chain.program, chain.first_spec, target, keys, rows_fn=rows_fn,
+                sample_key=contrib[keys[0]][0], partials=True, lift=False,
+                host_count=lambda: meta.get("count") is not None)
         launches = [fetch] if fetch is not None else []
         launches += _with_gathers(launch, self.device)
         acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
         launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys],
-                                       host_count=count))
+                                       host_count=meta.get("count")))
         return launches
 
     def exec_dag(self, dag, array_names):
@@ -1185,26 +1191,33 @@ class GpuDagExecutor(DagExecutor):
                               f"MI355X holds ({HBM_BYTES_PER_GPU})")
 
 
-def _chain_global_count(chain, rops):
+def _chain_global_count(lowerer, chain, rops, keys, contrib, leaves):
     """The global COUNT of a chain run over several ranks, when the host
     knows it: a plain ``count`` field of a sum-only chain (mean's ``n``)
-    counts every element of the reduced axes, which the chain covers whole --
-    the product of the reduced extents of the first op's full-rank inputs,
-    if they all agree (else None: the counts are reduced over RCCL)."""
+    counts the elements of the reduced dims of every first-level task that
+    contributes to an output block -- on every rank together.  Taken from the
+    lowering geometry of ALL contributing tasks (``geometry_only``: the same
+    extents on every rank, whoever owns the chunks), in the program's own
+    iteration space, so permuted or reshaped leaves, broadcast inputs and
+    chains ending before the last round count what the kernel counts.  None
+    when blocks differ (the counts are then reduced over RCCL)."""
+    from ...storage import geometry_only
     from .dist import SUM_ROPS
 
     if "count" not in rops or not all(r in SUM_ROPS for r in rops) or chain.regions:
         return None
+    p1 = chain.first_spec.function
     axes = tuple(chain.program.reduce.axes)
-    n = chain.program.ndim
-    exts = set()
-    for proxy in chain.first_spec.reads_map.values():
-        shape = getattr(getattr(proxy, "array", None), "shape", None)
-        if shape is not None and len(shape) == n:
-            exts.add(tuple(int(shape[a]) for a in axes))
-    if len(exts) != 1:
-        return None
-    return int(np.prod(exts.pop(), dtype=np.int64))
+    counts = set()
+    with geometry_only():
+        for K in keys:
+            c = 0
+            for t in contrib[K]:
+                lay = lowerer.task_layout(p1, chain.first_spec, chain.first_target, t, leaves,
+                                          [], p1.structured, [])
+                c += math.prod(int(lay.extent[a]) for a in axes)
+            counts.add(c)
+    return counts.pop() if len(counts) == 1 else None
 
 
 class _Schedule:

@@ -54,6 +54,61 @@ def test_quad_means_partials_per_rank(built, world):
         assert (part.field_view(0) == 80).all()
 
 
+def _partials(dry, m):
+    dry.launched.clear()
+    arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+    part = [l for l in dry.launched if isinstance(l, PartialsLaunch)]
+    return part[0] if part else None
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_count_from_geometry_transposed(built, world):
+    """mean over axis 0 of a TRANSPOSED non-square input (permute_dims fuses
+    into the chain with permuted leaf axes): the host-filled count is the
+    reduced extent of the chain's own iteration space (60), not of the leaf
+    array's first axis (40) -- the same on every rank."""
+    x = np.arange(40 * 60, dtype=np.float64).reshape(40, 60)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+        # row chunks of 40: the chain reads the permuted chunks in place
+        a = cubed.from_array(x, chunks=(40, 15), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        part = _partials(dry, xp.mean(xp.permute_dims(a, (1, 0)), axis=0))
+        assert part is not None and part.host_count == [True, False]
+        assert (part.field_view(0) == 60).all()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_count_from_geometry_broadcast(built, world):
+    """mean(u * w, axis=0) with w (16, 32) broadcast against u (80, 16, 32):
+    the broadcast leaf has no reduced axis; the count is 80."""
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=dry)
+        random.seed(2)
+        u = crandom.random((80, 16, 32), chunks=(10, 16, 32), spec=spec)
+        w = crandom.random((16, 32), chunks=(16, 32), spec=spec)
+        arrays_to_plan(u, w).execute(executor=dry, array_names=[u.name, w.name])
+        part = _partials(dry, xp.mean(u * w, axis=0))
+        assert part is not None and part.host_count == [True, False]
+        assert (part.field_view(0) == 80).all()
+
+
+def test_host_count_geometry_counts_contributing_tasks(built):
+    """The geometry count sums every contributing task's reduced extent
+    (all ranks), with an edge chunk along the reduced axis (T = 75)."""
+    world = 2
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        u, v, m = _quad(dry, T=75)
+        part = [l for l in dry.launched if isinstance(l, PartialsLaunch)]
+        if part and any(part[0].host_count):
+            assert (part[0].field_view(part[0].host_count.index(True)) == 75).all()
+        else:  # the edge chunk splits the chain: the count is reduced over the ranks
+            assert not part or not any(part[0].host_count)
+
+
 def test_rechunk_is_one_exchange_per_rank(built):
     world = 4
     x = np.arange(60 * 50, dtype=np.float32).reshape(60, 50)
