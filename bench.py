@@ -59,12 +59,16 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
-EXTRAS = ("rechunk", "rechunk_mean", "rechunk_mean_share", "rechunk_mean_rehearsal", "config1", "vorticity",
-          "matmul_f32", "matmul_bf16")
+EXTRAS = ("rechunk", "rechunk_rehearsal", "rechunk_mean", "rechunk_mean_share", "rechunk_mean_rehearsal",
+          "config1", "vorticity", "var", "matmul_f32", "matmul_bf16")
 # RCCL all-reduce of the rehearsed ranks' group partials (50000 f64 totals =
 # 400 KB, + 50 int64 counts) over 8 GPUs: NOT measured here (one GPU per box);
 # an allowance added to the rehearsed per-rank step for the 8-GPU prediction
 RCCL_ALLOWANCE_US = 40.0
+# xGMI: 7 links per MI355X, one to each peer of an 8-GPU node, ~153 GB/s per
+# direction each (task statement / SURVEY.md §5; not measured here): the
+# rechunk_rehearsal prediction of the per-pair transfers
+XGMI_LINK_GBS = 153.0
 
 
 def parse(argv=None):
@@ -399,12 +403,13 @@ def sample_columns(shape, k, seed):
     return np.stack(np.unravel_index(flat, shape), axis=1) if shape else np.zeros((1, 0), np.int64)
 
 
-def owned_column_sums(arrs, fn, cols):
+def owned_column_sums(arrs, fn, cols, center=None):
     """f64 sums over axis 0 of ``fn(*chunks)`` at the sampled trailing
     multi-indices ``cols`` (k, ndim - 1), over the chunks of ``arrs`` (equal
     chunking) this rank owns.  ``fn`` gets the chunks in their own dtype
     (numpy's arithmetic: f32 * f32 stays f32) and its result is summed in f64
-    (statistical_functions.py:57, ``dtype=float64``)."""
+    (statistical_functions.py:57, ``dtype=float64``).  ``center`` (k,): sum
+    the squared deviations from it instead (a two-pass variance)."""
     import torch
 
     A = arrs[0]
@@ -418,7 +423,11 @@ def owned_column_sums(arrs, fn, cols):
         local = np.ravel_multi_index(tuple((cols[sel] - st).T), tuple(ext))
         li = torch.as_tensor(local, device=A.device)
         vals = [device_chunk(a, coords).reshape(A.chunk_extent(coords)[0], -1)[:, li] for a in arrs]
-        acc[torch.as_tensor(sel, device=A.device)] += fn(*vals).double().sum(0)
+        ts = torch.as_tensor(sel, device=A.device)
+        val = fn(*vals).double()
+        if center is not None:
+            val = (val - center[ts]) ** 2
+        acc[ts] += val.sum(0)
     return acc
 
 
@@ -748,6 +757,151 @@ def rechunk_mean_rehearsal_extra(args, rank, world, t1_ms=None):
         out["one_gpu_step_ms"] = t1_ms
         out["predicted_speedup"] = round(t1_ms / out["predicted_step_ms"], 2)
     return out
+
+
+def rechunk_rehearsal_extra(args, rank, world, t1_ms=None):
+    """Config 3's MATERIALISED rechunk (50000^2 f32 rows -> (50000, 1000)
+    columns) as each rank of an N-rank job, rehearsed on this one GPU: all N
+    rehearsed ranks (LoopbackComm over one LoopbackMesh) allocate their
+    block-cyclic shares and run RechunkLaunch for real -- pack of the strided
+    source pieces, local copies, and the receive side of every peer transfer
+    written into the target slots from the peer's recorded send (matched by
+    pair and order, so the targets hold the right bytes and are checked bit
+    for bit).  Per rank: the HIP-event time of each phase and the bytes it
+    sends over xGMI.  The 8-GPU prediction adds the transfer time at a
+    STATED link rate (XGMI_LINK_GBS per direction on the dedicated link of
+    each peer pair, not measured: one GPU per box) -- serial (pack + local
+    copies + unpack, then every transfer) and overlapped (the first slice's
+    pack, then the transfers, with the later packs and local copies behind
+    them: RechunkLaunch's slicing) bounds.  The rehearsal's slot writes
+    stand in for RCCL's receive-side writes and are reported, not charged."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.comm import LoopbackComm, LoopbackMesh
+    from cubed_amd.runtime.executors.dist import RechunkLaunch
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    W = args.rehearse_world
+    N = 50000
+    mesh = LoopbackMesh(W)
+    ranks = []
+    for r in range(W):
+        ex = GpuDagExecutor(comm=LoopbackComm(r, W, mesh=mesh))
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2000)
+        x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        y = x.rechunk((N, 1000))
+        plan = arrays_to_plan(y)
+        step = step_fn(plan, ex, [y], x)
+        step()  # record phase: this rank's sends go to the mesh
+        ranks.append((ex, x, y, step))
+    sync()
+    mesh.phase = "replay"
+    xl = regenerate_source((N, N), (1000, N), 2000)
+    out = {"world": W, "xgmi_link_gbs_assumed": XGMI_LINK_GBS, "ranks": {}}
+    ok = True
+    for r, (ex, x, y, step) in enumerate(ranks):
+        step()
+        dt, summ = timed_launches(ex, step, 5, 1)
+        rl = [l for v in ex._cache.values() for l in v[1] if isinstance(l, RechunkLaunch)][0]
+        plan = rl.plan
+        phases = {k[2]: round(c * ms / 5, 4) for k, (c, ms) in summ.items() if k[0] == "rechunk"}
+        per_peer = [sum(x_.nbytes for x_ in lst) for lst in plan.send]
+        xgmi_ms = max(max(per_peer), max(sum(x_.nbytes for x_ in lst) for lst in plan.recv)) / \
+            (XGMI_LINK_GBS * 1e9) * 1e3
+        # the rank's own stream work: pack, local copies, unpack.  The
+        # slot writes are the loopback's stand-in for RCCL writing the
+        # arriving bytes (part of the transfer on a real rank, not charged)
+        local_ms = sum(phases.get(p, 0.0) for p in ("pack", "local_copies", "unpack"))
+        first_pack = phases.get("pack", 0.0) / max(1, len(rl.slices))
+        chk = rechunk_check(xl, y)
+        ok &= chk["pass"]
+        out["ranks"][r] = dict(ms=round(dt * 1e3, 4), phases_ms=phases, slices=len(rl.slices),
+                               stream_work_ms=round(local_ms, 4),
+                               bytes_out=plan.send_bytes, bytes_in=plan.recv_bytes,
+                               max_bytes_per_peer=max(per_peer), xgmi_ms_assumed=round(xgmi_ms, 4),
+                               predicted_serial_ms=round(local_ms + xgmi_ms, 4),
+                               predicted_overlapped_ms=round(max(local_ms, first_pack + xgmi_ms), 4),
+                               check=chk["pass"])
+    busiest = max(out["ranks"].values(), key=lambda v: v["predicted_serial_ms"])
+    out["predicted_step_ms"] = {"serial": busiest["predicted_serial_ms"],
+                                "overlapped": max(v["predicted_overlapped_ms"] for v in out["ranks"].values())}
+    if t1_ms:
+        out["one_gpu_step_ms"] = t1_ms
+        out["predicted_speedup"] = {k: round(t1_ms / v, 2) for k, v in out["predicted_step_ms"].items()}
+    out["check"] = {"kind": "bit-exact", "pass": bool(ok), "what": f"every target chunk of all {W} rehearsed "
+                    f"ranks vs a local Philox regeneration of the source"}
+    CHECKS.append(("rechunk_rehearsal", out["check"]))
+    del ranks, xl
+    free_gpu()
+    return out
+
+
+def var_extra(args, ex, rank, world):
+    """north_star's var at config 2's size: xp.var(u * v, axis=0) and
+    xp.std(u * v, axis=0), u, v (1000, 720, 1440) f32 in (10, 720, 1440)
+    chunks -- the mean's reduction pattern (statistical_functions.py:28-100)
+    over a {n, mu, M2} intermediate, one fused pass.  No reference var
+    exists in v0.12.0 (api_status.md:72,74): checked against a two-pass f64
+    var of the resident inputs (numpy's definition)."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+
+    T = args.t_length * world
+    spec = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex)
+    random.seed(1000)
+    u = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+    v = xp.astype(crandom.random((T, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
+    arrays_to_plan(u, v).execute(executor=ex, array_names=[u.name, v.name])
+    sync()
+    out = {}
+    for fname in ("var", "std"):
+        m = getattr(xp, fname)(u * v, axis=0)
+        plan = arrays_to_plan(m)
+        step = step_fn(plan, ex, [m], (u, v))
+        step()
+        step()
+        dt, summ = timed_launches(ex, step, 10, world)
+        r = dict(metric=f"{fname}(u*v, axis=0) effective input GB/s", value=round((u.nbytes + v.nbytes) / dt / 1e9, 1),
+                 ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ), **overhead(dt, summ, 10))
+        if world == 1:
+            key, ms = dominant(summ, "FusedLaunch")
+            r["roofline"] = roofline_hbm(u.nbytes + v.nbytes, ms, f"{fname}_stream", args,
+                                         f"{key[0]}#{key[1]} ({key[2]}), mean {ms:.4f} ms/launch")
+        else:
+            r["roofline"] = roofline_step((u.nbytes + v.nbytes) // world, dt)
+        r["check"] = column_var_check(u, v, m, fname == "std")
+        CHECKS.append((fname, r["check"]))
+        out[fname] = r
+        del m, plan
+    return out
+
+
+def column_var_check(u, v, m, sqrt, k=64, seed=13):
+    """Two-pass f64 var over axis 0 of u*v (f32 products) at k sampled
+    columns: every rank sums its chunks, one all-reduce for the sums, one
+    for the squared deviations from the mean; rtol 1e-6 (f32 output)."""
+    import torch
+
+    M = m.zarray
+    cols = sample_columns(M.shape, k, seed)
+    U, V = u.zarray, v.zarray
+    n = u.shape[0]
+    s1 = allreduce_(owned_column_sums([U, V], lambda a, b: a * b, cols))
+    s2 = allreduce_(owned_column_sums([U, V], lambda a, b: a * b, cols, center=s1 / n))
+    exp = s2 / n
+    if sqrt:
+        exp = torch.sqrt(exp)
+    got = allreduce_(owned_output_values(M, cols))
+    r = check_close(got.cpu().numpy(), exp.cpu().numpy(), 1e-6,
+                    f"64 sampled {'std' if sqrt else 'var'} vs a two-pass f64 var of the resident inputs")
+    r.update(kind="sampled", entries=len(cols), world=world_size())
+    return r
 
 
 def config1_extra(args, ex, rank, world):
@@ -1150,6 +1304,10 @@ def main(argv=None):
         try:
             if name == "rechunk":
                 extra[name] = rechunk_extra(args, ex, rank, world)
+            elif name == "rechunk_rehearsal":
+                if world == 1:
+                    t1 = extra.get("rechunk", {}).get("plan_288GB", {}).get("ms")
+                    extra[name] = rechunk_rehearsal_extra(args, rank, world, t1)
             elif name == "rechunk_mean":
                 extra[name] = rechunk_mean_extra(args, ex, rank, world)
             elif name == "rechunk_mean_share":
@@ -1160,6 +1318,8 @@ def main(argv=None):
                     extra[name] = rechunk_mean_rehearsal_extra(args, rank, world, t1)
             elif name == "config1":
                 extra[name] = config1_extra(args, ex, rank, world)
+            elif name == "var":
+                extra[name] = var_extra(args, ex, rank, world)
             elif name == "vorticity":
                 extra[name] = vorticity_extra(args, ex, rank, world)
             elif name.startswith("matmul"):

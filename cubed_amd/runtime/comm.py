@@ -28,7 +28,7 @@ otherwise identical.
 
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence
 
 
 class Comm:
@@ -48,14 +48,8 @@ class Comm:
         # control-plane agreements (all_ok) go over a host-side gloo group:
         # a device all-reduce + .item() would wait for every kernel queued on
         # the stream, serialising the first step of each new plan across the
-        # ranks.  Created here (collectively: every rank builds its Comm at
-        # the same point), for the world group only.
-        self.ctrl = None
-        if not self.staged and group is None:
-            try:
-                self.ctrl = dist.new_group(backend="gloo")
-            except Exception:  # no gloo: fall back to the device group
-                self.ctrl = None
+        # ranks.  One per process and world group (control_group).
+        self.ctrl = control_group(dist) if not self.staged and group is None else None
 
     # -- helpers --------------------------------------------------------------
     def _stage(self, t):
@@ -146,6 +140,36 @@ class Comm:
         return self.dist.get_global_rank(self.group, r)
 
 
+_CTRL: dict = {}
+
+
+def control_group(dist):
+    """The host-side gloo group beside the world group, created ONCE per
+    process and world group (``dist.new_group`` is collective and opens its
+    own connections, so building one per executor would leak them).  Every
+    rank agrees on the result over the world group before using it: if the
+    gloo group could not be made on some rank, all ranks fall back to the
+    device group (None)."""
+    import torch
+
+    world = dist.group.WORLD
+    key = id(world)
+    if key in _CTRL and _CTRL[key][0] is world:
+        return _CTRL[key][1]
+    try:
+        ctrl = dist.new_group(backend="gloo")
+    except Exception:  # noqa: BLE001 -- agreed below
+        ctrl = None
+    dev = "cuda" if str(dist.get_backend()).lower() != "gloo" else "cpu"
+    t = torch.tensor([0 if ctrl is None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if not int(t.item()):
+        ctrl = None
+    _CTRL.clear()  # a re-initialised world drops the previous one's group
+    _CTRL[key] = (world, ctrl)
+    return ctrl
+
+
 class Pending:
     """Transfers started by ``Comm.exchange``."""
 
@@ -160,6 +184,33 @@ class Pending:
         self.works, self.fixups = [], []
 
 
+class LoopbackMesh:
+    """The point-to-point transfers of several ``LoopbackComm`` ranks
+    rehearsed in one process, matched by (sender, receiver) pair and issue
+    order -- the pairing RCCL's grouped send / receive gives
+    (``batch_isend_irecv``: per peer, both ends list their transfers in the
+    same order).  Two phases, set by the caller:
+
+    * ``"record"``: every rank's sends are copied into its mailboxes
+      ``box[(src, dst)]`` (run every rank once); receives are left as they
+      are (their senders may not have run yet);
+    * ``"replay"``: a receive from ``src`` takes the next recorded send of
+      that pair (a per-pair cursor that wraps, so every step of a rank
+      consumes the pair's sequence once) -- the bytes land exactly where the
+      peer's RCCL send would put them, so the assembled target of all ranks
+      can be checked bit for bit.  Sends are not copied again."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.phase = "record"
+        self.box: Dict = {}
+        self.cursor: Dict = {}
+        self.log: List = []  # (src, dst, nbytes) of every recorded send, in issue order
+
+    def bytes_between(self, src: int, dst: int) -> int:
+        return sum(t.numel() * t.element_size() for t in self.box.get((src, dst), ()))
+
+
 class LoopbackComm:
     """Rank ``rank`` of a ``world``-rank job, rehearsed in ONE process on one
     GPU: the executor plans, allocates and launches exactly what that rank
@@ -170,18 +221,29 @@ class LoopbackComm:
     (there are no other ranks): a rehearsal times the per-rank launch list; a
     test folds the recorded partials of all ``world`` rehearsed ranks itself
     (``record=True`` keeps a copy of every reduce / all-reduce input, in
-    issue order, in ``self.records``)."""
+    issue order, in ``self.records``).
+
+    Point-to-point exchanges (``exchange``) are matched by peer and order:
+    with a shared ``LoopbackMesh`` the receives get the bytes the peer rank
+    sent (see there); alone, every receive is written from a scratch buffer
+    of its size (the write traffic of the arriving bytes, values
+    meaningless)."""
 
     backend = "loopback"
     staged = False
 
-    def __init__(self, rank: int, world: int, record: bool = False):
+    def __init__(self, rank: int, world: int, record: bool = False, mesh: Optional[LoopbackMesh] = None):
         if not 0 <= rank < world:
             raise ValueError(f"rank {rank} outside a world of {world}")
+        if mesh is not None and mesh.world != world:
+            raise ValueError(f"a mesh of {mesh.world} ranks for a world of {world}")
         self.rank, self.world = rank, world
         self.record = record
         self.records: List = []
         self._scratch = None
+        self.mesh = mesh
+        self.sent_bytes = 0  # bytes this rank's exchanges sent / received (per call, cumulative)
+        self.recv_bytes = 0
 
     def _copy(self, t):
         """Read + write ``t``'s bytes once (into a scratch buffer)."""
@@ -202,10 +264,47 @@ class LoopbackComm:
         if n:
             recv[:n].copy_(send[:n])
 
+    def _scratch_of(self, nbytes, device):
+        import torch
+
+        if self._scratch is None or self._scratch.numel() < nbytes or self._scratch.device != device:
+            self._scratch = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+        return self._scratch
+
     def exchange(self, sends, recvs) -> "Pending":
-        for (s, _), (r, _) in zip(sends, recvs):
-            n = min(s.numel(), r.numel())
-            r.reshape(-1)[:n].copy_(s.reshape(-1)[:n])
+        mesh = self.mesh
+        for t, peer in sends:
+            if not 0 <= peer < self.world or peer == self.rank:
+                raise ValueError(f"rank {self.rank} sends to {peer}")
+            nb = t.numel() * t.element_size()
+            self.sent_bytes += nb
+            if mesh is not None and mesh.phase == "record":
+                mesh.box.setdefault((self.rank, peer), []).append(t.detach().reshape(-1).clone())
+                mesh.log.append((self.rank, peer, nb))
+        for t, peer in recvs:
+            if not 0 <= peer < self.world or peer == self.rank:
+                raise ValueError(f"rank {self.rank} receives from {peer}")
+            import torch
+
+            flat = t.reshape(-1).view(torch.uint8)
+            nb = flat.numel()
+            self.recv_bytes += nb
+            if mesh is None:
+                flat.copy_(self._scratch_of(nb, flat.device)[:nb])
+                continue
+            if mesh.phase != "replay":
+                continue
+            key = (peer, self.rank)
+            box = mesh.box.get(key)
+            if not box:
+                raise RuntimeError(f"rank {self.rank}: nothing recorded from rank {peer}")
+            i = mesh.cursor.get(key, 0)
+            mesh.cursor[key] = (i + 1) % len(box)
+            src = box[i].view(torch.uint8)
+            if src.numel() != nb:
+                raise RuntimeError(f"rank {self.rank}: transfer {i} from rank {peer} is "
+                                   f"{src.numel()} B, the receive {nb} B")
+            flat.copy_(src)
         return Pending([], [])
 
     def _reduce(self, kind, t):

@@ -161,6 +161,9 @@ class RechunkLaunch:
         self.collective = True  # every rank takes part, even with nothing to move
 
     def run(self, stream):
+        timing = getattr(self.ctx, "timing", None)
+        if timing is not None and getattr(self.ctx.comm, "backend", None) == "loopback":
+            return self._run_phases(stream, timing)
         pending = []
         for pack, sends, recvs in self.slices:
             pack.run(stream)
@@ -169,6 +172,31 @@ class RechunkLaunch:
         for p in pending:
             p.wait()
         self.unpack.run(stream)
+
+    def _run_phases(self, stream, timing):
+        """A rehearsed rank (LoopbackComm) under bench timing: the same
+        launches, with HIP events around each phase (pack, the slot writes
+        of the arriving bytes, local copies, unpack) -- on one stream, so the
+        phases run back to back instead of overlapping the transfers."""
+        import torch
+
+        cur = torch.cuda.current_stream()
+
+        def timed(name, fn):
+            e0, e1 = timing.events()
+            e0.record(cur)
+            fn()
+            e1.record(cur)
+            timing.add(("rechunk", 0, name), e0, e1)
+
+        pending = []
+        for pack, sends, recvs in self.slices:
+            timed("pack", lambda: pack.run(stream))
+            timed("slot_writes", lambda: pending.append(self.ctx.comm.exchange(sends, recvs)))
+        timed("local_copies", lambda: self.local.run(stream))
+        for p in pending:
+            p.wait()
+        timed("unpack", lambda: self.unpack.run(stream))
 
 
 SUM_ROPS = {"sum", "nansum", "count", "count_nonnan"}

@@ -269,3 +269,57 @@ def test_agreement_over_the_control_group():
     stream; every rank gets the same answers, in call order."""
     res = run_ranks(_agree_rank, 3)
     assert res == [(True, False, True)] * 3
+
+
+def _ctrl_once_rank(rank, world):
+    import torch.distributed as dist
+
+    import cubed_amd.runtime.comm as C
+
+    made = []
+    real = dist.new_group
+
+    def counting(*a, **k):
+        made.append(1)
+        return real(*a, **k)
+
+    dist.new_group = counting
+    try:
+        g1 = C.control_group(dist)
+        g2 = C.control_group(dist)  # a second executor's Comm: no new group
+    finally:
+        dist.new_group = real
+    return len(made), g1 is g2, g1 is not None
+
+
+def test_control_group_is_made_once_per_process():
+    """one gloo control group per process and world group (every
+    default_executor() used to open another one)."""
+    assert run_ranks(_ctrl_once_rank, 2) == [(1, True, True)] * 2
+
+
+def _ctrl_fail_rank(rank, world):
+    import torch.distributed as dist
+
+    import cubed_amd.runtime.comm as C
+
+    real = dist.new_group
+
+    def flaky(*a, **k):
+        g = real(*a, **k)  # collective: every rank takes part
+        if rank == 1:
+            raise RuntimeError("no gloo here")
+        return g
+
+    dist.new_group = flaky
+    try:
+        C._CTRL.clear()
+        return C.control_group(dist) is None
+    finally:
+        dist.new_group = real
+
+
+def test_control_group_failure_is_agreed():
+    """If the gloo group cannot be made on one rank, EVERY rank falls back to
+    the device group (otherwise all_ok would run on different groups)."""
+    assert run_ranks(_ctrl_fail_rank, 2) == [True, True]

@@ -93,3 +93,77 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
     assert np.all(count == shape[0])
     got = (total.reshape(ngroups, cols) / count[:, None]).reshape(-1)[:shape[1]].astype(np.float32)
     np.testing.assert_allclose(got, want, rtol=1e-6)
+
+
+def _targets_unwritten(plan, keep):
+    from cubed_amd.storage import DeviceArray
+
+    for _, d in plan._finalize_dag().nodes(data=True):
+        t = d.get("target")
+        if isinstance(t, DeviceArray) and t is not keep:
+            t.written = False
+
+
+@pytest.mark.parametrize("shape,rows,cols", [((4000, 3000), 100, 100),    # config 3's shape, reduced
+                                             ((4050, 3050), 100, 90),     # ragged edge chunks both ways
+                                             ((1200, 1000), 150, 1000)])  # one target chunk per rank row
+def test_eight_rehearsed_ranks_rechunk_bit_exact(gpu_executor, shape, rows, cols):
+    """Config 3's MATERIALISED rechunk (rows -> columns) on 8 rehearsed
+    ranks: each rank packs, copies its local pieces and writes the pieces it
+    receives into its target slots (RechunkLaunch); the LoopbackMesh hands
+    every receive the bytes its peer sent, matched by pair and order.  The
+    target assembled from the 8 ranks' slots equals the 1-GPU rechunk bit
+    for bit.  Reference: cubed/primitive/rechunk.py:23-98,187-192."""
+    import torch
+
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.comm import LoopbackComm, LoopbackMesh
+    from cubed_amd.runtime.executors.dist import RechunkLaunch
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    def build(ex):
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2002)
+        x = xp.astype(crandom.random(shape, chunks=(rows, shape[1]), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        y = x.rechunk((shape[0], cols))
+        return x, y, arrays_to_plan(y)
+
+    x1, y1, _ = build(gpu_executor)
+    want = y1.compute()
+    assert np.array_equal(want.view(np.uint32), x1.compute().view(np.uint32))
+
+    world = 8
+    mesh = LoopbackMesh(world)
+    ranks = []
+    for r in range(world):
+        ex = GpuDagExecutor("cuda:0", comm=LoopbackComm(r, world, mesh=mesh))
+        x, y, plan = build(ex)
+        plan.execute(executor=ex, array_names=[y.name], resume=True)  # record phase
+        ranks.append((ex, x, y, plan))
+    torch.cuda.synchronize()
+    mesh.phase = "replay"
+    planned = 0
+    for ex, x, y, plan in ranks:
+        _targets_unwritten(plan, x.zarray)
+        plan.execute(executor=ex, array_names=[y.name], resume=True)
+        rl = [l for v in ex._cache.values() for l in v[1] if isinstance(l, RechunkLaunch)]
+        assert len(rl) == 1
+        planned += rl[0].plan.send_bytes
+        assert ex.comm.recv_bytes == 2 * rl[0].plan.recv_bytes  # record + replay
+    torch.cuda.synchronize()
+    assert planned == sum(n for _, _, n in mesh.log)
+    Y = ranks[0][2].zarray
+    got = np.empty(shape, np.float32)
+    import itertools
+
+    for tc in itertools.product(*[range(n) for n in Y.numblocks]):
+        owner = Y.chunk_offset(tc) % world
+        Yo = ranks[owner][2].zarray
+        assert Yo.rank == owner
+        st, ext = Yo.chunk_start(tc), Yo.chunk_extent(tc)
+        got[st[0]:st[0] + ext[0], st[1]:st[1] + ext[1]] = Yo.read_chunk(tc)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

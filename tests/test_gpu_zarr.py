@@ -173,3 +173,52 @@ def test_resume_at_complete_zarr_sink_in_a_new_process(tmp_path):
     third = _run_resume_proc(tmp_path, path, True)
     assert third["ran"] and third["tasks"] > 0
     assert np.array_equal(Z.open_array(path)[...], before)
+
+
+# ------------------------------------------------ retries (python_async.py:36-40)
+
+
+def _every_third(fn, counter):
+    """The reference's fault injection (tests/test_executor_features.py:
+    44-73): every 3rd call raises IOError."""
+    def wrapped(*a, **k):
+        counter[0] += 1
+        if counter[0] % 3 == 0:
+            raise IOError("Test fault injection")
+        return fn(*a, **k)
+    return wrapped
+
+
+def test_retries(tmp_path, spec, monkeypatch):
+    """test_retries restated on the Zarr source and sink: every 3rd chunk
+    read and every 3rd chunk write fails once; the retries (2 per chunk)
+    make the results exact anyway."""
+    a = np.arange(9, dtype=np.int64).reshape(3, 3) + 1
+    src = Z.ZarrV2Array.create(str(tmp_path / "a.zarr"), a.shape, a.dtype, (2, 2))
+    src[...] = a
+    reads, writes = [0], [0]
+    monkeypatch.setattr(Z.ZarrV2Array, "decode_into", _every_third(Z.ZarrV2Array.decode_into, reads))
+    monkeypatch.setattr(Z.ZarrV2Array, "write_chunk", _every_third(Z.ZarrV2Array.write_chunk, writes))
+    b = xp.asarray(np.ones((3, 3), np.int64), chunks=(2, 2), spec=spec)
+    c = xp.add(cubed.from_zarr(str(tmp_path / "a.zarr"), spec=spec), b)
+    assert np.array_equal(c.compute(), a + 1)
+    assert reads[0] >= 5  # 4 chunks, at least one failed read retried
+    cubed.to_zarr(c, str(tmp_path / "c.zarr"))
+    assert writes[0] >= 5
+    monkeypatch.undo()
+    assert np.array_equal(Z.open_array(str(tmp_path / "c.zarr"))[...], a + 1)
+
+
+def test_third_consecutive_failure_propagates(tmp_path, spec, monkeypatch):
+    src = Z.ZarrV2Array.create(str(tmp_path / "a.zarr"), (4, 4), np.float32, (2, 2))
+    src[...] = np.ones((4, 4), np.float32)
+    calls = [0]
+
+    def always(self, coords, out):
+        calls[0] += 1
+        raise IOError("disk on fire")
+
+    monkeypatch.setattr(Z.ZarrV2Array, "decode_into", always)
+    with pytest.raises(IOError, match="disk on fire"):
+        cubed.from_zarr(str(tmp_path / "a.zarr"), spec=spec).compute()
+    assert calls[0] >= 3 and calls[0] % 3 == 0  # 1 + 2 retries per chunk tried

@@ -37,13 +37,56 @@ def test_all_gather_fills_every_slot():
     assert out.tolist() == [1, 2, 1, 2, 1, 2]
 
 
-def test_exchange_and_all_to_all_copy_bytes():
+def test_exchange_alone_writes_every_receive():
+    """Without a mesh a rehearsed rank writes each receive (from scratch:
+    the arriving bytes' write traffic) and reads nothing of its sends into
+    them -- the round-4 form paired sends with receives by list position."""
     c = LoopbackComm(2, 8)
     s = [(torch.arange(4, dtype=torch.uint8), 1), (torch.arange(4, 8, dtype=torch.uint8), 3)]
-    r = [(torch.zeros(4, dtype=torch.uint8), 1), (torch.zeros(4, dtype=torch.uint8), 3)]
+    r = [(torch.full((6,), 7, dtype=torch.uint8), 5)]
     c.exchange(s, r).wait()
-    assert r[0][0].tolist() == [0, 1, 2, 3] and r[1][0].tolist() == [4, 5, 6, 7]
+    assert (c.sent_bytes, c.recv_bytes) == (8, 6)
+    with pytest.raises(ValueError):
+        c.exchange([(s[0][0], 2)], [])  # to itself
     send = torch.arange(6, dtype=torch.uint8)
     recv = torch.zeros(8, dtype=torch.uint8)
     c.all_to_all(recv, send, [3, 3], [3, 3])
     assert recv[:6].tolist() == list(range(6))
+
+
+def test_mesh_matches_transfers_by_peer_and_order():
+    """Three rehearsed ranks: the receives of the replay phase get the bytes
+    the PEER sent, pair by pair in issue order, whatever the order of the
+    receive list across peers."""
+    from cubed_amd.runtime.comm import LoopbackMesh
+
+    mesh = LoopbackMesh(3)
+    comms = [LoopbackComm(r, 3, mesh=mesh) for r in range(3)]
+
+    def t(*v):
+        return torch.tensor(v, dtype=torch.uint8)
+
+    sends = {0: [(t(1, 2), 1), (t(3, 4, 5), 2), (t(6), 1)],
+             1: [(t(10, 11, 12), 2), (t(13), 0)],
+             2: [(t(20), 0), (t(21, 22), 1)]}
+    shapes = {0: [(1, 1), (2, 1)], 1: [(0, 2), (2, 2), (0, 1)], 2: [(1, 3), (0, 3)]}
+
+    def recvs(r):
+        return [(torch.zeros(n, dtype=torch.uint8), peer) for peer, n in shapes[r]]
+
+    for r in range(3):  # record: receives untouched
+        comms[r].exchange(sends[r], recvs(r))
+    assert mesh.bytes_between(0, 1) == 3 and mesh.bytes_between(1, 2) == 3
+    mesh.phase = "replay"
+    got = {}
+    for step in range(2):  # the cursors wrap: every step sees the same bytes
+        for r in range(3):
+            rv = recvs(r)
+            comms[r].exchange(sends[r], rv)
+            got[r] = [x.tolist() for x, _ in rv]
+        assert got[0] == [[13], [20]]
+        assert got[1] == [[1, 2], [21, 22], [6]]
+        assert got[2] == [[10, 11, 12], [3, 4, 5]]
+    bad = [(torch.zeros(5, dtype=torch.uint8), 1)]
+    with pytest.raises(RuntimeError, match="B, the receive"):
+        comms[0].exchange([], bad)

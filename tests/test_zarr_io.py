@@ -507,6 +507,31 @@ def test_blosclz_stream_by_hand(built):
         assert native_decode(fr, len(w_)) == w_
 
 
+def test_unpinned_blosc_codecs_warn_once(built):
+    """blosclz / snappy frames decode, with a one-time warning that their
+    parity against numcodecs-written frames is unpinned."""
+    import warnings
+
+    import cubed_amd.zarr_io as Z
+
+    Z._WARNED.clear()
+    want = b"ab" + b"b" * 10
+    fr = frame(want, 1, len(want), 0, False, True, lambda b: bytes([1]) + b"ab" + bytes([7 << 5, 1, 0]))
+    for n in range(2):
+        out = np.zeros(len(want), np.uint8)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            Z._blosc_decompress(fr, out)
+        assert out.tobytes() == want
+        assert len([x for x in w if "blosclz" in str(x.message)]) == (1 if n == 0 else 0)
+    # lz4 (pinned) frames never warn
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        enc = Z._blosc_compress(np.frombuffer(want * 10, np.uint8).copy(), 1, 1)
+        Z._blosc_decompress(enc, np.zeros(len(want) * 10, np.uint8))
+    assert not w
+
+
 @pytest.mark.parametrize("codec", [0, 2])
 @pytest.mark.parametrize("ts,shuf,dont_split", [(4, True, False), (8, True, True), (1, False, True)])
 def test_blosclz_snappy_frames_round_trip(built, codec, ts, shuf, dont_split):
@@ -591,3 +616,30 @@ def test_zarr_overwrite_removes_nested_chunks(tmp_path, built):
     b.write_chunk((0, 0), np.ones((2, 2)))
     got = Z.open_array(p)[...]
     assert np.array_equal(got[:2, :2], np.ones((2, 2))) and np.all(got[2:] == -2.0) and np.all(got[:, 2:] == -2.0)
+
+
+def test_chunk_io_retries_restate_the_threads_executor():
+    """with_retries = tenacity Retrying(reraise=True,
+    stop=stop_after_attempt(retries + 1)) with retries=2
+    (runtime/executors/python_async.py:36-40)."""
+    from cubed_amd.zarr_io import CHUNK_IO_RETRIES, with_retries
+
+    assert CHUNK_IO_RETRIES == 2
+    calls = []
+
+    def flaky(fails):
+        def f(x):
+            calls.append(x)
+            if len(calls) <= fails:
+                raise IOError(f"fail {len(calls)}")
+            return x * 2
+        return f
+
+    assert with_retries(flaky(2), 21) == 42 and len(calls) == 3
+    calls.clear()
+    with pytest.raises(IOError, match="fail 3"):  # the third consecutive failure propagates
+        with_retries(flaky(3), 1)
+    assert len(calls) == 3
+    calls.clear()
+    with pytest.raises(IOError, match="fail 1"):
+        with_retries(flaky(1), 1, retries=0)
