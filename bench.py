@@ -65,6 +65,11 @@ EXTRAS = ("rechunk", "rechunk_rehearsal", "rechunk_mean", "rechunk_mean_share", 
 # 400 KB, + 50 int64 counts) over 8 GPUs: NOT measured here (one GPU per box);
 # an allowance added to the rehearsed per-rank step for the 8-GPU prediction
 RCCL_ALLOWANCE_US = 40.0
+# ... and for a REDUCE-SCATTER of the same partials (several owners of the
+# output blocks, dist.ScatterCombine): a ring reduce-scatter is the first
+# half of a ring all-reduce -- (W-1) of its 2(W-1) latency-bound steps, on
+# 1/W of the bytes per step -- so half the allowance (same assumption)
+RCCL_SCATTER_ALLOWANCE_US = RCCL_ALLOWANCE_US / 2
 # xGMI: 7 links per MI355X, one to each peer of an 8-GPU node, ~153 GB/s per
 # direction each (task statement / SURVEY.md §5; not measured here): the
 # rechunk_rehearsal prediction of the per-pair transfers
@@ -744,15 +749,25 @@ def rechunk_mean_rehearsal_extra(args, rank, world, t1_ms=None):
         step()
         dt, summ = timed_launches(ex, step, 20, 1)
         nchunks = len([c for c in range(x.numblocks[0]) if c % W == r])
+        from cubed_amd.runtime.executors.dist import DistPiecesLaunch
+
+        dps = [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistPiecesLaunch)]
+        scatter = bool(dps) and dps[0].scatter is not None
         out["ranks"][r] = dict(ms=round(dt * 1e3, 4), row_chunks=nchunks,
                                input_gbs=round(nchunks * 1000 * N * 4 / dt / 1e9, 1),
+                               collective="reduce_scatter" if scatter else "all_reduce",
                                launches_ms=fmt_launches(summ), **overhead(dt, summ, 20))
         del x, m, plan, ex
         free_gpu()
     busiest = max(v["ms"] for v in out["ranks"].values())
+    scatter = all(v["collective"] == "reduce_scatter" for v in out["ranks"].values())
+    allowance = RCCL_SCATTER_ALLOWANCE_US if scatter else RCCL_ALLOWANCE_US
     out["busiest_ms"] = busiest
-    out["rccl_allowance_us"] = RCCL_ALLOWANCE_US
-    out["predicted_step_ms"] = round(busiest + RCCL_ALLOWANCE_US / 1e3, 4)
+    out["rccl_allowance_us"] = allowance
+    out["rccl_allowance"] = ("reduce-scatter of the f64 totals (owner-major, 1/W per rank): half the 40 us "
+                             "all-reduce allowance (W-1 of its 2(W-1) ring steps); assumed, not measured"
+                             if scatter else "all-reduce of the f64 totals: assumed, not measured")
+    out["predicted_step_ms"] = round(busiest + allowance / 1e3, 4)
     if t1_ms:
         out["one_gpu_step_ms"] = t1_ms
         out["predicted_speedup"] = round(t1_ms / out["predicted_step_ms"], 2)

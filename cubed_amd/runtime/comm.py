@@ -14,8 +14,10 @@ xGMI with RCCL (torch.distributed's "nccl" backend is RCCL on ROCm):
   owned by another rank (one ``all_to_all_single`` of a packed byte buffer,
   issued on torch's current stream, so it is ordered with the pack kernel
   before it);
-* ``reduce`` / ``all_reduce`` -- the final combine round of a reduction
-  (SUM of f64 totals / i64 counts);
+* ``reduce`` / ``all_reduce`` / ``reduce_scatter`` -- the final combine
+  round of a reduction (SUM of f64 totals / i64 counts): to the one owner of
+  the output, or, with several owners, a reduce-scatter of the partials in
+  owner-major order (dist.ScatterCombine);
 * ``all_gather`` -- partials whose combine RCCL cannot express with numpy's
   semantics (max/min with NaN, prod, any/all), folded afterwards by
   ``cubed_combine_partials`` in rank order;
@@ -99,6 +101,16 @@ class Comm:
         h, staged = self._stage(t)
         self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
         self._unstage(h, t, staged)
+
+    def reduce_scatter_sum(self, out, t):
+        """SUM of every rank's ``t`` (world equal parts), rank r keeping part
+        r in ``out``.  gloo has no reduce-scatter: all-reduce, keep a part."""
+        if self.staged:
+            h = t.cpu() if t.device.type != "cpu" else t.clone()
+            self.dist.all_reduce(h, op=self.dist.ReduceOp.SUM, group=self.group)
+            out.copy_(h.view(self.world, -1)[self.rank])
+            return
+        self.dist.reduce_scatter_tensor(out, t, op=self.dist.ReduceOp.SUM, group=self.group)
 
     def reduce_sum(self, t, dst: int):
         h, staged = self._stage(t)
@@ -317,6 +329,10 @@ class LoopbackComm:
 
     def reduce_sum(self, t, dst: int):
         self._reduce("reduce_sum", t)
+
+    def reduce_scatter_sum(self, out, t):
+        self._reduce("reduce_scatter_sum", t)
+        out.copy_(t.view(self.world, -1)[self.rank])
 
     def all_gather(self, out, t):
         flat = t.reshape(-1)

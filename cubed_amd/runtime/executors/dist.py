@@ -36,6 +36,7 @@ from ...storage import DeviceArray, c_strides
 from ..exchange import FetchExchange, RechunkExchange, box_offset
 
 FETCH_ROW = 4096  # bytes per row of a whole-chunk pack copy (one wave moves 4 KiB)
+SCATTER = True  # multi-owner sum reductions combine by reduce-scatter (ScatterCombine); tests flip it
 
 
 def _round(n, a):
@@ -202,11 +203,91 @@ class RechunkLaunch:
 SUM_ROPS = {"sum", "nansum", "count", "count_nonnan"}
 
 
+class ScatterCombine:
+    """The cross-rank combine of a sum-only reduction whose output blocks
+    have SEVERAL owners, as one RCCL reduce-scatter instead of an all-reduce
+    of every block's partials (each rank finishes only its own blocks, so it
+    needs only their sums).
+
+    The SoA partials ([field][group][kept], group = output block) are
+    scattered by one ``index_copy_`` into owner-major order, [rank][field]
+    [slot][kept] with ``L`` slots per rank (the most blocks any rank owns;
+    unused slots stay zero), and ``reduce_scatter`` leaves each rank the
+    summed [field][slot][kept] of its own blocks -- straight in the finish's
+    SoA buffer, whose host-count fields (mean's n) are filled once here.
+    The finish runs over this rank's blocks only (padding slots write to a
+    discard buffer).  Payload per rank: (W-1)/W of W*L*kept*8 B per field
+    on a ring, against 2(W-1)/W of the whole G*kept*8 for the all-reduce.
+
+    Used when every field sums (SUM_ROPS), the plain COUNT fields' global
+    values are known on the host (geometry: the same on every rank) and the
+    summed fields are one contiguous run of one accumulator dtype."""
+
+    def __init__(self, ctx, fused, rows, group_owner, nf, mko, f0, f1, acc_int, host_counts, discard):
+        import dataclasses
+
+        import torch
+
+        W, rank = ctx.world, ctx.rank
+        G = len(group_owner)
+        per = [[g for g in range(G) if group_owner[g] == q] for q in range(W)]
+        L = max(1, max(len(p) for p in per))
+        pos = {g: i for q in range(W) for i, g in enumerate(per[q])}
+        nfr = f1 - f0
+        self.ctx, self.fused = ctx, fused
+        self.G, self.L, self.mko, self.nf, self.f0, self.f1 = G, L, mko, nf, f0, f1
+        self.mine = per[rank]
+        dt = torch.int64 if acc_int else torch.float64
+        self.dst = torch.tensor([(group_owner[g] * nfr + fr) * L + pos[g] for fr in range(nfr) for g in range(G)],
+                                dtype=torch.int64, device=ctx.device)
+        self.perm = torch.zeros(W * nfr * L * mko, dtype=dt, device=ctx.device)
+        self.fin = torch.zeros(max(nf * L * mko, 2), dtype=torch.int64, device=ctx.device).view(torch.uint8)
+        self.fin_red = self.fin[f0 * L * mko * 8:f1 * L * mko * 8].view(dt)
+        for f, counts in (host_counts or {}).items():
+            v = self.fin[f * L * mko * 8:(f + 1) * L * mko * 8].view(torch.int64).view(L, mko)
+            vals = [int(counts[g]) for g in self.mine] + [1] * (L - len(self.mine))
+            v.copy_(torch.tensor(vals, dtype=torch.int64, device=ctx.device)[:, None].expand(L, mko))
+        self.finish_here = bool(self.mine)
+        if self.finish_here:
+            tmpl = rows.rows[self.mine[0]]
+            pad = dataclasses.replace(tmpl, obases=[discard] * len(tmpl.obases))
+            fin_rows = [rows.rows[g] for g in self.mine] + [pad] * (L - len(self.mine))
+            self.table = dataclasses.replace(rows, rows=fin_rows).table(ctx.device)
+
+    @staticmethod
+    def plan(rops, counts_known, acc_int):
+        """(f0, f1) of the summed fields when the reduce-scatter form applies
+        (``counts_known``: the host knows every plain COUNT field's value)."""
+        if not all(r in SUM_ROPS for r in rops) or ("count" in rops and not counts_known):
+            return None
+        red = [f for f, r in enumerate(rops) if r != "count"]
+        if not red:
+            return None
+        if red != list(range(red[0], red[-1] + 1)) or len({bool(acc_int[f]) for f in red}) != 1:
+            return None
+        return red[0], red[-1] + 1
+
+    def run(self, soa_bytes, stream):
+        """``soa_bytes``: the [field][group][kept] partials (8-B words)."""
+        G, mko = self.G, self.mko
+        src = soa_bytes[self.f0 * G * mko * 8:self.f1 * G * mko * 8].view(self.perm.dtype).view(-1, mko)
+        self.perm.view(-1, mko).index_copy_(0, self.dst, src)
+        self.ctx.comm.reduce_scatter_sum(self.fin_red, self.perm)
+        if self.finish_here:
+            fused_finish(self.fused, self.table, self.L, mko, self.fin, stream)
+
+    def unpermute(self, perm_sum):
+        """[field][group][kept] from an owner-major buffer (tests: the sum of
+        every rank's recorded reduce-scatter input)."""
+        return perm_sum.view(-1, self.mko)[self.dst].view(self.f1 - self.f0, self.G, self.mko)
+
+
 class PartialsLaunch:
     """Cross-rank combine + epilogue of a reduction chain run in partials
     mode (the FusedLaunch before it leaves SoA partials in its workspace)."""
 
-    def __init__(self, ctx, fused, rops: List[str], acc_int: List[bool], owners: List[int], host_count=None):
+    def __init__(self, ctx, fused, rops: List[str], acc_int: List[bool], owners: List[int], host_count=None,
+                 discard=0):
         import torch
 
         self.ctx = ctx
@@ -229,11 +310,22 @@ class PartialsLaunch:
         # value crosses the ranks (8 B per block instead of 8 B per element:
         # quad-means' RCCL payload halves, 16.6 -> 8.3 MB per rank)
         self.uniform = [r == "count" for r in rops]
+        group_owner = list(owners)
         owners = sorted(set(owners))
         # one owner for every output block (e.g. a full reduction): RCCL reduce
-        # to it; otherwise all-reduce and every rank finishes its own blocks
+        # to it; otherwise reduce-scatter in owner-major order (ScatterCombine)
+        # or, where that does not apply, all-reduce; every rank finishes its
+        # own blocks
         self.root = owners[0] if len(owners) == 1 else None
         self.finish_here = ctx.rank in owners
+        self.scatter = None
+        fr = ScatterCombine.plan(rops, host_count is not None, acc_int) if self.root is None and SCATTER else None
+        if fr is not None and fused.ntasks == len(group_owner):
+            self.scatter = ScatterCombine(
+                ctx, fused, fused.layout, group_owner, self.nf, fused.max_kept, fr[0], fr[1], acc_int[fr[0]],
+                {f: [int(host_count)] * len(group_owner) for f, r in enumerate(rops) if r == "count"},
+                discard)
+            self.finish_here = self.scatter.finish_here
         if not self.sum_only:
             self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8,
                                         device=ctx.device)
@@ -250,6 +342,9 @@ class PartialsLaunch:
     def run(self, stream):
         comm = self.ctx.comm
         L = nat.lib()
+        if self.scatter is not None:
+            self.scatter.run(self.fused.ws, stream)
+            return
         if self.sum_only:
             mk = self.fused.max_kept
             for f in range(self.nf):
@@ -341,7 +436,7 @@ class DistPiecesLaunch:
     (cubed_fused_finish over one row per group)."""
 
     def __init__(self, ctx, fused, group_start, group_table, max_kept_out, rops, acc_int, owners,
-                 soa_direct=False, host_counts=None):
+                 soa_direct=False, host_counts=None, group_layout=None, discard=0, group_counts=None):
         import torch
 
         self.ctx = ctx
@@ -379,6 +474,15 @@ class DistPiecesLaunch:
         uniq = sorted(set(owners))
         self.root = uniq[0] if len(uniq) == 1 else None
         self.finish_here = ctx.rank in uniq
+        self.scatter = None
+        # group_counts: every group's global element count (geometry, all ranks)
+        fr = ScatterCombine.plan(rops, group_counts is not None, acc_int) \
+            if self.root is None and group_layout is not None and SCATTER else None
+        if fr is not None:
+            self.scatter = ScatterCombine(
+                ctx, fused, group_layout, list(owners), self.nf, max_kept_out, fr[0], fr[1], acc_int[fr[0]],
+                {f: list(group_counts) for f, r in enumerate(rops) if r == "count"}, discard)
+            self.finish_here = self.scatter.finish_here
         if not self.sum_only:
             self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8, device=ctx.device)
 
@@ -397,6 +501,9 @@ class DistPiecesLaunch:
                                              F.max_kept, F.ws.data_ptr(), self.gs.data_ptr(), self.ngroups,
                                              self.mko, self.gsoa.data_ptr(), stream), "cubed_combine_groups")
         comm = self.ctx.comm
+        if self.scatter is not None:
+            self.scatter.run(self.gsoa, stream)
+            return
         if self.sum_only:
             mk = self.mko
             for f in range(self.nf):

@@ -555,10 +555,12 @@ class GpuDagExecutor(DagExecutor):
             lay.max_kept == meta["mko"]
         assert launch.group_layout is None or soa_direct, "merged kept runs need one row per group"
         out = [meta["fetch"]] if meta.get("fetch") is not None else []
+        glay = dataclasses.replace(lay, rows=[lay.rows[i] for i in starts])
         out.append(DistPiecesLaunch(self, launch, np.array(starts + [len(lay.rows)], dtype=np.int64),
                                     table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys],
                                     soa_direct=soa_direct,
-                                    host_counts=meta["counts"] if launch.prog.mode & MODE_HOST_COUNT else None))
+                                    host_counts=meta["counts"] if launch.prog.mode & MODE_HOST_COUNT else None,
+                                    group_layout=glay, discard=meta["discard"], group_counts=meta["counts"]))
         return out
 
     def _lower_local(self, program, cfg, target, keys):
@@ -894,7 +896,7 @@ class GpuDagExecutor(DagExecutor):
         launches += _with_gathers(launch, self.device)
         acc_int = [bool(launch.prog.field_acc[i]) for i in range(len(rops))]
         launches.append(PartialsLaunch(self, launch, rops, acc_int, [target.owner(K) for K in keys],
-                                       host_count=meta.get("count")))
+                                       host_count=meta.get("count"), discard=discard))
         return launches
 
     def exec_dag(self, dag, array_names):

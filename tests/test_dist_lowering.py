@@ -5,6 +5,7 @@ rank would launch, no launches and no collectives)."""
 import random
 
 import numpy as np
+import torch
 import pytest
 
 import cubed_amd as cubed
@@ -245,3 +246,27 @@ def test_rechunk_mean_runs_pieces_where_chunks_live(built, monkeypatch, merge):
         assert rows == mine * 10 * 50  # every local source row once per output block
         total += dp.fused.ntasks
     assert total == (50 * 50 if not merge else 50 * world)
+
+
+def test_rechunk_mean_combines_by_reduce_scatter(built):
+    """Several owners of the output blocks: the group partials combine by
+    ONE reduce-scatter in owner-major order (each rank receives only its own
+    blocks' sums and finishes them), not an all-reduce of every block."""
+    world = 4
+    x = np.ones((500, 500), dtype=np.float32)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+        a = cubed.from_array(x, chunks=(10, 500), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        m = xp.mean(a.rechunk((500, 10)), axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        dp = dry.launched[0]
+        sc = dp.scatter
+        assert sc is not None and sc.L == 13 and sc.mine == [g for g in range(50) if g % world == rank]
+        assert (sc.f0, sc.f1) == (1, 2)  # n is host-filled; only the totals cross the ranks
+        assert sc.perm.numel() == world * 13 * 10
+        cnt = sc.fin.view(torch.int64)[:13 * 10].view(13, 10)
+        k = len(sc.mine)  # the counts of this rank's blocks, then padding slots
+        assert (cnt[:k] == 500).all() and (cnt[k:] == 1).all()

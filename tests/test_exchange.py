@@ -323,3 +323,68 @@ def test_control_group_failure_is_agreed():
     """If the gloo group cannot be made on one rank, EVERY rank falls back to
     the device group (otherwise all_ok would run on different groups)."""
     assert run_ranks(_ctrl_fail_rank, 2) == [True, True]
+
+
+# ------------------------------------------------ reduce-scatter combine
+
+
+def _scatter_rank(rank, world, G, mko):
+    """ScatterCombine over gloo with CPU tensors: each rank's SoA partials
+    ([count][total] x G groups x mko) hold (rank + 1) * (g + 1) in every
+    total; the finish is patched to capture the buffer it would run on."""
+    import types
+
+    import torch
+
+    import cubed_amd.runtime.executors.dist as D
+    from cubed_amd.lowering import Layout, TaskRow
+    from cubed_amd.runtime.comm import Comm
+
+    comm = Comm()
+    ctx = types.SimpleNamespace(world=world, rank=rank, device=torch.device("cpu"), comm=comm)
+    owner = [g % world for g in range(G)]
+    rows = Layout(order=[0], groups=[[0]], ndim=1, nred=0, mode=0, max_kept=mko, max_red=1,
+                  rows=[TaskRow([mko], [0], [[1]], [1000 + g], [[1]], 0, 0, 0) for g in range(G)])
+    counts = [50 + g for g in range(G)]
+    assert D.ScatterCombine.plan(["count", "sum"], True, [True, False]) == (1, 2)
+    sc = D.ScatterCombine(ctx, None, rows, owner, 2, mko, 1, 2, False, {0: counts}, discard=7)
+    soa = torch.zeros(2 * G * mko, dtype=torch.float64)
+    soa.view(2, G, mko)[1] = torch.tensor([(rank + 1.0) * (g + 1) for g in range(G)])[:, None]
+    seen = []
+    real = D.fused_finish
+    D.fused_finish = lambda F, table, nt, mk, part, st: seen.append((nt, mk, part.clone()))
+    try:
+        sc.run(soa.view(torch.uint8), 0)
+    finally:
+        D.fused_finish = real
+    out = {"mine": sc.mine, "L": sc.L, "finished": len(seen)}
+    if seen:
+        nt, mk, part = seen[0]
+        fin = part.view(torch.int64).view(2, sc.L, mko)
+        out["counts"] = fin[0, :, 0].tolist()
+        out["totals"] = fin[1].view(torch.float64)[:, 0].tolist()
+        out["obases"] = [int(x) for x in np.frombuffer(sc.table.numpy().tobytes(), dtype=__import__(
+            "cubed_amd._native", fromlist=["TASK_DTYPE"]).TASK_DTYPE)["out_base"][:, 0]]
+    return out
+
+
+@pytest.mark.parametrize("world,G", [(2, 5), (3, 7), (4, 2)])
+def test_scatter_combine_over_gloo(world, G):
+    """Each rank ends with the SUM over ranks of exactly its own blocks
+    (owner-major slots, padding to the busiest rank), the host counts of its
+    blocks, a finish table of its blocks (+ padding rows to the discard
+    buffer) -- and ranks owning no block run no finish."""
+    mko = 3
+    res = run_ranks(_scatter_rank, world, G, mko)
+    tri = world * (world + 1) / 2
+    L = -(-G // world)
+    for r, out in enumerate(res):
+        mine = [g for g in range(G) if g % world == r]
+        assert out["mine"] == mine and out["L"] == max(1, L)
+        assert out["finished"] == (1 if mine else 0)
+        if mine:
+            pad = out["L"] - len(mine)
+            assert out["totals"][:len(mine)] == [tri * (g + 1) for g in mine]
+            assert out["totals"][len(mine):] == [0.0] * pad
+            assert out["counts"] == [50 + g for g in mine] + [1] * pad
+            assert out["obases"] == [1000 + g for g in mine] + [7] * pad

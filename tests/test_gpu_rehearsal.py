@@ -50,8 +50,7 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
     np.testing.assert_allclose(want, host.mean(axis=0).astype(np.float32), rtol=1e-6)
 
     world = 8
-    totals, counts, host_counts = [], [], []
-    direct = []
+    scat, direct = [], []
     for r in range(world):
         comm = LoopbackComm(r, world, record=True)
         ex = GpuDagExecutor("cuda:0", comm=comm)
@@ -61,38 +60,29 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
         torch.cuda.synchronize()
         launches = [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistPiecesLaunch)]
         assert len(launches) == 1
-        direct.append(launches[0].soa_direct)
-        recs = [t for kind, t in comm.records if kind == "all_reduce_sum"]
-        tot = [t for t in recs if t.dtype == torch.float64]
-        cnt = [t for t in recs if t.dtype == torch.int64]
-        assert len(tot) == 1
-        totals.append(tot[0].cpu().numpy())
-        if launches[0].soa_direct:
-            # the global counts are filled by the host (CUBED_MODE_HOST_COUNT):
-            # nothing crosses the ranks for them; every rank holds the totals
-            assert cnt == [] and any(launches[0].host_count)
-            host_counts.append(launches[0].field_view(0).view(-1, launches[0].mko)[:, 0].cpu().numpy())
-        else:
-            assert len(cnt) == 1
-            counts.append(cnt[0].cpu().numpy())
+        dp = launches[0]
+        direct.append(dp.soa_direct)
+        # several owners of the output blocks: ONE reduce-scatter of the f64
+        # totals in owner-major order; the counts never cross the ranks
+        kinds = [kind for kind, _ in comm.records]
+        assert kinds == ["reduce_scatter_sum"], kinds
+        assert dp.scatter is not None and dp.scatter.mine == [g for g in range(dp.ngroups) if g % world == r]
+        scat.append((dp.scatter, comm.records[0][1]))
         del x, m, ex
     # uniform groups stream as merged kept runs (no combine_groups pass)
     assert all(direct) == (shape[0] % chunks[0] == 0 and shape[1] % cols == 0)
-    total = totals[0].copy()
+    total = scat[0][1].clone()
     for r in range(1, world):  # the RCCL sum, in rank order
-        total += totals[r]
-    if host_counts:
-        assert len(host_counts) == world and all(np.array_equal(h, host_counts[0]) for h in host_counts)
-        count = host_counts[0]
-    else:
-        count = counts[0].copy()
-        for r in range(1, world):
-            count += counts[r]
+        total += scat[r][1]
     ngroups = -(-shape[1] // cols)
-    assert count.shape == (ngroups,)
-    assert np.all(count == shape[0])
-    got = (total.reshape(ngroups, cols) / count[:, None]).reshape(-1)[:shape[1]].astype(np.float32)
+    tot = scat[0][0].unpermute(total)[0].cpu().numpy()
+    assert tot.shape == (ngroups, cols)
+    got = (tot / shape[0]).reshape(-1)[:shape[1]].astype(np.float32)
     np.testing.assert_allclose(got, want, rtol=1e-6)
+    # every rank finished exactly its own blocks: their counts are the global ones
+    for sc, _ in scat:
+        cnt = sc.fin.view(torch.int64)[:sc.L * sc.mko].view(sc.L, sc.mko)[:len(sc.mine), 0]
+        assert (cnt == shape[0]).all()
 
 
 def _targets_unwritten(plan, keep):

@@ -1,0 +1,190 @@
+// mfma_gap_probe.hip -- development probe (not part of the library).
+//
+// What one filler instruction costs inside the gap of a v_mfma_f32_32x32x16_bf16
+// stream when ONE wave owns its SIMD (the 128 x 128-per-wave bf16 GEMM
+// schedule the round-4 review asks for: 16 accumulators of 32 x 32 = 256
+// AGPRs, 32 MFMAs per 32-deep K step, per step 8 ds_read_b128 (A), 16
+// ds_read_b64_tr_b16 (B) and 8 global_load_lds pieces (this wave's quarter
+// of a 256 x 256 x 32 stage)).  Each variant runs the same 32-MFMA step
+// ITERS times with a different filler set placed one-per-gap by
+// sched_barrier, on every CU at once (one 256-thread workgroup per CU,
+// LDS sized to keep it alone); s_memtime around the loop gives cycles per
+// MFMA (the floor is 32), HIP events the kernel time.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/mfma_gap_probe tools/mfma_gap_probe.hip
+// Run:   tools/mfma_gap_probe [iters]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#define L3 __attribute__((address_space(3)))
+#define G1 __attribute__((address_space(1)))
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+constexpr int LDS_BYTES = 96 * 1024;  // one workgroup per CU
+
+// filler kinds per gap g (0..31) of a step
+enum { F_NONE = 0, F_B128 = 1, F_TR = 2, F_GLDS = 4 };
+
+// V: 0 bare | 1 b128 every gap | 2 tr every gap | 3 glds every 4th gap |
+//    4 glds every 2nd gap | 5 the step's 24 reads (8 b128 + 16 tr) |
+//    6 the full step (24 reads + 8 glds) | 7 full step + lgkmcnt/vmcnt wait +
+//    s_barrier at the step's end (the real loop's step boundary) |
+//    8 full step with the glds in the first 8 gaps | 9 full step, 2 fillers
+//    per gap in the first 16 gaps then bare
+template <int V>
+__device__ __forceinline__ int filler(int g) {
+  switch (V) {
+    case 1: return F_B128;
+    case 2: return F_TR;
+    case 3: return (g % 4 == 0) ? F_GLDS : 0;
+    case 4: return (g % 2 == 0) ? F_GLDS : 0;
+    case 5: return (g % 4 == 0) ? F_B128 : F_TR * ((g % 4) != 3 || g < 0) ;  // 8 b128, 24 tr -> trimmed below
+    case 6: case 7: return ((g % 4 == 0) ? F_B128 : ((g % 4 == 1 || g % 4 == 3) ? F_TR : F_GLDS));
+    case 8: return (g < 8 ? F_GLDS : 0) | ((g % 4 == 0) ? F_B128 : ((g % 4 == 1 || g % 4 == 3) ? F_TR : 0));
+    case 9: return g < 16 ? ((g % 2 == 0) ? (F_B128 | F_GLDS) : (F_TR)) : ((g % 2 == 0) ? F_TR : 0);
+    default: return 0;
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(256, 1) void k_gap(const char* __restrict__ src, size_t src_mask, int iters,
+                                                  unsigned long long* __restrict__ cyc, float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(1024))) char lds_[LDS_BYTES];
+  L3 char* lds = (L3 char*)lds_;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{};
+  bf16x8 a[4], b[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    for (int e = 0; e < 8; ++e) {
+      a[i][e] = (__bf16)(0.001f * (lane + e + i));
+      b[i][e] = (__bf16)(0.002f * (lane - e + i));
+    }
+  }
+  u32x4 rd = {0, 0, 0, 0};
+  s16x4 rt = {0, 0, 0, 0};
+  const uint32_t lb = (uint32_t)(uintptr_t)(lds + w * 16384 + lane * 16);
+  const uint32_t lt = (uint32_t)(uintptr_t)(lds + 65536 + (lane & 15) * 512 + (lane >> 4) * 16);
+  size_t goff = ((size_t)(blockIdx.x * 4 + w) * 65536 + lane * 16) & src_mask;
+  __syncthreads();
+  unsigned long long t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int it = 0; it < iters; ++it) {
+    // every read of a step lands in its own registers, consumed at the step's
+    // end (the next step's fragments): the only lgkmcnt wait is there
+    u32x4 ra[32];
+    s16x4 rtt[32];
+#pragma unroll
+    for (int g = 0; g < 32; ++g) {
+      const int mi = (g >> 1) & 3, ni = (g >> 3) & 3;
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      int f = filler<V>(g);
+      if (V == 5) f = (g % 4 == 0) ? F_B128 : ((g % 4 == 1 || g % 4 == 3) ? F_TR : 0);
+      if (f & F_B128)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ra[g]) : "v"(lb), "i"(0));
+      else
+        ra[g] = u32x4{0, 0, 0, 0};
+      if (f & F_TR)
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(rtt[g]) : "v"(lt));
+      else
+        rtt[g] = s16x4{0, 0, 0, 0};
+      if (f & F_GLDS) {
+        __builtin_amdgcn_global_load_lds((const G1 void*)(uintptr_t)(src + goff),
+                                         (L3 void*)(lds + w * 16384 + (g & 7) * 1024), 16, 0, 0);
+        goff = (goff + 4096) & src_mask;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int g = 0; g < 32; ++g) {
+      rd ^= ra[g];
+      rt ^= rtt[g];
+    }
+    if (V == 7) {
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += acc[i][j][lane & 15];
+  s += (float)(rd[0] ^ rd[1] ^ rd[2] ^ rd[3]) * 1e-30f + (float)(rt[0] ^ rt[3]) * 1e-30f;
+  sink[blockIdx.x * 256 + threadIdx.x] = s;
+  if (lane == 0) cyc[blockIdx.x * 4 + w] = t1 - t0;
+}
+
+template <int V>
+void run(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
+         float* d_sink) {
+  hipLaunchKernelGGL(k_gap<V>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);  // warm
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(k_gap<V>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> c(nblk * 4);
+  CHECK(hipMemcpy(c.data(), d_cyc, c.size() * 8, hipMemcpyDeviceToHost));
+  std::sort(c.begin(), c.end());
+  const double per = 32.0 * iters;
+  const double flop = 32768.0 * 32 * iters * 4 * nblk;
+  printf("%-44s cyc/MFMA median %6.2f  p90 %6.2f  kernel %8.3f ms  %7.1f TF  (clk %.2f GHz)\n", name,
+         c[c.size() / 2] / per, c[c.size() * 9 / 10] / per, ms, flop / (ms * 1e-3) / 1e12,
+         c[c.size() / 2] / (ms * 1e-3) / 1e9);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 2000;
+  int dev = 0, ncu = 0;
+  CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int nblk = ncu;
+  unsigned long long* d_cyc;
+  float* d_sink;
+  CHECK(hipMalloc(&d_cyc, nblk * 4 * 8));
+  CHECK(hipMalloc(&d_sink, nblk * 256 * 4));
+  // glds sources: L2-resident (4 MiB per XCD-ish) and HBM-streamed (1 GiB)
+  for (size_t bytes : {(size_t)4 << 20, (size_t)1 << 30}) {
+    char* src;
+    CHECK(hipMalloc(&src, bytes));
+    CHECK(hipMemset(src, 1, bytes));
+    const size_t mask = bytes - 1;
+    printf("# %d CUs x 1 workgroup (4 waves, one per SIMD), %d steps of 32 MFMAs; glds source %zu MiB\n", ncu,
+           iters, bytes >> 20);
+    run<0>("bare 32x32x16 MFMAs", src, mask, iters, nblk, d_cyc, d_sink);
+    run<1>("+1 ds_read_b128 every gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<2>("+1 ds_read_b64_tr_b16 every gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<3>("+1 glds16 every 4th gap (8/step)", src, mask, iters, nblk, d_cyc, d_sink);
+    run<4>("+1 glds16 every 2nd gap (16/step)", src, mask, iters, nblk, d_cyc, d_sink);
+    run<5>("step reads: 8 b128 + 16 tr, 1/gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<6>("full step: 24 reads + 8 glds, 1/gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<7>("full step + vmcnt/lgkmcnt + s_barrier", src, mask, iters, nblk, d_cyc, d_sink);
+    run<8>("full step, glds in gaps 0-7", src, mask, iters, nblk, d_cyc, d_sink);
+    run<9>("full step, 2/gap in gaps 0-15", src, mask, iters, nblk, d_cyc, d_sink);
+    CHECK(hipFree(src));
+  }
+  return 0;
+}
