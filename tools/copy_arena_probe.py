@@ -65,7 +65,7 @@ def main():
     for delta in (0, 256, 4096, 65536, 1 << 20, 1 << 21, (1 << 21) + 4096, 3 << 20, 1 << 24,
                   (1 << 24) + (1 << 20), 1 << 28, 1 << 29, 3 << 28):
         ms = time_copy(base, base + ten + delta, reps)
-        print(f"src=base       dst=base+{ten:#x}+{delta:#x}: {ms:.4f} ms  ({2 * TOTAL / ms / 1e9:.0f} GB/s moved)",
+        print(f"src=base       dst=base+{ten:#x}+{delta:#x}: {ms:.4f} ms  ({2 * TOTAL / ms / 1e6:.0f} GB/s moved)",
               flush=True)
     for delta in (0, 4096, 1 << 21, 1 << 28):
         ms = time_copy(base + ten + delta, base, reps)
@@ -73,8 +73,38 @@ def main():
     for so in (4096, 1 << 20, 1 << 21, 1 << 28):
         ms = time_copy(base + so, base + so + ten + (1 << 21), reps)
         print(f"src=base+{so:#x} dst=src+{ten:#x}+0x200000: {ms:.4f} ms", flush=True)
-    del arena
+    # physical placement: several arenas held at once occupy different HBM
+    # pages; the same copy in each (and across them)
+    arenas = [arena]
+    for _ in range(int(os.environ.get("ARENAS", "4"))):
+        a = torch.empty(2 * TOTAL + 2 * pad, dtype=torch.uint8, device="cuda")
+        a.view(torch.int32)[: (2 * TOTAL) // 4].fill_(7)
+        arenas.append(a)
     torch.cuda.synchronize()
+    bases = [(a.data_ptr() + (1 << 21) - 1) // (1 << 21) * (1 << 21) for a in arenas]
+    for rep in range(2):
+        for k, b in enumerate(bases):
+            ms = time_copy(b, b + ten, reps)
+            print(f"arena {k} ({b:#x}): {ms:.4f} ms", flush=True)
+    for k in range(1, len(bases)):
+        ms = time_copy(bases[0], bases[k] + ten, reps)
+        print(f"src arena 0, dst arena {k}: {ms:.4f} ms", flush=True)
+    # box references in the same process: hipMemcpy D2D of 10 GB, a read-only sum
+    x = arenas[0][:TOTAL]
+    y = arenas[1][:TOTAL]
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    y.copy_(x)
+    e0.record(s)
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    print(f"reference: torch D2D copy of 1e10 B: {ms:.4f} ms ({2 * TOTAL / ms / 1e6:.0f} GB/s moved)", flush=True)
+    del arenas, arena, x, y
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     for k in range(4):  # fresh torch allocations, as the executor makes them
         x = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")
         y = torch.empty(TOTAL, dtype=torch.uint8, device="cuda")

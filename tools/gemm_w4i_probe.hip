@@ -1,0 +1,160 @@
+// gemm_w4i_probe.hip -- development probe (not part of the library): the
+// chained bf16 GEMM of BASELINE config 5 (40000^2 in 5000^2 chunks, 64 output
+// chunks x 8 k segments, chunk-contiguous slots as the executor lays them out)
+// on the library's ping-pong kernel and on the one-wave interleaved kernel
+// (tools/gemm_bf16_w4i.h), in one process; max |diff| between the two (they
+// sum each K=16/32 slice in a different MFMA shape: not bit-identical).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude \
+//          -o tools/gemm_w4i_probe tools/gemm_w4i_probe.hip
+// Run:   tools/gemm_w4i_probe [reps]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+#include <algorithm>
+
+namespace cubed {
+thread_local char g_err[512];
+}
+#include "../cubed_amd/csrc/gemm_chain.hip"
+#include "gemm_bf16_w4i.h"
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void k_fill(uint16_t* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    const float v = (float)(h >> 8) * (1.0f / 16777216.0f);  // U[0, 1) as config 5
+    p[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+
+__global__ void k_diff(const float* a, const float* b, int64_t n, float* out) {
+  float m = 0.f, r = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float d = fabsf(a[i] - b[i]);
+    m = fmaxf(m, d);
+    r = fmaxf(r, d / fmaxf(fabsf(a[i]), 1e-30f));
+  }
+  atomicMax((int*)out, __float_as_int(m));
+  atomicMax((int*)out + 1, __float_as_int(r));
+}
+
+typedef void (*kfn)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*, GemmGrid);
+typedef void (*kfn_s)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*, GemmGrid,
+                      unsigned long long*);
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 2;
+  const int64_t N = argc > 2 ? atoll(argv[2]) : 40000, Cc = 5000, nb = N / Cc;
+  const int64_t slot_in = (Cc * Cc * 2 + 255) / 256 * 256, slot_out = (Cc * Cc * 4 + 255) / 256 * 256;
+  char *A, *B, *C0, *C1, *Z;
+  CHECK(hipMalloc(&A, slot_in * nb * nb));
+  CHECK(hipMalloc(&B, slot_in * nb * nb));
+  CHECK(hipMalloc(&C0, slot_out * nb * nb));
+  CHECK(hipMalloc(&C1, slot_out * nb * nb));
+  CHECK(hipMalloc(&Z, 4096));
+  CHECK(hipMemset(Z, 0, 4096));
+  CHECK(hipMemset(C0, 0, slot_out * nb * nb));
+  CHECK(hipMemset(C1, 0, slot_out * nb * nb));
+  k_fill<<<4096, 256>>>((uint16_t*)A, slot_in * nb * nb / 2, 12345u);
+  k_fill<<<4096, 256>>>((uint16_t*)B, slot_in * nb * nb / 2, 777u);
+  std::vector<cubed_gemm_chain_t> tasks(nb * nb);
+  std::vector<cubed_gemm_seg_t> segs(nb * nb * nb);
+  for (int64_t i = 0; i < nb; ++i)
+    for (int64_t j = 0; j < nb; ++j) {
+      const int64_t t = i * nb + j;
+      tasks[t] = {0, Cc, Cc, Cc, t * nb, nb, N, 0};
+      for (int64_t k = 0; k < nb; ++k)
+        segs[t * nb + k] = {(int64_t)(uintptr_t)(A + (i * nb + k) * slot_in),
+                            (int64_t)(uintptr_t)(B + (k * nb + j) * slot_in), Cc, Cc, Cc, 0};
+    }
+  cubed_gemm_chain_t *dt0, *dt1;
+  cubed_gemm_seg_t* ds;
+  CHECK(hipMalloc(&dt0, sizeof(cubed_gemm_chain_t) * tasks.size()));
+  CHECK(hipMalloc(&dt1, sizeof(cubed_gemm_chain_t) * tasks.size()));
+  CHECK(hipMalloc(&ds, sizeof(cubed_gemm_seg_t) * segs.size()));
+  for (auto& t : tasks) t.c = (int64_t)(uintptr_t)(C0 + (&t - &tasks[0]) * slot_out);
+  CHECK(hipMemcpy(dt0, tasks.data(), sizeof(cubed_gemm_chain_t) * tasks.size(), hipMemcpyHostToDevice));
+  for (auto& t : tasks) t.c = (int64_t)(uintptr_t)(C1 + (&t - &tasks[0]) * slot_out);
+  CHECK(hipMemcpy(dt1, tasks.data(), sizeof(cubed_gemm_chain_t) * tasks.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(ds, segs.data(), sizeof(cubed_gemm_seg_t) * segs.size(), hipMemcpyHostToDevice));
+  const int64_t tm = (Cc + HB_BM - 1) / HB_BM, tn = (Cc + HB_BN - 1) / HB_BN;
+  const dim3 grid((unsigned)(nb * nb * tm * tn));
+  const double flop = 2.0 * N * N * N;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  float* dmax;
+  CHECK(hipMalloc(&dmax, 8));
+
+  struct V { const char* name; kfn f; kfn_s fs; int threads; bool check; };
+  V vs[] = {
+      {"library ping-pong (16x16x32, 8 waves)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
+      {"one wave/SIMD, interleaved (w4i), 4 slots", nullptr, k_gemm_bf16_w4i<false>, 256, true},
+
+  };
+  unsigned long long* dstamp;
+  CHECK(hipMalloc(&dstamp, (size_t)grid.x * 4 * 2 * 8));
+  const int only = argc > 3 ? atoi(argv[3]) : -1;
+  for (const V& v : vs) {
+    if (only >= 0 && &v - vs != only) continue;
+    float best = 1e30f, sum = 0.f;
+    for (int r = 0; r < reps + 1; ++r) {
+      CHECK(hipEventRecord(e0));
+      if (v.f)
+        hipLaunchKernelGGL(v.f, grid, dim3(v.threads), 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z,
+                           GemmGrid{});
+      else
+        hipLaunchKernelGGL(v.fs, grid, dim3(v.threads), 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z,
+                           GemmGrid{}, (unsigned long long*)nullptr);
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (r > 0) {
+        sum += ms;
+        if (ms < best) best = ms;
+      }
+    }
+    printf("%-40s best %9.3f ms %7.1f TF   mean %9.3f ms\n", v.name, best, flop / best / 1e9, sum / reps);
+    if (v.check) {
+      CHECK(hipMemset(dmax, 0, 8));
+      k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
+      float m[2];
+      CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+      printf("   vs library: max |diff| %g, max rel %g\n", m[0], m[1]);
+    }
+    fflush(stdout);
+  }
+  // stamped builds of w4i: K-loop cycles per MFMA (clock-independent) and the
+  // clock, for the kernel and its ablations (results wrong for ABL != 0)
+  auto stamped = [&](const char* name, kfn_s f) {
+    CHECK(hipMemset(dstamp, 0, (size_t)grid.x * 4 * 2 * 8));
+    hipLaunchKernelGGL(f, grid, dim3(256), 0, 0, dt1, ds, tm, tn, (const char*)Z, GemmGrid{}, dstamp);
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(f, grid, dim3(256), 0, 0, dt1, ds, tm, tn, (const char*)Z, GemmGrid{}, dstamp);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> h((size_t)grid.x * 8);
+    CHECK(hipMemcpy(h.data(), dstamp, h.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, steps = 0;
+    for (size_t i = 0; i < h.size(); i += 2) {
+      cyc += (double)h[i];
+      steps += (double)h[i + 1];
+    }
+    printf("%-44s %8.3f ms %7.1f TF  main loop %6.2f cyc/MFMA  clock ~%.2f GHz\n", name, ms, flop / ms / 1e9,
+           cyc / (steps * 32), (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+  stamped("w4i stamped, 4 slots", k_gemm_bf16_w4i<false, 4, true, 0, 4>);
+  stamped("  ABL A staging stale (B real)", k_gemm_bf16_w4i<false, 4, true, 16, 4>);
+  stamped("  ABL B staging stale (A real)", k_gemm_bf16_w4i<false, 4, true, 32, 4>);
+  stamped("  ABL both stale", k_gemm_bf16_w4i<false, 4, true, 48, 4>);
+  stamped("  ABL no barrier, A stale", k_gemm_bf16_w4i<false, 4, true, 17, 4>);
+  return 0;
+}

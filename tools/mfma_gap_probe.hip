@@ -52,6 +52,9 @@ __device__ __forceinline__ int filler(int g) {
     case 6: case 7: return ((g % 4 == 0) ? F_B128 : ((g % 4 == 1 || g % 4 == 3) ? F_TR : F_GLDS));
     case 8: return (g < 8 ? F_GLDS : 0) | ((g % 4 == 0) ? F_B128 : ((g % 4 == 1 || g % 4 == 3) ? F_TR : 0));
     case 9: return g < 16 ? ((g % 2 == 0) ? (F_B128 | F_GLDS) : (F_TR)) : ((g % 2 == 0) ? F_TR : 0);
+    case 10: return (g % 2 == 0) ? F_TR : 0;
+    case 11: return (g % 2 == 0) ? F_B128 : 0;
+    case 12: return F_B128 | F_TR;
     default: return 0;
   }
 }
@@ -77,8 +80,16 @@ __global__ __launch_bounds__(256, 1) void k_gap(const char* __restrict__ src, si
   }
   u32x4 rd = {0, 0, 0, 0};
   s16x4 rt = {0, 0, 0, 0};
-  const uint32_t lb = (uint32_t)(uintptr_t)(lds + w * 16384 + lane * 16);
-  const uint32_t lt = (uint32_t)(uintptr_t)(lds + 65536 + (lane & 15) * 512 + (lane >> 4) * 16);
+  // the fragment addresses of the library's one-wave layout
+  // (tools/gemm_bf16_experiments.h k_gemm_bf16_w4): A [256][64 B] rows, chunk
+  // slot s of row r = k chunk s ^ ((r >> 2) & 3); B [32 k-rows][512 B], chunk
+  // slot s of k-row r = col chunk s ^ 4 * (r & 3) -- both conflict-free
+  const int ra_ = lane & 31;
+  const uint32_t lb = (uint32_t)(uintptr_t)(lds + ra_ * 64 + 16 * (((lane >> 5)) ^ ((ra_ >> 2) & 3)));
+  const int bq = lane >> 4, krow = (bq >> 1) * 8 + ((lane & 15) >> 2);
+  const uint32_t lt = (uint32_t)(uintptr_t)(lds + 16384 + krow * 512 +
+                                            16 * (((bq & 1) * 2 + ((lane & 3) >> 1)) ^ (4 * (krow & 3))) +
+                                            8 * (lane & 1));
   size_t goff = ((size_t)(blockIdx.x * 4 + w) * 65536 + lane * 16) & src_mask;
   __syncthreads();
   unsigned long long t0, t1;
@@ -184,6 +195,9 @@ int main(int argc, char** argv) {
     run<7>("full step + vmcnt/lgkmcnt + s_barrier", src, mask, iters, nblk, d_cyc, d_sink);
     run<8>("full step, glds in gaps 0-7", src, mask, iters, nblk, d_cyc, d_sink);
     run<9>("full step, 2/gap in gaps 0-15", src, mask, iters, nblk, d_cyc, d_sink);
+    run<10>("+1 ds_read_b64_tr_b16 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<11>("+1 ds_read_b128 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<12>("+1 b128 + 1 tr every gap", src, mask, iters, nblk, d_cyc, d_sink);
     CHECK(hipFree(src));
   }
   return 0;
