@@ -511,6 +511,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
       }
 }
 
+#include "gemm_bf16_w4l.h"
+
 // ------------------------------------------------------------------ f32 MFMA
 // v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate): lane l gives
 // A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31].  256x256 output tile per
@@ -953,11 +955,22 @@ extern "C" int cubed_gemm_chain(const cubed_gemm_chain_t* tasks, const cubed_gem
     if (blocks > 0x7fffffff) return fail("grid too large");
     const dim3 grid((unsigned)blocks), blk(512);
     const char* z = (const char*)d_zero;
-    // ping-pong schedule: 1072-1098 TF vs 1021-1041 for the single-slot loop
-    // on config 5 (profiles/r02_gemm_bf16_variants.log); the 4-phase and
-    // one-wave-per-SIMD experiments in tools/gemm_bf16_probe.hip measured
-    // slower (profiles/r02_gemm_bf16_q4_w4.log)
-    if (out_dtype == CUBED_BF16)
+    // round 5: one wave per SIMD with A staged in full 128-B lines
+    // (gemm_bf16_w4l.h: 1256-1258 TF on config 5) whenever every segment
+    // spans a 64-k A tile; otherwise the round-2 ping-pong schedule
+    // (1072-1098 TF, profiles/r02_gemm_bf16_variants.log)
+    bool w4l = true;
+    for (int64_t t = 0; t < ntasks && w4l; ++t)
+      for (int64_t i = tasks[t].seg0; i < tasks[t].seg0 + tasks[t].nseg; ++i)
+        if (segs[i].k < 64) { w4l = false; break; }
+    if (w4l) {
+      if (out_dtype == CUBED_BF16)
+        hipLaunchKernelGGL((k_gemm_bf16_w4l<true>), grid, dim3(256), 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{},
+                           nullptr);
+      else
+        hipLaunchKernelGGL((k_gemm_bf16_w4l<false>), grid, dim3(256), 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{},
+                           nullptr);
+    } else if (out_dtype == CUBED_BF16)
       hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{});
     else
       hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, GemmGrid{});

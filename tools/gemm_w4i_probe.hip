@@ -93,6 +93,9 @@ int main(int argc, char** argv) {
   V vs[] = {
       {"library ping-pong (16x16x32, 8 waves)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
       {"one wave/SIMD, interleaved (w4i), 4 slots", nullptr, k_gemm_bf16_w4i<false>, 256, true},
+      {"w4l: A staged in full 128-B lines", nullptr, k_gemm_bf16_w4l<false>, 256, true},
+      {"library ping-pong (again)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
+      {"w4l (again)", nullptr, k_gemm_bf16_w4l<false>, 256, true},
 
   };
   unsigned long long* dstamp;
@@ -151,10 +154,12 @@ int main(int argc, char** argv) {
            cyc / (steps * 32), (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
-  stamped("w4i stamped, 4 slots", k_gemm_bf16_w4i<false, 4, true, 0, 4>);
-  stamped("  ABL A staging stale (B real)", k_gemm_bf16_w4i<false, 4, true, 16, 4>);
-  stamped("  ABL B staging stale (A real)", k_gemm_bf16_w4i<false, 4, true, 32, 4>);
-  stamped("  ABL both stale", k_gemm_bf16_w4i<false, 4, true, 48, 4>);
-  stamped("  ABL no barrier, A stale", k_gemm_bf16_w4i<false, 4, true, 17, 4>);
+  stamped("w4i stamped", k_gemm_bf16_w4i<false, 4, true, 0, 4>);
+  stamped("w4l stamped", k_gemm_bf16_w4l<false, 4, true>);
+  stamped("  w4l ABL no barrier", k_gemm_bf16_w4l<false, 4, true, 1>);
+  stamped("  w4l ABL no fragment reads", k_gemm_bf16_w4l<false, 4, true, 4>);
+  stamped("  w4l ABL A stale", k_gemm_bf16_w4l<false, 4, true, 16>);
+  stamped("  w4l ABL B stale", k_gemm_bf16_w4l<false, 4, true, 32>);
+  stamped("  w4l ABL both stale", k_gemm_bf16_w4l<false, 4, true, 48>);
   return 0;
 }
