@@ -51,11 +51,16 @@ __device__ __forceinline__ void wl_seq(F&& f) {
 // wrong when nonzero): 1 no K-loop barrier, 4 no fragment reads, 16 A
 // sources never advance, 32 B sources never advance.  STAMP: probe builds
 // store per-wave main-loop cycles to stamp_out (nullptr in the library).
-template <bool OUT_BF16, int GM = 4, bool STAMP = false, int ABL = 0>
+// GRID (cubed_gemm_chain_grid): 256 x 256 tiles over the WHOLE output of a
+// regular chunk grid, as k_gemm_bf16_chain<.., GRID>: a lane's A row / B
+// column / C element lies in chunk row I0 or I0+1 / column J0 or J0+1
+// (selected per lane where the sources are computed and in the epilogue),
+// so 5000-wide chunks are not each padded to 5120 (4.9 % of the MFMAs).
+template <bool OUT_BF16, int GM = 4, bool STAMP = false, int ABL = 0, bool GRID = false>
 __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain_t* __restrict__ tasks,
                                                        const cubed_gemm_seg_t* __restrict__ segs,
                                                        int64_t tiles_m, int64_t tiles_n,
-                                                       const char* __restrict__ zero, GemmGrid,
+                                                       const char* __restrict__ zero, GemmGrid gg,
                                                        unsigned long long* __restrict__ stamp_out) {
   __shared__ __attribute__((aligned(1024))) char lds_[WL_LDS];
   CUBED_L char* lds = (CUBED_L char*)lds_;
@@ -63,11 +68,15 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   CUBED_L char* ldsB = lds + WL_NA * WL_ATILE;
   int64_t t, m0, n0;
   tile_of<HB_BM, HB_BN, GM>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
-  const cubed_gemm_chain_t* __restrict__ T = tasks + t;
-  const int64_t M = T->m, N = T->n;
+  GridTile gt{0, 0, 0, 0, tasks + t, tasks + t, tasks + t};
+  if constexpr (GRID) gt = grid_tile(tasks, gg, m0, n0);
+  const cubed_gemm_chain_t* __restrict__ T = gt.T;
+  const int64_t M = GRID ? gg.M : T->m, N = GRID ? gg.N : T->n;
   const int32_t KT = (int32_t)T->ktot;
   if (m0 >= M || n0 >= N) return;
   const int64_t seg0 = T->seg0, segN = T->seg0 + T->nseg;
+  // GRID: segment s of chunk row I0+1 / column J0+1 is s + dsI / s + dsJ
+  const int64_t dsI = gt.TI1->seg0 - T->seg0, dsJ = gt.TJ1->seg0 - T->seg0;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -78,32 +87,44 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   // = (lane & 7) ^ ((4 (i & 1) + (lane >> 4)) & 7).  Computed where needed
   // (segment edges only): registers go to the fragments
   const int cA0 = (lane & 7) ^ ((lane >> 4) & 7), cA1 = (lane & 7) ^ ((4 + (lane >> 4)) & 7);
-  auto rowA = [&](int i) __attribute__((always_inline)) {
-    const int64_t r = m0 + 64 * w + 8 * i + (lane >> 3);
-    return r < M ? r : M - 1;
+  // the row inside its chunk, and (GRID) whether that chunk is row I0 + 1
+  auto rowA = [&](int i, bool& hi) __attribute__((always_inline)) {
+    int64_t r = m0 + 64 * w + 8 * i + (lane >> 3);
+    r = r < M ? r : M - 1;
+    hi = GRID && r >= gt.mb;
+    return GRID ? r - (hi ? gt.mb : gt.I0 * gg.cm) : r;
   };
   // ---- B staging geometry (as w4i): piece i (0..3) = k-rows 2(4w+i) + (lane>>5)
   auto rowB = [&](int i) __attribute__((always_inline)) { return 2 * (4 * w + i) + (lane >> 5); };
-  auto colB = [&](int i) __attribute__((always_inline)) {
+  auto colB = [&](int i, bool& hi) __attribute__((always_inline)) {
     const int r = rowB(i);
-    const int64_t n = n0 + 8 * ((lane & 31) ^ (4 * (r & 3)));
-    return n + 8 <= N ? n : N - 8;
+    int64_t n = n0 + 8 * ((lane & 31) ^ (4 * (r & 3)));
+    n = n + 8 <= N ? n : N - 8;
+    hi = GRID && n >= gt.nb;
+    return GRID ? n - (hi ? gt.nb : gt.J0 * gg.cn) : n;
   };
 
   // ---- two independent segment walks: A in 64-k tiles, B in 32-k steps
+  // GRID: whether B piece i's columns (this lane) lie in chunk column J0+1,
+  // whose row pitch may differ (the last chunk column is narrower)
+  bool hB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) colB(i, hB[i]);
+  // (hi: GRID only, the same segment of chunk row I0+1 for A / column J0+1 for B)
   struct Walk {
     int64_t s;
     int32_t ks, ke;
-    Seg cur;
+    Seg cur, hi;
     bool inc_ok;
   };
-  Walk wa{seg0, 0, (int32_t)segs[seg0].k, load_seg(segs, seg0), false};
-  Walk wb = wa;
-  auto advance = [&](Walk& W, int32_t k0, int32_t len) __attribute__((always_inline)) {
+  Walk wa{seg0, 0, (int32_t)segs[seg0].k, load_seg(segs, seg0), load_seg(segs, seg0 + dsI), false};
+  Walk wb{seg0, 0, (int32_t)segs[seg0].k, load_seg(segs, seg0), load_seg(segs, seg0 + dsJ), false};
+  auto advance = [&](Walk& W, int32_t k0, int32_t len, int64_t dh) __attribute__((always_inline)) {
     if (k0 + len >= W.ke && W.s + 1 < segN) {
       W.ks = W.ke;
       ++W.s;
       W.cur = load_seg(segs, W.s);
+      if constexpr (GRID) W.hi = load_seg(segs, W.s + dh);
       W.ke = W.ks + (int32_t)segs[W.s].k;
       W.inc_ok = false;
     }
@@ -114,16 +135,30 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   uint64_t stA[8], stB[4];
   auto stageA_full = [&](int32_t k0) __attribute__((always_inline)) {
     wa.inc_ok = k0 + 64 <= wa.ke;
-    const uint64_t a0 = (uint64_t)(uintptr_t)wa.cur.a + (uint64_t)((int64_t)(k0 - wa.ks) * 2);
+    const int64_t dk = (int64_t)(k0 - wa.ks) * 2;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) stA[i] = a0 + (uint64_t)(rowA(i) * wa.cur.lda2 + ((i & 1) ? cA1 : cA0) * 16);
+    for (int i = 0; i < 8; ++i) {
+      // (fields selected one by one: a per-lane select of a struct reference
+      // puts the walks in scratch memory)
+      bool hi;
+      const int64_t r = rowA(i, hi);
+      const uint64_t base = hi ? (uint64_t)(uintptr_t)wa.hi.a : (uint64_t)(uintptr_t)wa.cur.a;
+      const int64_t ld = hi ? wa.hi.lda2 : wa.cur.lda2;
+      stA[i] = base + (uint64_t)(dk + r * ld + ((i & 1) ? cA1 : cA0) * 16);
+    }
     if (k0 + 64 > wa.ke) {
       const bool has_next = wa.s + 1 < segN;
-      const Seg nxt = load_seg(segs, has_next ? wa.s + 1 : wa.s);
+      const int64_t sn = has_next ? wa.s + 1 : wa.s;
+      const Seg nxt = load_seg(segs, sn);
+      const Seg nxtI = GRID ? load_seg(segs, sn + dsI) : nxt;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
+        bool hi;
+        const int64_t r = rowA(i, hi);
+        const uint64_t nbase = hi ? (uint64_t)(uintptr_t)nxtI.a : (uint64_t)(uintptr_t)nxt.a;
+        const int64_t nld = hi ? nxtI.lda2 : nxt.lda2;
         const int32_t ka = k0 + 8 * ((i & 1) ? cA1 : cA0);
-        const uint64_t na = (uint64_t)(uintptr_t)nxt.a + (uint64_t)(rowA(i) * nxt.lda2 + (int64_t)(ka - wa.ke) * 2);
+        const uint64_t na = nbase + (uint64_t)(r * nld + (int64_t)(ka - wa.ke) * 2);
         const uint64_t alt = (has_next && ka < KT) ? na : z;
         stA[i] = ka < wa.ke ? stA[i] : alt;
       }
@@ -131,16 +166,27 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   };
   auto stageB_full = [&](int32_t k0) __attribute__((always_inline)) {
     wb.inc_ok = k0 + HB_BK <= wb.ke;
-    const uint64_t b0 = (uint64_t)(uintptr_t)wb.cur.b + (uint64_t)((int64_t)(k0 - wb.ks) * wb.cur.ldb2);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) stB[i] = b0 + (uint64_t)(rowB(i) * wb.cur.ldb2 + colB(i) * 2);
+    for (int i = 0; i < 4; ++i) {
+      bool hi;
+      const int64_t c = colB(i, hi);
+      const uint64_t base = hi ? (uint64_t)(uintptr_t)wb.hi.b : (uint64_t)(uintptr_t)wb.cur.b;
+      const int64_t ld = hi ? wb.hi.ldb2 : wb.cur.ldb2;
+      stB[i] = base + (uint64_t)((int64_t)(k0 - wb.ks + rowB(i)) * ld + c * 2);
+    }
     if (k0 + HB_BK > wb.ke) {
       const bool has_next = wb.s + 1 < segN;
-      const Seg nxt = load_seg(segs, has_next ? wb.s + 1 : wb.s);
+      const int64_t sn = has_next ? wb.s + 1 : wb.s;
+      const Seg nxt = load_seg(segs, sn);
+      const Seg nxtJ = GRID ? load_seg(segs, sn + dsJ) : nxt;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        bool hi;
+        const int64_t c = colB(i, hi);
+        const uint64_t nbase = hi ? (uint64_t)(uintptr_t)nxtJ.b : (uint64_t)(uintptr_t)nxt.b;
+        const int64_t nld = hi ? nxtJ.ldb2 : nxt.ldb2;
         const int32_t kb = k0 + rowB(i);
-        const uint64_t nbp = (uint64_t)(uintptr_t)nxt.b + (uint64_t)((int64_t)(kb - wb.ke) * nxt.ldb2 + colB(i) * 2);
+        const uint64_t nbp = nbase + (uint64_t)((int64_t)(kb - wb.ke) * nld + c * 2);
         const uint64_t alt = (has_next && kb < KT) ? nbp : z;
         stB[i] = kb < wb.ke ? stB[i] : alt;
       }
@@ -236,20 +282,20 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
       } else if (!(ABL & 16) || k0 == 0) {
         stageA_full(k0);
       }
-      advance(wa, k0, 64);
+      advance(wa, k0, 64, dsI);
     }
     if (p + 4 < nst) {
       const int32_t k0 = (int32_t)((p + 4) * HB_BK);
       if (wb.inc_ok && k0 + HB_BK <= wb.ke) {
-        const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2);
+        const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2), dBh = (uint64_t)(HB_BK * wb.hi.ldb2);
         if constexpr (!(ABL & 32)) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) stB[i] += dB;
+          for (int i = 0; i < 4; ++i) stB[i] += hB[i] ? dBh : dB;
         }
       } else if (!(ABL & 32) || k0 == 0) {
         stageB_full(k0);
       }
-      advance(wb, k0, HB_BK);
+      advance(wb, k0, HB_BK, dsJ);
     }
   };
 
@@ -275,7 +321,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
     }
     const bool incB = wb.inc_ok && kB + HB_BK <= wb.ke;
     if (!incB && (!(ABL & 32) || kB == 0)) stageB_full(kB);
-    const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2);
+    const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2), dBh = (uint64_t)(HB_BK * wb.hi.ldb2);
     __builtin_amdgcn_sched_barrier(0);
     wl_seq<32>([&](auto G) __attribute__((always_inline)) {
       constexpr int g = decltype(G)::value, r = g & 3, i = g >> 2;
@@ -287,7 +333,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
         if constexpr (i < 4) {
           if constexpr (q == 0 && !(ABL & 16)) if (incA) { stA[i] += 128; stA[i + 4] += 128; }
         } else {
-          if constexpr (!(ABL & 32)) if (incB) stB[i - 4] += dB;
+          if constexpr (!(ABL & 32)) if (incB) stB[i - 4] += hB[i - 4] ? dBh : dB;
         }
       }
       else if constexpr (r == 2) {
@@ -296,8 +342,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
       } else { if constexpr (!(ABL & 4)) read_b(std::integral_constant<int, 2 * i + 1>{}, Y, lb); }
       __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (q == 0) advance(wa, kA, 64);
-    advance(wb, kB, HB_BK);
+    if constexpr (q == 0) advance(wa, kA, 64, dsI);
+    advance(wb, kB, HB_BK, dsJ);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -307,10 +353,15 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
     __builtin_amdgcn_s_barrier();
     prep_stage(p);
     const int64_t ta = (p + 5) >> 1;
-    const int q = (int)((p + 1) & 1);
+    // (static piece indices: a runtime index into stA puts it in scratch)
     if (ta < ntile) {
+      if ((p + 1) & 1) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pieceA(4 * q + i, (int)ta);
+        for (int i = 4; i < 8; ++i) pieceA(i, (int)ta);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pieceA(i, (int)ta);
+      }
     }
     if (p + 4 < nst) {
 #pragma unroll
@@ -335,20 +386,20 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
     } else {
       stageA_full(k0);
     }
-    advance(wa, k0, 64);
+    advance(wa, k0, 64, dsI);
 #pragma unroll
     for (int i = 0; i < 8; ++i) pieceA(i, (int)ta);
   }
   for (int64_t pb = 0; pb < WL_NB && pb < nst; ++pb) {
     const int32_t k0 = (int32_t)(pb * HB_BK);
     if (wb.inc_ok && k0 + HB_BK <= wb.ke) {
-      const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2);
+      const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2), dBh = (uint64_t)(HB_BK * wb.hi.ldb2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) stB[i] += dB;
+      for (int i = 0; i < 4; ++i) stB[i] += hB[i] ? dBh : dB;
     } else {
       stageB_full(k0);
     }
-    advance(wb, k0, HB_BK);
+    advance(wb, k0, HB_BK, dsJ);
 #pragma unroll
     for (int i = 0; i < 4; ++i) pieceB(i, pb);
   }
@@ -369,13 +420,13 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
     if (p + 4 < nst) {
       const int32_t k0 = (int32_t)((p + 4) * HB_BK);
       if (wb.inc_ok && k0 + HB_BK <= wb.ke) {
-        const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2);
+        const uint64_t dB = (uint64_t)(HB_BK * wb.cur.ldb2), dBh = (uint64_t)(HB_BK * wb.hi.ldb2);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) stB[i] += dB;
+        for (int i = 0; i < 4; ++i) stB[i] += hB[i] ? dBh : dB;
       } else {
         stageB_full(k0);
       }
-      advance(wb, k0, HB_BK);
+      advance(wb, k0, HB_BK, dsJ);
 #pragma unroll
       for (int i = 0; i < 4; ++i) pieceB(i, p + 4);
     }
@@ -409,32 +460,53 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   }
 
   // ---- epilogue: 32x32 C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  char* C = (char*)(uintptr_t)T->c;
-  const int64_t ldc = T->ldc;
+  // (GRID: each element's chunk and its offset inside it)
   const bool accum = T->accumulate != 0;
   const int64_t gn0 = n0 + wc * 128 + (lane & 31);
   const int64_t gm0 = m0 + wr * 128 + 4 * (lane >> 5);
+  // (static indices throughout: an accumulator indexed at run time would put
+  // all of acc in scratch memory, main loop included).  GRID: the four
+  // chunks' (C, ldc) are read once; per element only two selects
+  uint64_t cbase[2][2];
+  int64_t cld[2][2];
+  const cubed_gemm_chain_t* TQ[2][2] = {{T, gt.TJ1}, {gt.TI1, gt.TI1 + (gt.TJ1 - T)}};
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int a = 0; a < (GRID ? 2 : 1); ++a)
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const int64_t gn = gn0 + nb * 32;
-      if (gn >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
+    for (int b = 0; b < (GRID ? 2 : 1); ++b) {
+      cbase[a][b] = (uint64_t)(uintptr_t)TQ[a][b]->c;
+      cld[a][b] = TQ[a][b]->ldc;
+    }
+  wl_seq<16>([&](auto MN) __attribute__((always_inline)) {
+    constexpr int mb = decltype(MN)::value >> 2, nb = decltype(MN)::value & 3;
+    const int64_t gn = gn0 + nb * 32;
+    if (gn < N) {
+      const bool hn = GRID && gn >= gt.nb;
+      const int64_t ln = GRID ? gn - (hn ? gt.nb : gt.J0 * gg.cn) : gn;
+      const uint64_t c0 = GRID && hn ? cbase[0][1] : cbase[0][0];
+      const uint64_t c1 = GRID && hn ? cbase[1][1] : cbase[1][0];
+      const int64_t l0 = GRID && hn ? cld[0][1] : cld[0][0];
+      const int64_t l1 = GRID && hn ? cld[1][1] : cld[1][0];
+      wl_seq<16>([&](auto R) __attribute__((always_inline)) {
+        constexpr int r = decltype(R)::value;
         const int64_t gm = gm0 + mb * 32 + (r & 3) + 8 * (r >> 2);
         if (gm < M) {
+          const bool hm = GRID && gm >= gt.mb;
+          const int64_t lm = GRID ? gm - (hm ? gt.mb : gt.I0 * gg.cm) : gm;
+          const uint64_t C = hm ? c1 : c0;
+          const int64_t ldc = hm ? l1 : l0;
           float v = acc[mb][nb][r];
           if constexpr (OUT_BF16) {
-            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (gm * ldc + gn) * 2);
+            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (uint64_t)(lm * ldc + ln) * 2);
             if (accum) v += bf16_to_f32(*c);
             *c = f32_to_bf16(v);
           } else {
-            CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (gm * ldc + gn) * 4);
+            CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (uint64_t)(lm * ldc + ln) * 4);
             if (accum) v += *c;
             *c = v;
           }
         }
-      }
+      });
     }
+  });
 }

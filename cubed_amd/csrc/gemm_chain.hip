@@ -1071,7 +1071,19 @@ extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cube
   hipStream_t st = (hipStream_t)stream;
   const char* z = (const char*)d_zero;
   static_assert(HB_BM == HF_BM && HB_BN == HF_BN, "one tile size");
-  if (in_dtype == CUBED_BF16 && out_dtype == CUBED_BF16)
+  // bf16: the one-wave full-line kernel (gemm_bf16_w4l.h) when every segment
+  // spans a 64-k A tile, else the ping-pong kernel's grid form
+  bool w4l = in_dtype == CUBED_BF16;
+  for (int64_t i = 0; i < ti * tj && w4l; ++i)
+    for (int64_t s = tasks[i].seg0; s < tasks[i].seg0 + tasks[i].nseg; ++s)
+      if (segs[s].k < 64) { w4l = false; break; }
+  if (w4l && out_dtype == CUBED_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_w4l<true, 4, false, 0, true>), grid, dim3(256), 0, st, d_tasks, d_segs, tm, tn, z,
+                       gg, nullptr);
+  else if (w4l)
+    hipLaunchKernelGGL((k_gemm_bf16_w4l<false, 4, false, 0, true>), grid, dim3(256), 0, st, d_tasks, d_segs, tm, tn, z,
+                       gg, nullptr);
+  else if (in_dtype == CUBED_BF16 && out_dtype == CUBED_BF16)
     hipLaunchKernelGGL((k_gemm_bf16_chain<true, 0, 1, HB_NS, 4, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
   else if (in_dtype == CUBED_BF16)
     hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1, HB_NS, 4, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);

@@ -763,10 +763,11 @@ class GemmLaunch:
 
     GRID = True  # probes set False to time the per-chunk tiling
     # input dtypes that take the grid tiling by default: f32 measured 133.6 TF
-    # grid vs 129-130 per chunk; bf16 1038 vs 1085-1097 (its M slot -- the
-    # fragment reads + staging issue, DESIGN.md -- gets the per-lane chunk
-    # selects), so bf16 keeps per-chunk tiles unless a test opts in
-    GRID_INPUTS = {ir.dtype_code(np.float32)}
+    # grid vs 129-130 per chunk.  bf16 stays per chunk: on config 5 the
+    # one-wave full-line kernel runs 1251-1256 TF per chunk vs 1076-1080 grid
+    # (its grid form keeps per-lane chunk selects live through the K loop;
+    # profiles/r05_gemm_bf16_ab.log, ping-pong grid 1048-1050)
+    GRID_INPUTS = {ir.dtype_code(np.float32)}  # (tools/gemm_ab.sh widens it for A/B runs)
 
     def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None):
         import torch

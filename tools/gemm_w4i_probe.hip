@@ -48,7 +48,9 @@ typedef void (*kfn_s)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 2;
   const int64_t N = argc > 2 ? atoll(argv[2]) : 40000, Cc = 5000, nb = N / Cc;
-  const int64_t slot_in = (Cc * Cc * 2 + 255) / 256 * 256, slot_out = (Cc * Cc * 4 + 255) / 256 * 256;
+  // chunk slot alignment: 256 B, or the executor's 32 B (storage.SLOT_ALIGN) with argv[4] = 32
+  const int64_t al = argc > 4 ? atoll(argv[4]) : 256;
+  const int64_t slot_in = (Cc * Cc * 2 + al - 1) / al * al, slot_out = (Cc * Cc * 4 + al - 1) / al * al;
   char *A, *B, *C0, *C1, *Z;
   CHECK(hipMalloc(&A, slot_in * nb * nb));
   CHECK(hipMalloc(&B, slot_in * nb * nb));
@@ -92,17 +94,17 @@ int main(int argc, char** argv) {
   struct V { const char* name; kfn f; kfn_s fs; int threads; bool check; };
   V vs[] = {
       {"library ping-pong (16x16x32, 8 waves)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
-      {"one wave/SIMD, interleaved (w4i), 4 slots", nullptr, k_gemm_bf16_w4i<false>, 256, true},
       {"w4l: A staged in full 128-B lines", nullptr, k_gemm_bf16_w4l<false>, 256, true},
       {"library ping-pong (again)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
       {"w4l (again)", nullptr, k_gemm_bf16_w4l<false>, 256, true},
 
   };
   unsigned long long* dstamp;
-  CHECK(hipMalloc(&dstamp, (size_t)grid.x * 4 * 2 * 8));
+  CHECK(hipMalloc(&dstamp, (size_t)(grid.x + 4096) * 4 * 2 * 8));
   const int only = argc > 3 ? atoi(argv[3]) : -1;
+  printf("# N %lld, chunk %lld, slot alignment %lld B\n", (long long)N, (long long)Cc, (long long)al);
   for (const V& v : vs) {
-    if (only >= 0 && &v - vs != only) continue;
+    if (only >= 0 && only != 99 && &v - vs != only) continue;
     float best = 1e30f, sum = 0.f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
@@ -154,12 +156,42 @@ int main(int argc, char** argv) {
            cyc / (steps * 32), (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
-  stamped("w4i stamped", k_gemm_bf16_w4i<false, 4, true, 0, 4>);
-  stamped("w4l stamped", k_gemm_bf16_w4l<false, 4, true>);
-  stamped("  w4l ABL no barrier", k_gemm_bf16_w4l<false, 4, true, 1>);
-  stamped("  w4l ABL no fragment reads", k_gemm_bf16_w4l<false, 4, true, 4>);
-  stamped("  w4l ABL A stale", k_gemm_bf16_w4l<false, 4, true, 16>);
-  stamped("  w4l ABL B stale", k_gemm_bf16_w4l<false, 4, true, 32>);
-  stamped("  w4l ABL both stale", k_gemm_bf16_w4l<false, 4, true, 48>);
+  {  // the grid tiling (cubed_gemm_chain_grid) of w4l: 157 x 157 tiles over the 40000^2 output
+    GemmGrid gg{nb, nb, Cc, Cc, N, N};
+    const int64_t gtm = (N + HB_BM - 1) / HB_BM;
+    CHECK(hipMemset(dstamp, 0, (size_t)grid.x * 4 * 2 * 8));
+    for (int r = 0; r < 2; ++r) {
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL((k_gemm_bf16_w4l<false, 4, true, 0, true>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0,
+                         dt1, ds, gtm, gtm, (const char*)Z, gg, dstamp);
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      std::vector<unsigned long long> h((size_t)gtm * gtm * 8);
+      CHECK(hipMemcpy(h.data(), dstamp, h.size() * 8, hipMemcpyDeviceToHost));
+      double cyc = 0, steps = 0;
+      for (size_t i = 0; i < h.size(); i += 2) {
+        cyc += (double)h[i];
+        steps += (double)h[i + 1];
+      }
+      printf("w4l GRID stamped: %.3f ms %.1f TF, main-loop steps per wave %.1f, %.2f cyc/MFMA\n", ms, flop / ms / 1e9,
+             steps / (h.size() / 2), cyc / (steps * 32));
+    }
+    CHECK(hipMemset(dmax, 0, 8));
+    k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
+    float m[2];
+    CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+    printf("   vs library per-chunk: max |diff| %g, max rel %g\n", m[0], m[1]);
+    fflush(stdout);
+  }
+  if (only == 99) {
+    stamped("w4l stamped", k_gemm_bf16_w4l<false, 4, true>);
+    stamped("  w4l ABL no barrier", k_gemm_bf16_w4l<false, 4, true, 1>);
+    stamped("  w4l ABL A stale", k_gemm_bf16_w4l<false, 4, true, 16>);
+    stamped("  w4l ABL B stale", k_gemm_bf16_w4l<false, 4, true, 32>);
+    stamped("  w4l ABL both stale", k_gemm_bf16_w4l<false, 4, true, 48>);
+  }
   return 0;
 }
