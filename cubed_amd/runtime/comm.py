@@ -319,10 +319,16 @@ class LoopbackComm:
             flat.copy_(src)
         return Pending([], [])
 
+    # timing only: reduce / all-reduce / reduce-scatter / all-gather /
+    # broadcast become no-ops (values meaningless), so a rehearsal can time
+    # the step without the local copies that stand in for RCCL's collective
+    skip_collectives = False
+
     def _reduce(self, kind, t):
         if self.record:
             self.records.append((kind, t.detach().clone()))
-        self._copy(t)
+        if not self.skip_collectives:
+            self._copy(t)
 
     def all_reduce_sum(self, t):
         self._reduce("all_reduce_sum", t)
@@ -332,16 +338,20 @@ class LoopbackComm:
 
     def reduce_scatter_sum(self, out, t):
         self._reduce("reduce_scatter_sum", t)
-        out.copy_(t.view(self.world, -1)[self.rank])
+        if not self.skip_collectives:
+            out.copy_(t.view(self.world, -1)[self.rank])
 
     def all_gather(self, out, t):
+        if self.skip_collectives:
+            return
         flat = t.reshape(-1)
         o = out.reshape(-1)
         for r in range(self.world):
             o[r * flat.numel():(r + 1) * flat.numel()].copy_(flat)
 
     def broadcast(self, t, src: int):
-        self._copy(t)
+        if not self.skip_collectives:
+            self._copy(t)
 
     def all_ok(self, ok: bool) -> bool:
         return bool(ok)

@@ -37,6 +37,25 @@ def test_all_gather_fills_every_slot():
     assert out.tolist() == [1, 2, 1, 2, 1, 2]
 
 
+def test_skip_collectives_moves_nothing():
+    """Timing mode: the collectives touch no buffer (records still kept)."""
+    c = LoopbackComm(2, 4, record=True)
+    c.skip_collectives = True
+    t = torch.arange(8, dtype=torch.float64)
+    out = torch.full((2,), -1.0, dtype=torch.float64)
+    c.reduce_scatter_sum(out, t)
+    g = torch.zeros(24, dtype=torch.float64)
+    c.all_gather(g, t)
+    c.all_reduce_sum(t)
+    c.broadcast(t, 0)
+    assert out.tolist() == [-1.0, -1.0] and not g.any()
+    assert c._scratch is None
+    assert [k for k, _ in c.records] == ["reduce_scatter_sum", "all_reduce_sum"]
+    c.skip_collectives = False
+    c.reduce_scatter_sum(out, t)
+    assert out.tolist() == [4.0, 5.0]
+
+
 def test_exchange_alone_writes_every_receive():
     """Without a mesh a rehearsed rank writes each receive (from scratch:
     the arriving bytes' write traffic) and reads nothing of its sends into
