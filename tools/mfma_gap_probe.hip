@@ -143,6 +143,110 @@ __global__ __launch_bounds__(256, 1) void k_gap(const char* __restrict__ src, si
   if (lane == 0) cyc[blockIdx.x * 4 + w] = t1 - t0;
 }
 
+// Two waves per SIMD (512 threads, 256 registers per wave): each wave owns
+// 128 x 64 (8 accumulators), a step = 16 MFMAs + this wave's fillers.  V2:
+// 0 bare | 1 the wave's step reads (8 b128 + 8 tr, one per gap) | 2 reads +
+// 4 glds (the wave's half of the stage) | 3 as 2 + lgkmcnt/vmcnt + s_barrier
+template <int V2>
+__global__ __launch_bounds__(512, 1) void k_gap2(const char* __restrict__ src, size_t src_mask, int iters,
+                                                   unsigned long long* __restrict__ cyc, float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(1024))) char lds_[LDS_BYTES];
+  L3 char* lds = (L3 char*)lds_;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  bf16x8 a[4], b[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    for (int e = 0; e < 8; ++e) a[i][e] = (__bf16)(0.001f * (lane + e + i));
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    for (int e = 0; e < 8; ++e) b[i][e] = (__bf16)(0.002f * (lane - e + i));
+  u32x4 rd = {0, 0, 0, 0};
+  s16x4 rt = {0, 0, 0, 0};
+  const int ra_ = lane & 31;
+  const uint32_t lb = (uint32_t)(uintptr_t)(lds + ra_ * 64 + 16 * (((lane >> 5)) ^ ((ra_ >> 2) & 3)));
+  const int bq = lane >> 4, krow = (bq >> 1) * 8 + ((lane & 15) >> 2);
+  const uint32_t lt = (uint32_t)(uintptr_t)(lds + 16384 + krow * 512 +
+                                            16 * (((bq & 1) * 2 + ((lane & 3) >> 1)) ^ (4 * (krow & 3))) +
+                                            8 * (lane & 1));
+  size_t goff = ((size_t)(blockIdx.x * 8 + w) * 65536 + lane * 16) & src_mask;
+  __syncthreads();
+  unsigned long long t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int it = 0; it < iters; ++it) {
+    u32x4 ra[16];
+    s16x4 rtt[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int mi = (g >> 1) & 3, ni = (g >> 3) & 1;
+      acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi], b[ni], acc[mi][ni], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (V2 >= 1 && (g & 1) == 0)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(ra[g]) : "v"(lb), "i"(0));
+      else
+        ra[g] = u32x4{0, 0, 0, 0};
+      if (V2 >= 1 && (g & 1) == 1)
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(rtt[g]) : "v"(lt));
+      else
+        rtt[g] = s16x4{0, 0, 0, 0};
+      if (V2 >= 2 && (g % 4) == 2) {
+        __builtin_amdgcn_global_load_lds((const G1 void*)(uintptr_t)(src + goff),
+                                         (L3 void*)(lds + (w & 3) * 16384 + (g & 7) * 1024), 16, 0, 0);
+        goff = (goff + 4096) & src_mask;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      rd ^= ra[g];
+      rt ^= rtt[g];
+    }
+    if (V2 == 3) {
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) s += acc[i][j][lane & 15];
+  s += (float)(rd[0] ^ rd[1] ^ rd[2] ^ rd[3]) * 1e-30f + (float)(rt[0] ^ rt[3]) * 1e-30f;
+  sink[blockIdx.x * 512 + threadIdx.x] = s;
+  if (lane == 0) cyc[blockIdx.x * 8 + w] = t1 - t0;
+}
+
+template <int V2>
+void run2(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
+          float* d_sink) {
+  hipLaunchKernelGGL(k_gap2<V2>, dim3(nblk), dim3(512), 0, 0, src, mask, iters, d_cyc, d_sink);  // warm
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(k_gap2<V2>, dim3(nblk), dim3(512), 0, 0, src, mask, iters, d_cyc, d_sink);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> c(nblk * 8);
+  CHECK(hipMemcpy(c.data(), d_cyc, c.size() * 8, hipMemcpyDeviceToHost));
+  std::sort(c.begin(), c.end());
+  const double per = 32.0 * iters;  // two waves x 16 MFMAs per step on one SIMD
+  const double flop = 32768.0 * 16 * iters * 8 * nblk;
+  printf("%-44s cyc/MFMA/SIMD median %6.2f  p90 %6.2f  kernel %8.3f ms  %7.1f TF  (clk %.2f GHz)\n", name,
+         c[c.size() / 2] / per, c[c.size() * 9 / 10] / per, ms, flop / (ms * 1e-3) / 1e12,
+         c[c.size() / 2] / (ms * 1e-3) / 1e9);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+}
+
 template <int V>
 void run(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
          float* d_sink) {
@@ -175,8 +279,8 @@ int main(int argc, char** argv) {
   const int nblk = ncu;
   unsigned long long* d_cyc;
   float* d_sink;
-  CHECK(hipMalloc(&d_cyc, nblk * 4 * 8));
-  CHECK(hipMalloc(&d_sink, nblk * 256 * 4));
+  CHECK(hipMalloc(&d_cyc, nblk * 8 * 8));
+  CHECK(hipMalloc(&d_sink, nblk * 512 * 4));
   // glds sources: L2-resident (4 MiB per XCD-ish) and HBM-streamed (1 GiB)
   for (size_t bytes : {(size_t)4 << 20, (size_t)1 << 30}) {
     char* src;
@@ -198,6 +302,12 @@ int main(int argc, char** argv) {
     run<10>("+1 ds_read_b64_tr_b16 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
     run<11>("+1 ds_read_b128 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
     run<12>("+1 b128 + 1 tr every gap", src, mask, iters, nblk, d_cyc, d_sink);
+    if (argc > 2) {  // two waves per SIMD
+      run2<0>("2 waves/SIMD: bare", src, mask, iters, nblk, d_cyc, d_sink);
+      run2<1>("2 waves/SIMD: 8 b128 + 8 tr per wave-step", src, mask, iters, nblk, d_cyc, d_sink);
+      run2<2>("2 waves/SIMD: + 4 glds per wave-step", src, mask, iters, nblk, d_cyc, d_sink);
+      run2<3>("2 waves/SIMD: + waits + s_barrier", src, mask, iters, nblk, d_cyc, d_sink);
+    }
     CHECK(hipFree(src));
   }
   return 0;

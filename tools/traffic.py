@@ -13,6 +13,11 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section),
 gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B/lane stores.
 The median over the kernel's dispatches is reported.
+
+    python tools/traffic.py --compact DIR COUNTER > DIR.json
+folds one pass's CSVs (which can exceed what a GPU call brings back) into
+{base name: {grid: [value per dispatch]}}; a .json in place of a directory
+above is read as such a file.
 """
 import csv
 import glob
@@ -31,10 +36,31 @@ def base_name(name):
     return n.split("::")[-1]
 
 
+def compact(d, counter):
+    vals = {}
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                name = base_name(row.get("Kernel_Name") or row.get("Kernel-Name") or "")
+                grid = row.get("Grid_Size") or row.get("Grid_Size_X") or ""
+                key = (name, grid, path, row.get("Dispatch_Id") or row.get("Correlation_Id") or str(len(vals)))
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    out = {}
+    for (name, grid, _, _), v in vals.items():
+        out.setdefault(name, {}).setdefault(grid, []).append(v)
+    return out
+
+
 def per_dispatch(d, counter, kernel_sub):
     grid = None
     if "@" in kernel_sub:
         kernel_sub, grid = kernel_sub.split("@", 1)
+    if d.endswith(".json"):
+        with open(d) as f:
+            by_grid = json.load(f).get(kernel_sub, {})
+        return [v for g, vs in by_grid.items() if grid is None or g == grid for v in vs]
     vals = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         with open(path) as f:
@@ -50,6 +76,10 @@ def per_dispatch(d, counter, kernel_sub):
 
 
 def main():
+    if sys.argv[1] == "--compact":
+        json.dump(compact(sys.argv[2], sys.argv[3]), sys.stdout)
+        print()
+        return
     fetch_dir, write_dir = sys.argv[1], sys.argv[2]
     out = {}
     for spec in sys.argv[3:]:
