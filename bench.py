@@ -891,11 +891,14 @@ def var_extra(args, ex, rank, world):
         m = getattr(xp, fname)(u * v, axis=0)
         plan = arrays_to_plan(m)
         step = step_fn(plan, ex, [m], (u, v))
-        step()
-        step()
-        dt, summ = timed_launches(ex, step, 10, world)
+        # var's first ~15 steps run up to 20 % slower than its steady state
+        # (tools/var_timing_probe.py: 5 steps 1.43 ms, then 1.204 ms = mean's
+        # step) -- warm 15 steps, time 20
+        for _ in range(15):
+            step()
+        dt, summ = timed_launches(ex, step, 20, world)
         r = dict(metric=f"{fname}(u*v, axis=0) effective input GB/s", value=round((u.nbytes + v.nbytes) / dt / 1e9, 1),
-                 ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ), **overhead(dt, summ, 10))
+                 ms=round(dt * 1e3, 4), launches_ms=fmt_launches(summ), **overhead(dt, summ, 20))
         if world == 1:
             key, ms = dominant(summ, "FusedLaunch")
             r["roofline"] = roofline_hbm(u.nbytes + v.nbytes, ms, f"{fname}_stream", args,

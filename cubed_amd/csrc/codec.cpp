@@ -25,7 +25,9 @@
 // the Blosc container is restated here).  blosclz and snappy are restated
 // from their published stream formats (below); no fixture written by
 // numcodecs exists in this image, so their parity is unpinned.  Bit shuffle
-// is refused.
+// (flag 0x04, numcodecs Blosc(shuffle=BITSHUFFLE)) is restated from the
+// bitshuffle algorithm Blosc 1.x bundles (bshuf_trans_bit_elem: byte
+// transpose, 8x8 bit transpose, bit-row transpose) -- also unpinned.
 // The encoder writes lz4 with byte shuffle and unsplit blocks (flag 0x10),
 // which every Blosc >= 1.x decoder reads.  Also the standalone numcodecs
 // "zstd" (one zstd frame) and "lz4" (a 4-byte size + one LZ4 block) chunks.
@@ -64,6 +66,45 @@ void byte_shuffle(const uint8_t* in, uint8_t* out, int64_t n, int ts) {
     for (int64_t j = 0; j < rows; ++j)
         for (int i = 0; i < ts; ++i) out[int64_t(i) * rows + j] = in[j * ts + i];
     std::memcpy(out + rows * ts, in + rows * ts, size_t(n - rows * ts));
+}
+
+// The 8x8 bit-matrix transpose of bitshuffle's TRANS_BIT_8X8 (little-endian
+// rows = bytes): bit 8r + c <-> bit 8c + r.  Its own inverse.
+inline uint64_t trans_bit_8x8(uint64_t x) {
+    uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x = x ^ t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x = x ^ t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    return x ^ t ^ (t << 28);
+}
+
+// Blosc 1.x bitunshuffle of one block of n bytes (shuffle.c): with
+// size = n / ts elements a multiple of 8, bit j of byte b of element e sits at
+// bit e % 8 of byte e / 8 of bit-row 8 b + j (rows of size / 8 bytes) -- the
+// forward bshuf_trans_bit_elem is a byte transpose ([e][b] -> [b][e]), an
+// 8x8 bit transpose of every 8 bytes (byte m of the result = bit m of the 8
+// input bytes) and a transpose of the [8][ts] bit-rows to [ts][8].  The
+// trailing n % ts bytes stay in place.  Otherwise (size % 8 != 0, only the
+// short last block of a frame) the block is stored as is.
+void bit_unshuffle(const uint8_t* in, uint8_t* out, int64_t n, int ts) {
+    const int64_t size = n / ts;
+    if (size % 8) {
+        std::memcpy(out, in, size_t(n));
+        return;
+    }
+    const int64_t rowb = size / 8;
+    for (int b = 0; b < ts; ++b) {
+        const uint8_t* rows = in + int64_t(b) * 8 * rowb;
+        for (int64_t g = 0; g < rowb; ++g) {
+            uint64_t x = 0;
+            for (int j = 0; j < 8; ++j) x |= uint64_t(rows[int64_t(j) * rowb + g]) << (8 * j);
+            x = trans_bit_8x8(x);  // byte m = byte b of element 8 g + m
+            uint8_t* o = out + (8 * g) * ts + b;
+            for (int m = 0; m < 8; ++m) o[int64_t(m) * ts] = uint8_t(x >> (8 * m));
+        }
+    }
+    std::memcpy(out + size * ts, in + size * ts, size_t(n - size * ts));
 }
 
 void byte_unshuffle(const uint8_t* in, uint8_t* out, int64_t n, int ts) {
@@ -367,7 +408,6 @@ int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t d
     const int flags = s[2], ts = s[3] ? s[3] : 1;
     const int64_t nbytes = rd32(s + 4), blocksize = rd32(s + 8), cbytes = rd32(s + 12);
     if (nbytes != dstlen || cbytes > srclen) return CUBED_E_ARG;
-    if (flags & 0x04) return CUBED_E_UNSUPPORTED;  // bit shuffle
     if (flags & 0x02) {
         if (kHeader + nbytes > srclen) return CUBED_E_CODEC;
         std::memcpy(d, s + kHeader, size_t(nbytes));
@@ -377,9 +417,12 @@ int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t d
     if (blocksize <= 0) return CUBED_E_CODEC;
     const int codec = flags >> 5;
     const bool shuffled = (flags & 0x01) && ts > 1;
+    // (blosc_d: the byte shuffle flag wins; bit shuffle needs a block of at
+    // least one element)
+    const bool bitsh = !(flags & 0x01) && (flags & 0x04);
     const int64_t nblocks = (nbytes + blocksize - 1) / blocksize;
     if (kHeader + 4 * nblocks > srclen) return CUBED_E_CODEC;
-    std::vector<uint8_t> tmp(shuffled ? size_t(blocksize) : 0);
+    std::vector<uint8_t> tmp(shuffled || bitsh ? size_t(blocksize) : 0);
     for (int64_t b = 0; b < nblocks; ++b) {
         const bool leftover = (b == nblocks - 1) && (nbytes % blocksize);
         const int64_t bsize = leftover ? nbytes % blocksize : blocksize;
@@ -387,7 +430,8 @@ int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t d
         const int nsplits = split ? ts : 1;
         const int64_t neblock = bsize / nsplits;
         int64_t pos = rd32(s + kHeader + 4 * b);
-        uint8_t* out = shuffled ? tmp.data() : d + b * blocksize;
+        const bool unbit = bitsh && bsize >= ts;
+        uint8_t* out = shuffled || unbit ? tmp.data() : d + b * blocksize;
         for (int j = 0; j < nsplits; ++j) {
             if (pos + 4 > srclen) return CUBED_E_CODEC;
             const int64_t csize = rd32(s + pos);
@@ -398,6 +442,7 @@ int cubed_blosc_decompress(const void* src, int64_t srclen, void* dst, int64_t d
             pos += csize;
         }
         if (shuffled) byte_unshuffle(tmp.data(), d + b * blocksize, bsize, ts);
+        if (unbit) bit_unshuffle(tmp.data(), d + b * blocksize, bsize, ts);
     }
     return 0;
 }

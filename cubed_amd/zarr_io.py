@@ -336,11 +336,19 @@ def _blosc_decompress(data: bytes, out_u8: np.ndarray):
             warnings.warn(f"decoding a Blosc frame with {codec} streams: this decoder is restated from the "
                           f"published {codec} format and has not been checked against frames written by "
                           f"numcodecs (parity unpinned, DESIGN.md 'Zarr sources and sinks')", stacklevel=3)
+        if data[2] & 0x04 and not data[2] & 0x01 and "bitshuffle" not in _WARNED:
+            import warnings
+
+            _WARNED.add("bitshuffle")
+            warnings.warn("decoding a bit-shuffled Blosc frame: the bit unshuffle is restated from the "
+                          "bitshuffle algorithm Blosc 1.x bundles and has not been checked against frames "
+                          "written by numcodecs (parity unpinned, DESIGN.md 'Zarr sources and sinks')",
+                          stacklevel=3)
     L = nat.lib()
     rc = L.cubed_blosc_decompress(data, len(data), out_u8.ctypes.data, out_u8.size)
     if rc != 0:
-        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec/shuffle (blosclz/lz4/snappy/zlib/zstd "
-                                                 "with byte or no shuffle; bit shuffle is not decoded)",
+        what = {-6: "malformed blosc frame", -7: "unsupported blosc codec (blosclz/lz4/snappy/zlib/zstd are "
+                                                 "decoded)",
                 -1: "size mismatch"}.get(rc, f"error {rc}")
         raise ValueError(f"blosc decode failed: {what}")
 

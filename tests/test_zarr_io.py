@@ -93,6 +93,8 @@ def py_blosc_decode(frame: bytes, dec=None) -> bytes:
             rows = n // ts
             a = np.frombuffer(bytes(blk[:rows * ts]), np.uint8).reshape(ts, rows).T.reshape(-1)
             blk = bytearray(a.tobytes()) + blk[rows * ts:]
+        elif flags & 4 and n >= ts:
+            blk = bytearray(bitunshuffle(bytes(blk), ts))
         out += blk
     return bytes(out)
 
@@ -116,19 +118,48 @@ def shuffle(block: bytes, ts: int) -> bytes:
     return a.tobytes() + block[rows * ts:]
 
 
-def frame(data: bytes, ts: int, bsize: int, codec: int, do_shuffle: bool, dont_split: bool,
+def bitshuffle(block: bytes, ts: int) -> bytes:
+    """Blosc 1.x bit shuffle of one block, written from the bitshuffle
+    algorithm's definition with numpy bit unpacking (independent of the C
+    decoder): bit-row 8 b + j holds bit j of byte b of every element, element
+    e at bit e % 8 of byte e / 8; blocks whose element count is not a multiple
+    of 8 are stored as they are; trailing bytes stay."""
+    size = len(block) // ts
+    if size % 8:
+        return block
+    a = np.frombuffer(block[:size * ts], np.uint8).reshape(size, ts)
+    bits = np.unpackbits(a, axis=1, bitorder="little").reshape(size, ts, 8)   # [e][b][j]
+    rows = np.packbits(bits.transpose(1, 2, 0), axis=2, bitorder="little")    # [b][j][e/8]
+    return rows.tobytes() + block[size * ts:]
+
+
+def bitunshuffle(block: bytes, ts: int) -> bytes:
+    size = len(block) // ts
+    if size % 8:
+        return block
+    rows = np.frombuffer(block[:size * ts], np.uint8).reshape(ts, 8, size // 8)
+    bits = np.unpackbits(rows, axis=2, bitorder="little")                     # [b][j][e]
+    a = np.packbits(bits.transpose(2, 0, 1), axis=2, bitorder="little")       # [e][b][1]
+    return a.reshape(-1).tobytes() + block[size * ts:]
+
+
+def frame(data: bytes, ts: int, bsize: int, codec: int, do_shuffle, dont_split: bool,
           encode) -> bytes:
-    """Assemble a Blosc 1.x frame from the published layout."""
+    """Assemble a Blosc 1.x frame from the published layout (``do_shuffle``:
+    False / True (byte) / "bit")."""
     nbytes = len(data)
     nblocks = -(-nbytes // bsize)
-    flags = (codec << 5) | (1 if do_shuffle else 0) | (0x10 if dont_split else 0)
+    bit = do_shuffle == "bit"
+    flags = (codec << 5) | (4 if bit else 1 if do_shuffle else 0) | (0x10 if dont_split else 0)
     body = bytearray()
     starts = []
     base = 16 + 4 * nblocks
     for b in range(nblocks):
         blk = data[b * bsize:(b + 1) * bsize]
         leftover = len(blk) != bsize
-        if do_shuffle and ts > 1:
+        if bit and len(blk) >= ts:
+            blk = bitshuffle(blk, ts)
+        elif do_shuffle and not bit and ts > 1:
             blk = shuffle(blk, ts)
         split = not dont_split and not leftover and ts <= 16 and bsize // ts >= 128
         ns = ts if split else 1
@@ -205,8 +236,8 @@ def test_decoder_memcpyed_and_errors(built):
     with pytest.raises(ValueError):
         native_decode(bytes(bad), 8192)
     bitshuffled = bytes([2, 1, 0x04 | (1 << 5), 4]) + struct.pack("<iii", 8, 8, 40) + bytes(24)
-    with pytest.raises(ValueError, match="unsupported"):
-        native_decode(bitshuffled, 8)
+    with pytest.raises(ValueError, match="malformed"):
+        native_decode(bitshuffled, 8)  # block start 0: points into the header
 
 
 # ----------------------------------------------------------------- encoder
@@ -283,11 +314,11 @@ def test_zarr_refuses_what_it_cannot_decode(tmp_path, built):
     json.dump(meta, open(tmp_path / "q.zarr" / ".zarray", "w"))
     with pytest.raises(NotImplementedError, match="snappy"):
         Z.open_array(str(tmp_path / "q.zarr"))
-    # bit-shuffled blosc frames: refused with a clear error
+    # an unknown blosc stream codec (flags >> 5 = 6): refused with a clear error
     data = patterned(4096)
     fr = bytearray(frame(data, 4, 4096, 3, True, True, lambda b: zlib.compress(b, 5)))
-    fr[2] |= 0x04  # bit shuffle
-    with pytest.raises(ValueError, match="bit shuffle"):
+    fr[2] = (fr[2] & 0x1F) | (6 << 5)
+    with pytest.raises(ValueError, match="unsupported"):
         native_decode(bytes(fr), len(data))
     # a corrupt blosclz stream (match before any output): malformed, not wrong data
     bad = bytes([0x00, 0x41, 0x20, 0x05])  # literal "A", then a match at distance 6
@@ -643,3 +674,55 @@ def test_chunk_io_retries_restate_the_threads_executor():
     calls.clear()
     with pytest.raises(IOError, match="fail 1"):
         with_retries(flaky(1), 1, retries=0)
+
+
+# ----------------------------------------------------------------- bit shuffle (Blosc flag 0x04)
+
+
+def test_bitshuffle_by_hand(built):
+    """Hand-built bit-shuffled blocks: typesize 1, element 0 = 0b11 -> bit-rows
+    0 and 1 each hold element 0's bit; typesize 2, element 1 = 0x0100 (byte 1
+    bit 0) -> bit-row 8, bit 1.  Parity with numcodecs-written frames is
+    unpinned (no such fixture in this image)."""
+    data = bytes([0x03, 0, 0, 0, 0, 0, 0, 0])
+    assert bitshuffle(data, 1) == bytes([0x01, 0x01, 0, 0, 0, 0, 0, 0])
+    data2 = struct.pack("<8H", 0, 0x0100, 0, 0, 0, 0, 0, 0)
+    exp2 = bytearray(16)
+    exp2[8] = 0x02
+    assert bitshuffle(data2, 2) == bytes(exp2)
+    for d, ts, shuffled in ((data, 1, bytes([0x01, 0x01, 0, 0, 0, 0, 0, 0])), (data2, 2, bytes(exp2))):
+        blk = lz4_literals(shuffled)
+        fr = bytes([2, 1, 0x04 | 0x10 | (1 << 5), ts]) + struct.pack("<iii", len(d), len(d), 24 + len(blk))
+        fr += struct.pack("<i", 20) + struct.pack("<i", len(blk)) + blk
+        assert native_decode(fr, len(d)) == d
+
+
+@pytest.mark.parametrize("ts, bsize, n", [
+    (4, 4096, 4 * 2500),       # leftover block of 1808 B = 452 elements (not a multiple of 8: stored as is)
+    (8, 2048, 8 * 1000),       # leftover 1664 B = 208 elements (bit-shuffled)
+    (2, 256, 2 * 777 + 1),     # odd byte count: a trailing byte past the elements
+    (1, 1000, 5000),
+    (4, 4096, 4 * 4096),       # split streams (bsize / ts >= 128)
+])
+@pytest.mark.parametrize("codec", [1, 3])
+def test_bitshuffled_frames_round_trip(built, ts, bsize, n, codec):
+    data = patterned(n // 4 + 1)[:n]
+    enc = lz4_literals if codec == 1 else (lambda b: zlib.compress(b, 5))
+    for dont_split in (True, False):
+        fr = frame(data, ts, bsize, codec, "bit", dont_split, enc)
+        assert py_blosc_decode(fr, None if codec == 1 else (lambda b, k: zlib.decompress(b))) == data
+        assert native_decode(fr, len(data)) == data
+
+
+def test_bitshuffle_warns_once(built):
+    Z._WARNED.discard("bitshuffle")
+    data = patterned(1024)
+    fr = frame(data, 4, 1024, 1, "bit", True, lz4_literals)
+    import warnings
+
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        native_decode(fr, len(data))
+        native_decode(fr, len(data))
+    msgs = [str(x.message) for x in w if "bit-shuffled" in str(x.message)]
+    assert len(msgs) == 1 and "unpinned" in msgs[0]
