@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <utility>
 #include <cstdlib>
 #include <vector>
 
@@ -55,6 +56,8 @@ __device__ __forceinline__ int filler(int g) {
     case 10: return (g % 2 == 0) ? F_TR : 0;
     case 11: return (g % 2 == 0) ? F_B128 : 0;
     case 12: return F_B128 | F_TR;
+    case 13: return (g % 2 == 0) ? F_B128 : ((g % 4 == 1) ? F_GLDS : 0);  // B^T step: 16 b128 + 8 glds
+    case 14: return (g % 2 == 0) ? F_B128 : 0;                             // 16 b128 only
     default: return 0;
   }
 }
@@ -247,6 +250,141 @@ void run2(const char* name, const char* src, size_t mask, int iters, int nblk, u
   CHECK(hipEventDestroy(e1));
 }
 
+// ---- k_flow<F>: the w4l main loop's data flow without global memory
+// semantics: two fragment sets, step p's 32 MFMAs read set X while this
+// step's fillers read LDS into set Y (the next step's operands) -- no VALU
+// consumes a read (k_gap above XORs every read into a sink after the step:
+// 4 VALU per b128, which is what its "per filler" cycles mostly measured).
+// F bits: 1 the 8 A ds_read_b128 | 2 the 16 B ds_read_b64_tr_b16 (or, with
+// 16, 8 B ds_read_b128: a B^T image) | 4 the 8 LDS-DMA pieces (+ one 64-bit
+// source increment each, every 4th gap) | 8 s_waitcnt + s_barrier per step.
+template <int J>
+using ic = std::integral_constant<int, J>;
+template <typename Fn, int... I>
+__device__ __forceinline__ void seq_(Fn&& f, std::integer_sequence<int, I...>) {
+  (f(ic<I>{}), ...);
+}
+template <int N, typename Fn>
+__device__ __forceinline__ void seq(Fn&& f) {
+  seq_(f, std::make_integer_sequence<int, N>{});
+}
+struct Fr {
+  bf16x8 a[4][2], bt[4][2];
+  s16x4 bl[4][2], bh[4][2];
+};
+template <int F>
+__device__ __forceinline__ void flow_step(const Fr& X, Fr& Y, f32x16 (&acc)[4][4], uint32_t la, uint32_t lbt,
+                                          const char* src, const char*& gp, size_t mask, L3 char* lds, int w) {
+  seq<32>([&](auto G) {
+    constexpr int g = decltype(G)::value, kh = g >> 4, mb = (g >> 2) & 3, nb = g & 3;
+    if constexpr (F & 16) {
+      acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X.a[mb][kh], X.bt[nb][kh], acc[mb][nb], 0, 0, 0);
+    } else {
+      const bf16x8 b = __builtin_bit_cast(bf16x8, __builtin_shufflevector(X.bl[nb][kh], X.bh[nb][kh], 0, 1, 2, 3,
+                                                                          4, 5, 6, 7));
+      acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X.a[mb][kh], b, acc[mb][nb], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int r = g & 3, i = g >> 2;
+    if constexpr (r == 0 && (F & 1)) {
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.a[i & 3][i >> 2]) : "v"(la), "i"((i & 3) * 4096));
+    } else if constexpr ((r == 1 || r == 3) && (F & 2)) {
+      constexpr int j = 2 * i + (r == 3), jn = (j >> 1) & 3, jk = j >> 3;
+      if constexpr (F & 16) {
+        if constexpr (r == 1)  // B^T: one b128 per fragment
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.bt[jn][jk]) : "v"(lbt), "i"(jn * 4096 + jk * 16384));
+      } else if constexpr (j & 1) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(Y.bh[jn][jk]) : "v"(lbt), "i"(jk * 8192 + 2048));
+      } else {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(Y.bl[jn][jk]) : "v"(lbt), "i"(jk * 8192));
+      }
+    } else if constexpr (r == 2 && (F & 4)) {
+      __builtin_amdgcn_global_load_lds((const G1 void*)gp, (L3 void*)(lds + 65536 + w * 8192 + (i & 7) * 1024), 16,
+                                       0, 0);
+      gp += 4096;  // one 64-bit increment per piece, as the library's sources
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  if constexpr (F & 4) gp = src + ((size_t)(gp - src) & mask);
+  if constexpr (F & 8) {
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int F>
+__global__ __launch_bounds__(256, 1) void k_flow(const char* __restrict__ src, size_t src_mask, int iters,
+                                                   unsigned long long* __restrict__ cyc, float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(1024))) char lds_[LDS_BYTES];
+  L3 char* lds = (L3 char*)lds_;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < LDS_BYTES / 4; i += 256) ((L3 float*)lds)[i] = 0.001f * (i & 255);
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{};
+  Fr f0, f1;
+  for (int i = 0; i < 4; ++i)
+    for (int k = 0; k < 2; ++k) {
+      for (int e = 0; e < 8; ++e) f0.a[i][k][e] = f1.a[i][k][e] = (__bf16)(0.001f * (lane + e + i));
+      f0.bl[i][k] = f1.bl[i][k] = s16x4{1, 2, 3, 4};
+      f0.bh[i][k] = f1.bh[i][k] = s16x4{5, 6, 7, 8};
+      f0.bt[i][k] = f1.bt[i][k] = f0.a[i][k];
+    }
+  // the library's conflict-free fragment addresses (gemm_bf16_w4l.h)
+  const int ra = (w >> 1) * 128 + (lane & 31);
+  const uint32_t la = (uint32_t)(uintptr_t)(lds + (ra & 127) * 128 + 16 * ((lane >> 5) ^ ((ra >> 1) & 7)));
+  const int bq = lane >> 4, krow = (bq >> 1) * 8 + ((lane & 15) >> 2);
+  const uint32_t lbt = (uint32_t)(uintptr_t)(lds + 16384 * 0 + krow * 512 +
+                                             16 * ((((w & 1) * 16) + (bq & 1) * 2 + ((lane & 3) >> 1)) ^ (4 * (krow & 3))) +
+                                             8 * (lane & 1));
+  const char* gp = src + (((size_t)(blockIdx.x * 4 + w) * 65536 + lane * 16) & src_mask);
+  __syncthreads();
+  unsigned long long t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int it = 0; it < iters; it += 2) {
+    flow_step<F>(f0, f1, acc, la, lbt, src, gp, src_mask, lds, w);
+    flow_step<F>(f1, f0, acc, la, lbt, src, gp, src_mask, lds, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += acc[i][j][lane & 15];
+  sink[blockIdx.x * 256 + threadIdx.x] = s;
+  if (lane == 0) cyc[blockIdx.x * 4 + w] = t1 - t0;
+}
+
+template <int F>
+void runf(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
+          float* d_sink) {
+  hipLaunchKernelGGL(k_flow<F>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);  // warm
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(k_flow<F>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> c(nblk * 4);
+  CHECK(hipMemcpy(c.data(), d_cyc, c.size() * 8, hipMemcpyDeviceToHost));
+  std::sort(c.begin(), c.end());
+  const double per = 32.0 * iters;
+  const double flop = 32768.0 * 32 * iters * 4 * nblk;
+  printf("flow %-39s cyc/MFMA median %6.2f  p90 %6.2f  kernel %8.3f ms  %7.1f TF  (clk %.2f GHz)\n", name,
+         c[c.size() / 2] / per, c[c.size() * 9 / 10] / per, ms, flop / (ms * 1e-3) / 1e12,
+         c[c.size() / 2] / (ms * 1e-3) / 1e9);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+}
+
 template <int V>
 void run(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
          float* d_sink) {
@@ -302,6 +440,18 @@ int main(int argc, char** argv) {
     run<10>("+1 ds_read_b64_tr_b16 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
     run<11>("+1 ds_read_b128 every 2nd gap", src, mask, iters, nblk, d_cyc, d_sink);
     run<12>("+1 b128 + 1 tr every gap", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<0>("bare (two fragment sets)", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<1>("8 A b128 reads", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<2>("16 B tr_b16 reads", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<3>("24 reads (A + B)", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<4>("8 LDS-DMA pieces", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<7>("24 reads + 8 DMA", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<15>("24 reads + 8 DMA + wait/barrier", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<8>("wait/barrier only", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<19>("B^T: 16 b128 reads", src, mask, iters, nblk, d_cyc, d_sink);
+    runf<31>("B^T: 16 b128 + 8 DMA + wait/barrier", src, mask, iters, nblk, d_cyc, d_sink);
+    run<13>("B^T step: 16 b128 + 8 glds, 1/gap", src, mask, iters, nblk, d_cyc, d_sink);
+    run<14>("16 b128 (every 2nd gap)", src, mask, iters, nblk, d_cyc, d_sink);
     if (argc > 2) {  // two waves per SIMD
       run2<0>("2 waves/SIMD: bare", src, mask, iters, nblk, d_cyc, d_sink);
       run2<1>("2 waves/SIMD: 8 b128 + 8 tr per wave-step", src, mask, iters, nblk, d_cyc, d_sink);
