@@ -18,6 +18,7 @@ thread_local char g_err[512];
 }
 #include "../cubed_amd/csrc/gemm_chain.hip"
 #include "gemm_bf16_w4i.h"
+#include "gemm_bf16_w4t.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -27,6 +28,28 @@ __global__ void k_fill(uint16_t* p, int64_t n, uint32_t seed) {
     h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
     const float v = (float)(h >> 8) * (1.0f / 16777216.0f);  // U[0, 1) as config 5
     p[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+
+// B^T chunks for the w4t kernel: dst (n, k) = src (k, n) of one 5000^2 chunk
+// per blockIdx.y (64 x 64 tiles through LDS)
+__global__ void k_transpose(const uint16_t* src, uint16_t* dst, int64_t C, int64_t slot_elems) {
+  __shared__ uint16_t tile[64][65];
+  const uint16_t* s = src + blockIdx.y * slot_elems;
+  uint16_t* d = dst + blockIdx.y * slot_elems;
+  const int64_t tiles = (C + 63) / 64;
+  for (int64_t tt = blockIdx.x; tt < tiles * tiles; tt += gridDim.x) {
+    const int64_t r0 = (tt / tiles) * 64, c0 = (tt % tiles) * 64;
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+      const int64_t r = r0 + i / 64, c = c0 + i % 64;
+      tile[i / 64][i % 64] = (r < C && c < C) ? s[r * C + c] : 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+      const int64_t r = c0 + i / 64, c = r0 + i % 64;  // dst row = src column
+      if (r < C && c < C) d[r * C + c] = tile[i % 64][i / 64];
+    }
+    __syncthreads();
   }
 }
 
@@ -99,6 +122,56 @@ int main(int argc, char** argv) {
       {"w4l (again)", nullptr, k_gemm_bf16_w4l<false>, 256, true},
 
   };
+  // B^T chunks and a segment table pointing at them (w4t)
+  char* BT;
+  CHECK(hipMalloc(&BT, slot_in * nb * nb));
+  k_transpose<<<dim3(1024, (unsigned)(nb * nb)), 256>>>((const uint16_t*)B, (uint16_t*)BT, Cc, slot_in / 2);
+  CHECK(hipGetLastError());
+  std::vector<cubed_gemm_seg_t> segsT(segs);
+  for (auto& g : segsT) g.b = (int64_t)(uintptr_t)(BT + ((char*)(uintptr_t)g.b - B));
+  cubed_gemm_seg_t* dsT;
+  CHECK(hipMalloc(&dsT, sizeof(cubed_gemm_seg_t) * segsT.size()));
+  CHECK(hipMemcpy(dsT, segsT.data(), sizeof(cubed_gemm_seg_t) * segsT.size(), hipMemcpyHostToDevice));
+  CHECK(hipDeviceSynchronize());
+  auto run_t = [&](const char* name, bool stamp, kfn_s fst = nullptr) {
+    unsigned long long* st = nullptr;
+    if (stamp) CHECK(hipMalloc(&st, (size_t)grid.x * 4 * 2 * 8));
+    float best = 1e30f;
+    for (int r = 0; r < reps + 1; ++r) {
+      CHECK(hipEventRecord(e0));
+      if (stamp)
+        hipLaunchKernelGGL(fst ? fst : (kfn_s)(k_gemm_bf16_w4t<false, 4, true>), grid, dim3(256), 0, 0, dt1, dsT,
+                           tm, tn, (const char*)Z, GemmGrid{}, st);
+      else
+        hipLaunchKernelGGL((k_gemm_bf16_w4t<false>), grid, dim3(256), 0, 0, dt1, dsT, tm, tn, (const char*)Z,
+                           GemmGrid{}, (unsigned long long*)nullptr);
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-40s best %9.3f ms %7.1f TF\n", name, best, flop / best / 1e9);
+    if (stamp) {
+      std::vector<unsigned long long> h((size_t)grid.x * 8);
+      CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+      double cyc = 0, steps = 0;
+      for (size_t i = 0; i < h.size(); i += 2) {
+        cyc += (double)h[i];
+        steps += (double)h[i + 1];
+      }
+      printf("   main loop %6.2f cyc/MFMA  clock ~%.2f GHz\n", cyc / (steps * 32),
+             (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (best * 1e-3) / 1e9);
+      CHECK(hipFree(st));
+    }
+    CHECK(hipMemset(dmax, 0, 8));
+    k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
+    float m[2];
+    CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+    printf("   vs library ping-pong: max |diff| %g, max rel %g\n", m[0], m[1]);
+    fflush(stdout);
+  };
   unsigned long long* dstamp;
   CHECK(hipMalloc(&dstamp, (size_t)(grid.x + 4096) * 4 * 2 * 8));
   const int only = argc > 3 ? atoi(argv[3]) : -1;
@@ -156,6 +229,28 @@ int main(int argc, char** argv) {
            cyc / (steps * 32), (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
+  if (only == 98 || only < 0) {
+    {  // timing of the transpose (one-off per matmul)
+      CHECK(hipEventRecord(e0));
+      k_transpose<<<dim3(1024, (unsigned)(nb * nb)), 256>>>((const uint16_t*)B, (uint16_t*)BT, Cc, slot_in / 2);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      printf("probe transpose of B (all chunks): %.3f ms\n", ms);
+    }
+    hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1>), grid, dim3(512), 0, 0, dt0, ds, tm, tn, (const char*)Z,
+                       GemmGrid{});  // the library ping-pong result (C0) to compare with
+    run_t("w4t: B^T staged like A, b128 B reads", false);
+    run_t("w4t stamped", true);
+    run_t("  w4t ABL no barrier", true, k_gemm_bf16_w4t<false, 4, true, 1>);
+    run_t("  w4t ABL no vmcnt wait", true, k_gemm_bf16_w4t<false, 4, true, 2>);
+    run_t("  w4t ABL A stale", true, k_gemm_bf16_w4t<false, 4, true, 16>);
+    run_t("  w4t ABL B^T stale", true, k_gemm_bf16_w4t<false, 4, true, 32>);
+    run_t("  w4t ABL both stale", true, k_gemm_bf16_w4t<false, 4, true, 48>);
+    run_t("w4t (again)", false);
+  }
+  if (only == 98) return 0;
   {  // the grid tiling (cubed_gemm_chain_grid) of w4l: 157 x 157 tiles over the 40000^2 output
     GemmGrid gg{nb, nb, Cc, Cc, N, N};
     const int64_t gtm = (N + HB_BM - 1) / HB_BM;

@@ -256,7 +256,7 @@ void run2(const char* name, const char* src, size_t mask, int iters, int nblk, u
 // consumes a read (k_gap above XORs every read into a sink after the step:
 // 4 VALU per b128, which is what its "per filler" cycles mostly measured).
 // F bits: 1 the 8 A ds_read_b128 | 2 the 16 B ds_read_b64_tr_b16 (or, with
-// 16, 8 B ds_read_b128: a B^T image) | 4 the 8 LDS-DMA pieces (+ one 64-bit
+// 16, 8 B ds_read_b128 from a B^T image laid out as A's, conflict-free) | 4 the 8 LDS-DMA pieces (+ one 64-bit
 // source increment each, every 4th gap) | 8 s_waitcnt + s_barrier per step.
 template <int J>
 using ic = std::integral_constant<int, J>;
@@ -292,7 +292,7 @@ __device__ __forceinline__ void flow_step(const Fr& X, Fr& Y, f32x16 (&acc)[4][4
       constexpr int j = 2 * i + (r == 3), jn = (j >> 1) & 3, jk = j >> 3;
       if constexpr (F & 16) {
         if constexpr (r == 1)  // B^T: one b128 per fragment
-          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.bt[jn][jk]) : "v"(lbt), "i"(jn * 4096 + jk * 16384));
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.bt[jn][jk]) : "v"(la), "i"(32768 + jn * 4096));
       } else if constexpr (j & 1) {
         asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(Y.bh[jn][jk]) : "v"(lbt), "i"(jk * 8192 + 2048));
       } else {
