@@ -48,7 +48,7 @@ __device__ __forceinline__ void wl_seq(F&& f) {
 // Requires every segment's k >= 64 (a 64-k A tile spans at most two
 // segments; cubed_gemm_chain checks) besides the MFMA path's rules.
 // ABL (tools/gemm_w4i_probe.hip ablations only, 0 in the library; results
-// wrong when nonzero): 1 no K-loop barrier, 4 no fragment reads, 16 A
+// wrong when nonzero): 1 no K-loop barrier, 2 no vmcnt wait in the K loop, 4 no fragment reads, 16 A
 // sources never advance, 32 B sources never advance.  STAMP: probe builds
 // store per-wave main-loop cycles to stamp_out (nullptr in the library).
 // GRID (cubed_gemm_chain_grid): 256 x 256 tiles over the WHOLE output of a
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4l(const cubed_gemm_chain
   // fragments into Y; pieces 0-3: A part q of tile (p+5)>>1, 4-7: B of step p+4
   auto full_step = [&](int64_t p, const Frags& X, Frags& Y, auto Q) __attribute__((always_inline)) {
     constexpr int q = decltype(Q)::value;  // (p + 1) & 1, static in the unrolled loop
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if constexpr (!(ABL & 2)) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (!(ABL & 1)) __builtin_amdgcn_s_barrier();  // every wave: step p+1 landed, step p's slots read
     __builtin_amdgcn_sched_barrier(0);

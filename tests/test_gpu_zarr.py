@@ -35,6 +35,36 @@ def test_from_zarr_bit_exact_and_mean(tmp_path, spec, compressor):
     assert np.allclose(got, exp, rtol=1e-6, atol=0)
 
 
+def test_from_zarr_bit_shuffled_chunks(tmp_path, spec):
+    """Chunks stored as bit-shuffled Blosc frames (numcodecs
+    Blosc(shuffle=BITSHUFFLE)), written here by the test's own frame
+    assembler (tests/test_zarr_io.py: numpy bit packing, split and unsplit
+    blocks, a short last block): uploaded bit-exact, then reduced."""
+    import itertools
+    import warnings
+    import zlib
+
+    from test_zarr_io import frame
+
+    x = np.random.default_rng(6).random((50, 37, 41)).astype(np.float32)
+    a = Z.ZarrV2Array.create(str(tmp_path / "b.zarr"), x.shape, x.dtype, (10, 37, 16))
+    a[...] = x
+    for n, coords in enumerate(itertools.product(*[range(k) for k in a.numblocks])):
+        buf = np.empty(a.chunks, dtype=x.dtype)
+        a.decode_into(coords, buf)
+        raw = buf.tobytes()  # 23680 B: blocks of 4096 / 2048 B and a short last one
+        fr = frame(raw, 4, 4096 if n % 2 else 2048, 3, "bit", bool(n % 3 == 0), lambda s: zlib.compress(s, 5))
+        with open(a.chunk_path(coords), "wb") as f:
+            f.write(fr)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # the unpinned-decoder warning
+        y = cubed.from_zarr(str(tmp_path / "b.zarr"), spec=spec)
+        assert np.array_equal(y.compute(), x)
+        got = xp.mean(y, axis=0).compute()
+    exp = R.mean(x, (10, 37, 16), 0, 2_000_000_000, 100_000_000)
+    assert np.allclose(got, exp, rtol=1e-6, atol=0)
+
+
 def test_from_zarr_missing_chunks_read_fill(tmp_path, spec):
     a = Z.ZarrV2Array.create(str(tmp_path / "f.zarr"), (7, 9), np.int64, (3, 4), fill_value=-3)
     a.write_chunk((1, 1), np.arange(12).reshape(3, 4))

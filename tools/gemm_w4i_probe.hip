@@ -120,6 +120,10 @@ int main(int argc, char** argv) {
       {"w4l: A staged in full 128-B lines", nullptr, k_gemm_bf16_w4l<false>, 256, true},
       {"library ping-pong (again)", k_gemm_bf16_chain<false, 0, 1>, nullptr, 512, false},
       {"w4l (again)", nullptr, k_gemm_bf16_w4l<false>, 256, true},
+      {"w4l GM=2 (tile-row groups)", nullptr, k_gemm_bf16_w4l<false, 2>, 256, true},
+      {"w4l GM=8", nullptr, k_gemm_bf16_w4l<false, 8>, 256, true},
+      {"w4l GM=20 (a chunk's tile column)", nullptr, k_gemm_bf16_w4l<false, 20>, 256, true},
+      {"w4l GM=4 (again)", nullptr, k_gemm_bf16_w4l<false>, 256, true},
 
   };
   // B^T chunks and a segment table pointing at them (w4t)
@@ -284,6 +288,8 @@ int main(int argc, char** argv) {
   if (only == 99) {
     stamped("w4l stamped", k_gemm_bf16_w4l<false, 4, true>);
     stamped("  w4l ABL no barrier", k_gemm_bf16_w4l<false, 4, true, 1>);
+    stamped("  w4l ABL no vmcnt wait", k_gemm_bf16_w4l<false, 4, true, 2>);
+    stamped("  w4l ABL no barrier, no vmcnt wait", k_gemm_bf16_w4l<false, 4, true, 3>);
     stamped("  w4l ABL A stale", k_gemm_bf16_w4l<false, 4, true, 16>);
     stamped("  w4l ABL B stale", k_gemm_bf16_w4l<false, 4, true, 32>);
     stamped("  w4l ABL both stale", k_gemm_bf16_w4l<false, 4, true, 48>);
