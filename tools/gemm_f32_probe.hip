@@ -15,6 +15,7 @@ namespace cubed {
 thread_local char g_err[512];
 }
 #include "../cubed_amd/csrc/gemm_chain.hip"
+#include "gemm_f32_w4.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -34,6 +35,8 @@ __global__ void k_diff(const float* a, const float* b, int64_t n, float* out) {
 }
 
 typedef void (*kfn)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*, GemmGrid);
+typedef void (*kfn_s)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, int64_t, int64_t, const char*, GemmGrid,
+                      unsigned long long*);
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 1;
@@ -76,19 +79,24 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e1));
   float* dmax;
   CHECK(hipMalloc(&dmax, 4));
-  struct V { const char* name; kfn f; bool check; };
+  struct V { const char* name; kfn f; bool check; kfn_s fs; };
   V vs[] = {
-      {"BK16 NS4 (library)", k_gemm_f32_chain<16, 4>, false},
-      {"BK16 NS4 ping-pong", k_gemm_f32_chain<16, 4, true>, true},
-      {"BK16 NS3 ping-pong", k_gemm_f32_chain<16, 3, true>, true},
-      {"BK16 NS4 (again)", k_gemm_f32_chain<16, 4>, true},
-      {"BK16 NS4 ping-pong (again)", k_gemm_f32_chain<16, 4, true>, true},
+      {"BK16 NS4 (library)", k_gemm_f32_chain<16, 4>, false, nullptr},
+      {"w4: one wave per SIMD", nullptr, true, k_gemm_f32_w4<false>},
+      {"BK16 NS4 (again)", k_gemm_f32_chain<16, 4>, true, nullptr},
+      {"w4 (again)", nullptr, true, k_gemm_f32_w4<false>},
   };
+  unsigned long long* dstamp;
+  CHECK(hipMalloc(&dstamp, (size_t)(grid.x + 30000) * 8 * 8));
   for (const V& v : vs) {
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(v.f, grid, blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z, GemmGrid{});
+      if (v.fs)
+        hipLaunchKernelGGL(v.fs, grid, dim3(256), 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z, GemmGrid{},
+                           (unsigned long long*)nullptr);
+      else
+        hipLaunchKernelGGL(v.f, grid, blk, 0, 0, v.check ? dt1 : dt0, ds, tm, tn, (const char*)Z, GemmGrid{});
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
@@ -105,6 +113,72 @@ int main(int argc, char** argv) {
       printf("   max |diff| vs first: %g\n", m);
     }
     fflush(stdout);
+  }
+  auto stamped = [&](const char* name, kfn_s f) {  // main-loop cycles per MFMA (the floor is 64: 32x32x2 f32)
+    CHECK(hipMemset(dstamp, 0, (size_t)grid.x * 8 * 8));
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(f, grid, dim3(256), 0, 0, dt1, ds, tm, tn, (const char*)Z, GemmGrid{}, dstamp);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> hs((size_t)grid.x * 8);
+    CHECK(hipMemcpy(hs.data(), dstamp, hs.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, steps = 0;
+    for (size_t i = 0; i < hs.size(); i += 2) {
+      cyc += (double)hs[i];
+      steps += (double)hs[i + 1];
+    }
+    printf("%-28s %9.3f ms %7.1f TF  main loop %.2f cyc/MFMA  clock ~%.2f GHz\n", name, ms, flop / ms / 1e9,
+           cyc / (steps * 128), (cyc / (hs.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
+    fflush(stdout);
+  };
+  stamped("w4 stamped", k_gemm_f32_w4<false, true>);
+  stamped("  ABL no barrier", k_gemm_f32_w4<false, true, 1>);
+  stamped("  ABL no vmcnt wait", k_gemm_f32_w4<false, true, 2>);
+  stamped("  ABL fills from step 0", k_gemm_f32_w4<false, true, 16>);
+  stamped("  ABL all three", k_gemm_f32_w4<false, true, 19>);
+  {  // the grid form stamped (157 x 157 tiles)
+    GemmGrid gg{nb, nb, Cc, Cc, N, N};
+    const int64_t gtm = (N + HF_BM - 1) / HF_BM;
+    CHECK(hipMemset(dstamp, 0, (size_t)grid.x * 8 * 8));
+    hipLaunchKernelGGL((k_gemm_f32_w4<true, true>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0, dt1, ds, gtm, gtm,
+                       (const char*)Z, gg, dstamp);
+    CHECK(hipDeviceSynchronize());
+    std::vector<unsigned long long> hs((size_t)gtm * gtm * 8);
+    CHECK(hipMemcpy(hs.data(), dstamp, hs.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, steps = 0;
+    for (size_t i = 0; i < hs.size(); i += 2) {
+      cyc += (double)hs[i];
+      steps += (double)hs[i + 1];
+    }
+    printf("w4 GRID stamped: main loop %.2f cyc/MFMA\n", cyc / (steps * 128));
+  }
+  {  // the grid tiling: library f32 (grid) vs w4 grid
+    GemmGrid gg{nb, nb, Cc, Cc, N, N};
+    const int64_t gtm = (N + HF_BM - 1) / HF_BM;
+    for (int r = 0; r < 2; ++r) {
+      float ms;
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), dim3((unsigned)(gtm * gtm)), blk, 0, 0, dt0, ds, gtm,
+                         gtm, (const char*)Z, gg);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      printf("library f32 GRID            %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL((k_gemm_f32_w4<true>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0, dt1, ds, gtm, gtm,
+                         (const char*)Z, gg, (unsigned long long*)nullptr);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      printf("w4 GRID                     %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
+    }
+    CHECK(hipMemset(dmax, 0, 4));
+    k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot * nb * nb / 4, dmax);
+    float m;
+    CHECK(hipMemcpy(&m, dmax, 4, hipMemcpyDeviceToHost));
+    printf("   max |diff| w4 GRID vs library GRID: %g\n", m);
   }
   return 0;
 }

@@ -24,6 +24,7 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 #define L3 __attribute__((address_space(3)))
 #define G1 __attribute__((address_space(1)))
@@ -385,6 +386,108 @@ void runf(const char* name, const char* src, size_t mask, int iters, int nblk, u
   CHECK(hipEventDestroy(e1));
 }
 
+// ---- k_flow32<F>: the f32 one-wave step (gemm_f32_w4.h): 128
+// v_mfma_f32_32x32x2_f32 over 16 accumulators, fragments f32x4 a[2][4] /
+// b[2][4] read for the next step (F & 1: the 16 ds_read_b128, one per 4
+// MFMAs in the first half), F & 4: 8 LDS-DMA pieces, F & 8: wait + barrier.
+struct Fr32 {
+  f32x4 a[2][4], b[2][4];
+};
+
+template <int F>
+__device__ __forceinline__ void flow32_step(const Fr32& X, Fr32& Y, f32x16 (&acc)[4][4], uint32_t la,
+                                            const char* src, const char*& gp, size_t mask, L3 char* lds, int w) {
+  seq<128>([&](auto G) {
+    constexpr int gi = decltype(G)::value, g = gi >> 6, j = (gi >> 4) & 3, rb = (gi >> 2) & 3, q = gi & 3;
+    acc[rb][q] = __builtin_amdgcn_mfma_f32_32x32x2f32(X.a[g][rb][j], X.b[g][j][q], acc[rb][q], 0, 0, 0);
+    if constexpr ((F & 1) && gi < 64 && (gi & 3) == 0) {
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int e = gi >> 2;
+      if constexpr (e < 8)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.a[e >> 2][e & 3]) : "v"(la), "i"((e & 3) * 2048));
+      else
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(Y.b[(e >> 2) & 1][e & 3]) : "v"(la), "i"(16384 + (e & 7) * 1024));
+      __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr ((F & 4) && gi > 64 && (gi & 7) == 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_global_load_lds((const G1 void*)gp, (L3 void*)(lds + 65536 + w * 8192 + (gi & 7) * 1024), 16,
+                                       0, 0);
+      gp += 4096;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+  if constexpr (F & 4) gp = src + ((size_t)(gp - src) & mask);
+  if constexpr (F & 8) {
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int F>
+__global__ __launch_bounds__(256, 1) void k_flow32(const char* __restrict__ src, size_t src_mask, int iters,
+                                                     unsigned long long* __restrict__ cyc, float* __restrict__ sink) {
+  __shared__ __attribute__((aligned(1024))) char lds_[LDS_BYTES];
+  L3 char* lds = (L3 char*)lds_;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < LDS_BYTES / 4; i += 256) ((L3 float*)lds)[i] = 0.001f * (i & 255);
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{};
+  Fr32 f0, f1;
+  for (int i = 0; i < 2; ++i)
+    for (int k = 0; k < 4; ++k) {
+      f0.a[i][k] = f1.a[i][k] = f32x4{0.5f, 0.25f, 0.125f, 1.f} * (float)(lane + k);
+      f0.b[i][k] = f1.b[i][k] = f32x4{1.f, 2.f, 3.f, 4.f} * 0.001f;
+    }
+  const uint32_t la = (uint32_t)(uintptr_t)(lds + (lane & 31) * 64 + 16 * ((lane >> 5) ^ ((lane >> 2) & 3)));
+  const char* gp = src + (((size_t)(blockIdx.x * 4 + w) * 65536 + lane * 16) & src_mask);
+  __syncthreads();
+  unsigned long long t0, t1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int it = 0; it < iters; it += 2) {
+    flow32_step<F>(f0, f1, acc, la, src, gp, src_mask, lds, w);
+    flow32_step<F>(f1, f0, acc, la, src, gp, src_mask, lds, w);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += acc[i][j][lane & 15];
+  sink[blockIdx.x * 256 + threadIdx.x] = s;
+  if (lane == 0) cyc[blockIdx.x * 4 + w] = t1 - t0;
+}
+
+template <int F>
+void runf32(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
+            float* d_sink) {
+  hipLaunchKernelGGL(k_flow32<F>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);  // warm
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(k_flow32<F>, dim3(nblk), dim3(256), 0, 0, src, mask, iters, d_cyc, d_sink);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::vector<unsigned long long> c(nblk * 4);
+  CHECK(hipMemcpy(c.data(), d_cyc, c.size() * 8, hipMemcpyDeviceToHost));
+  std::sort(c.begin(), c.end());
+  const double per = 128.0 * iters;
+  const double flop = 4096.0 * 128 * iters * 4 * nblk;
+  printf("flow32 %-37s cyc/MFMA median %6.2f  p90 %6.2f  kernel %8.3f ms  %7.1f TF  (clk %.2f GHz)\n", name,
+         c[c.size() / 2] / per, c[c.size() * 9 / 10] / per, ms, flop / (ms * 1e-3) / 1e12,
+         c[c.size() / 2] / (ms * 1e-3) / 1e9);
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+}
+
 template <int V>
 void run(const char* name, const char* src, size_t mask, int iters, int nblk, unsigned long long* d_cyc,
          float* d_sink) {
@@ -450,6 +553,10 @@ int main(int argc, char** argv) {
     runf<8>("wait/barrier only", src, mask, iters, nblk, d_cyc, d_sink);
     runf<19>("B^T: 16 b128 reads", src, mask, iters, nblk, d_cyc, d_sink);
     runf<31>("B^T: 16 b128 + 8 DMA + wait/barrier", src, mask, iters, nblk, d_cyc, d_sink);
+    runf32<0>("f32 bare (128 MFMAs/step)", src, mask, iters / 4, nblk, d_cyc, d_sink);
+    runf32<1>("f32 + 16 b128 reads", src, mask, iters / 4, nblk, d_cyc, d_sink);
+    runf32<5>("f32 + reads + 8 DMA", src, mask, iters / 4, nblk, d_cyc, d_sink);
+    runf32<13>("f32 + reads + DMA + wait/barrier", src, mask, iters / 4, nblk, d_cyc, d_sink);
     run<13>("B^T step: 16 b128 + 8 glds, 1/gap", src, mask, iters, nblk, d_cyc, d_sink);
     run<14>("16 b128 (every 2nd gap)", src, mask, iters, nblk, d_cyc, d_sink);
     if (argc > 2) {  // two waves per SIMD
