@@ -29,7 +29,7 @@ def main():
         step = bench.step_fn(plan, ex, [m], (u, v))
         step()
         step()
-        for n in (5, 10, 20, 40, 10, 5):
+        for n in (5, 5, 5, 5, 10, 10, 10, 20, 40, 80):
             dt = bench.timed(step, n, 1)
             print(f"{fname} steps={n:3d}: {dt * 1e3:.4f} ms/step, host enqueue median "
                   f"{sorted(bench.HOST_US)[len(bench.HOST_US) // 2] * 1e6:.1f} us, max {max(bench.HOST_US) * 1e6:.1f} us",
