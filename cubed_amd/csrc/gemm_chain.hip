@@ -512,6 +512,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 }
 
 #include "gemm_bf16_w4l.h"
+#include "gemm_bf16_w4p.h"
 
 // ------------------------------------------------------------------ f32 MFMA
 // v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate): lane l gives
@@ -1089,6 +1090,91 @@ extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cube
     hipLaunchKernelGGL((k_gemm_bf16_chain<false, 0, 1, HB_NS, 4, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
   else
     hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), grid, blk, 0, st, d_tasks, d_segs, tm, tn, z, gg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+// ---- packed operands (bf16; gemm_bf16_w4p.h): the chain set must be a
+// regular chunk grid (cubed_gemm_grid_check) of ONE product -- segment s of
+// every task in chunk row I reads the same A chunk, of every task in chunk
+// column J the same B chunk.
+namespace {
+int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs, int64_t nsegs,
+              int32_t in_dtype, int32_t out_dtype, PackPlan& pp, GemmGrid& gg) {
+  if (in_dtype != CUBED_BF16) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: bf16 inputs only");
+    return CUBED_E_LAYOUT;
+  }
+  if (int rc = cubed_gemm_grid_check(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype)) return rc;
+  const int64_t nseg = tasks[0].nseg;
+  for (int64_t I = 0; I < ti; ++I)
+    for (int64_t J = 0; J < tj; ++J)
+      for (int64_t s = 0; s < nseg; ++s) {
+        const cubed_gemm_seg_t &g = segs[tasks[I * tj + J].seg0 + s], &a = segs[tasks[I * tj].seg0 + s],
+                               &b = segs[tasks[J].seg0 + s];
+        if (g.a != a.a || g.lda != a.lda || g.b != b.b || g.ldb != b.ldb) {
+          snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: the tasks are not one chunked product");
+          return CUBED_E_LAYOUT;
+        }
+      }
+  gg.ti = ti;
+  gg.tj = tj;
+  gg.cm = tasks[0].m;
+  gg.cn = tasks[0].n;
+  gg.M = (ti - 1) * gg.cm + tasks[(ti - 1) * tj].m;
+  gg.N = (tj - 1) * gg.cn + tasks[tj - 1].n;
+  pp.ti = ti;
+  pp.tj = tj;
+  pp.cm = gg.cm;
+  pp.cn = gg.cn;
+  pp.M = gg.M;
+  pp.N = gg.N;
+  pp.K = tasks[0].ktot;
+  pp.TM = (pp.M + HB_BM - 1) / HB_BM;
+  pp.TN = (pp.N + HB_BN - 1) / HB_BN;
+  pp.KTL = (pp.K + 63) / 64;
+  if (pp.TM * pp.TN > 0x7fffffff) return fail("grid too large");
+  return 0;
+}
+}  // namespace
+
+extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                                         const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,
+                                         int32_t out_dtype) {
+  if (!tasks || !segs || ti < 1 || tj < 1) return fail("packed: bad argument");
+  PackPlan pp;
+  GemmGrid gg;
+  if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  return (pp.TM + pp.TN) * pp.KTL * (int64_t)WL_ATILE;
+}
+
+extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
+                                       int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs,
+                                       const cubed_gemm_seg_t* d_segs, int64_t nsegs, int32_t in_dtype,
+                                       int32_t out_dtype, void* d_ws, int64_t ws_bytes, void* stream) {
+  if (!tasks || !segs || !d_tasks || !d_segs || ti < 1 || tj < 1) return fail("packed: bad argument");
+  PackPlan pp;
+  GemmGrid gg;
+  if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  const int64_t bytesA = pp.TM * pp.KTL * (int64_t)WL_ATILE, bytesB = pp.TN * pp.KTL * (int64_t)WL_ATILE;
+  if (!d_ws || ws_bytes < bytesA + bytesB || ((uintptr_t)d_ws & 255)) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: the workspace is missing, short or not 256-B aligned");
+    return CUBED_E_WORKSPACE;
+  }
+  char* PA = (char*)d_ws;
+  char* PB = PA + bytesA;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t na = pp.TM * pp.KTL, nb = pp.TN * pp.KTL;
+  hipLaunchKernelGGL(k_pack_a, dim3((unsigned)(na < 16384 ? na : 16384)), dim3(256), 0, st, d_tasks, d_segs, pp, PA);
+  hipLaunchKernelGGL(k_pack_bt, dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, st, d_tasks, d_segs, pp, PB);
+  const dim3 grid((unsigned)(pp.TM * pp.TN));
+  if (out_dtype == CUBED_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB, pp,
+                       gg, nullptr);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB, pp,
+                       gg, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
   return 0;

@@ -768,8 +768,13 @@ class GemmLaunch:
     # (its grid form keeps per-lane chunk selects live through the K loop;
     # profiles/r05_gemm_bf16_ab.log, ping-pong grid 1048-1050)
     GRID_INPUTS = {ir.dtype_code(np.float32)}  # (tools/gemm_ab.sh widens it for A/B runs)
+    # bf16 chunk grids of one product take the packed-operand kernel
+    # (cubed_gemm_chain_packed): both operands rewritten once into the GEMM's
+    # LDS image, then whole-matrix tiles -- config 5 GEMM 1330 TF vs 1214 for
+    # the per-chunk w4l kernel, + 2.6 ms of packing (profiles/r05_gemm_bf16_w4p.log)
+    PACKED = True  # probes set False to time the per-chunk kernel
 
-    def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None):
+    def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None, scratch=None):
         import torch
 
         self.n = len(tasks)
@@ -786,6 +791,17 @@ class GemmLaunch:
                 nat.lib().cubed_gemm_grid_check(self.tasks.ctypes.data, grid[0], grid[1], self.segs.ctypes.data,
                                                 len(self.segs), in_code, out_code) == 0:
             self.grid = tuple(grid)
+        # packed: (workspace pointer, bytes) from scratch(nbytes), which returns
+        # None when the workspace does not fit beside the plan's arrays
+        self.packed = None
+        if grid is not None and self.GRID and self.PACKED and scratch is not None and in_code == ir.dtype_code(ir.bfloat16) and \
+                self.path == nat.GEMM_AUTO and grid[0] * grid[1] == self.n:
+            nbytes = nat.lib().cubed_gemm_pack_bytes(self.tasks.ctypes.data, grid[0], grid[1], self.segs.ctypes.data,
+                                                     len(self.segs), in_code, out_code)
+            ws = scratch(nbytes) if nbytes > 0 else None
+            if ws is not None:
+                self.packed = (ws, nbytes)
+                self.grid = tuple(grid)
         self.flops = 2.0 * float(sum(int(t["m"]) * int(t["n"]) * int(t["ktot"]) for t in self.tasks))
         if not self.n:
             return
@@ -803,6 +819,12 @@ class GemmLaunch:
         if not self.n:
             return
         L = nat.lib()
+        if self.packed is not None:
+            nat.check(L.cubed_gemm_chain_packed(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.grid[0],
+                                                self.grid[1], self.segs.ctypes.data, self.d_segs.data_ptr(),
+                                                len(self.segs), self.in_code, self.out_code, self.packed[0],
+                                                self.packed[1], stream), "cubed_gemm_chain_packed")
+            return
         if self.grid is not None:
             nat.check(L.cubed_gemm_chain_grid(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.grid[0],
                                               self.grid[1], self.segs.ctypes.data, self.d_segs.data_ptr(),

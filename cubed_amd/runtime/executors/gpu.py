@@ -851,8 +851,16 @@ class GpuDagExecutor(DagExecutor):
         # matrix (cubed_gemm_chain_grid checks the grid and the dtype)
         grid = (F.numblocks[0], F.numblocks[-1]) if self.world == 1 and len(tasks) > 1 else None
         out.append(GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
-                              self.zero_page(), grid=grid))
+                              self.zero_page(), grid=grid, scratch=self._gemm_workspace))
         return out
+
+    def _gemm_workspace(self, nbytes):
+        """HBM workspace of the packed bf16 GEMM (both operands rewritten
+        once), or None when it would not fit beside the plan's arrays -- the
+        chain set then runs on the per-chunk kernel, which needs none."""
+        if self.check_memory and self._resident_bytes + self.owned_bytes() + nbytes > HBM_BYTES_PER_GPU:
+            return None
+        return self.scratch(nbytes)
 
     def _compiled_chain_dist(self, chain, target, keys):
         """A reduction chain over chunks spread across the ranks: each rank

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 13
+#define CUBED_ABI_VERSION 14
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -419,6 +419,26 @@ int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cubed_gemm_chai
                           int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
                           int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
                           void* stream);
+
+/* Packed operands (bf16 in, f32 / bf16 out): the same chain set as
+ * cubed_gemm_chain_grid, additionally ONE chunked product (segment s of every
+ * task in chunk row I reads the same A chunk, in chunk column J the same B
+ * chunk).  Both operands are first rewritten into the workspace as 32 KiB
+ * blocks that are the GEMM's LDS image (A: 256-row panels x 64-k tiles; B
+ * transposed, 256-column panels x 64-k tiles; K segments concatenated, pads
+ * zero), then one launch tiles the whole output.  Same results contract as
+ * cubed_gemm_chain (bit-identical to its bf16 MFMA path).
+ * cubed_gemm_pack_bytes (host only): workspace bytes the set needs, or a
+ * negative CUBED_E_* with the message set when it does not pack.
+ * cubed_gemm_chain_packed: d_ws 256-B aligned, ws_bytes >= that size
+ * (else CUBED_E_WORKSPACE); stream-ordered, the workspace is free again once
+ * the launches have run. */
+int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                              const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype, int32_t out_dtype);
+int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti,
+                            int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
+                            int64_t nsegs, int32_t in_dtype, int32_t out_dtype, void* d_ws, int64_t ws_bytes,
+                            void* stream);
 
 /* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
  * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and

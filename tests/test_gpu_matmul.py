@@ -131,7 +131,7 @@ _orig_init = L.GemmLaunch.__init__
 
 
 def _forced_path_init(path):
-    def init(self, tasks, segs, in_code, out_code, device, zero_ptr, path_=None, grid=None):
+    def init(self, tasks, segs, in_code, out_code, device, zero_ptr, path_=None, grid=None, scratch=None):
         _orig_init(self, tasks, segs, in_code, out_code, device, zero_ptr, path=path)
     return init
 
@@ -270,3 +270,96 @@ def test_grid_check_refuses_irregular_tables(built):
     assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float64), ir.dtype_code(np.float64)) != 0
     tasks["ktot"][3] = 128
     assert L_.cubed_gemm_grid_check(*args, ir.dtype_code(np.float32), ir.dtype_code(np.float32)) != 0
+
+
+@pytest.mark.parametrize("shapes", [((700, 1144), (1144, 392), (300, 520), (520, 256)),  # ragged M, N; K edge mid-tile
+                                    ((512, 2048), (2048, 512), (256, 512), (512, 256))])  # whole tiles
+def test_packed_bf16_bit_identical(gpu_executor, shapes, monkeypatch):
+    """bf16 chains over a regular chunk grid of one product run packed
+    (cubed_gemm_chain_packed: A and B^T rewritten into the GEMM's LDS image,
+    then whole-matrix tiles) -- bit-identical to the per-chunk one-wave
+    kernel (each element the same f32 chain over K in the same order), and
+    within the bound of the f64 product."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    sa, sb, ca, cb = shapes
+    x, y = _operands(sa, sb, 23)
+    res = {}
+    for packed in (True, False):
+        monkeypatch.setattr(L.GemmLaunch, "PACKED", packed)
+        e = GpuDagExecutor("cuda:0")
+        spec = cubed.Spec(allowed_mem="2GB", executor=e)
+        a = xp.astype(cubed.from_array(x, chunks=ca, spec=spec), xp.bfloat16)
+        b = xp.astype(cubed.from_array(y, chunks=cb, spec=spec), xp.bfloat16)
+        res[packed] = xp.matmul(a, b).compute()
+        gl = _launches(e)
+        assert len(gl) == 1 and (gl[0].packed is not None) == packed
+    assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
+    _check_bound(res[True], _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64), sa[1],
+                 out_bf16=True)
+
+
+def test_packed_abi_accumulate_f32_out(gpu_executor):
+    """The C ABI directly: f32 output, accumulate = 1 (C += A @ B), chunk
+    tables of one product (3 x 2 chunks, ragged last row / column, K
+    segments 520 / 520 / 104): cubed_gemm_chain_packed equals
+    cubed_gemm_chain bit for bit; a short workspace is refused."""
+    import torch
+
+    ti, tj, cm, cn, ks = 3, 2, 300, 256, [520, 520, 104]
+    ms = [cm, cm, 100]
+    ns = [cn, 136]
+    r = np.random.default_rng(31)
+    dev = "cuda:0"
+    Ach = {(I, s): torch.from_numpy(r.random((ms[I], k), dtype=np.float32) - 0.5).to(dev).bfloat16()
+           for I in range(ti) for s, k in enumerate(ks)}
+    Bch = {(s, J): torch.from_numpy(r.random((k, ns[J]), dtype=np.float32) - 0.5).to(dev).bfloat16()
+           for J in range(tj) for s, k in enumerate(ks)}
+    C0 = {(I, J): torch.from_numpy(r.random((ms[I], ns[J]), dtype=np.float32)).to(dev)
+          for I in range(ti) for J in range(tj)}
+    outs = []
+    for _ in range(2):
+        C = {key: v.clone() for key, v in C0.items()}
+        tasks = np.zeros(ti * tj, dtype=nat.CHAIN_DTYPE)
+        segs = np.zeros(ti * tj * len(ks), dtype=nat.SEG_DTYPE)
+        for I in range(ti):
+            for J in range(tj):
+                t = I * tj + J
+                tasks[t] = (C[I, J].data_ptr(), ms[I], ns[J], ns[J], t * len(ks), len(ks), sum(ks), 1)
+                for s, k in enumerate(ks):
+                    segs[t * len(ks) + s] = (Ach[I, s].data_ptr(), Bch[s, J].data_ptr(), k, k, ns[J], 0)
+        outs.append((C, tasks, segs))
+    Lb = nat.lib()
+    bf, f32 = ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)
+    zero = torch.zeros(64, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    C, tasks, segs = outs[0]
+    d_t = torch.from_numpy(tasks.view(np.uint8).copy()).to(dev)
+    d_s = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+    nat.check(Lb.cubed_gemm_chain(tasks.ctypes.data, d_t.data_ptr(), len(tasks), segs.ctypes.data, d_s.data_ptr(),
+                                  len(segs), bf, f32, zero.data_ptr(), nat.GEMM_AUTO, stream), "cubed_gemm_chain")
+    C, tasks, segs = outs[1]
+    d_t2 = torch.from_numpy(tasks.view(np.uint8).copy()).to(dev)
+    d_s2 = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+    nbytes = Lb.cubed_gemm_pack_bytes(tasks.ctypes.data, ti, tj, segs.ctypes.data, len(segs), bf, f32)
+    assert nbytes == (3 + 2) * 18 * 32768
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    assert ws.data_ptr() % 256 == 0
+    rc = Lb.cubed_gemm_chain_packed(tasks.ctypes.data, d_t2.data_ptr(), ti, tj, segs.ctypes.data, d_s2.data_ptr(),
+                                    len(segs), bf, f32, ws.data_ptr(), nbytes - 32768, stream)
+    assert rc == -4 and b"workspace" in Lb.cubed_last_error()
+    nat.check(Lb.cubed_gemm_chain_packed(tasks.ctypes.data, d_t2.data_ptr(), ti, tj, segs.ctypes.data,
+                                         d_s2.data_ptr(), len(segs), bf, f32, ws.data_ptr(), nbytes, stream),
+              "cubed_gemm_chain_packed")
+    torch.cuda.synchronize()
+    for key in C0:
+        a, b = outs[0][0][key].cpu().numpy(), outs[1][0][key].cpu().numpy()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), key
+    # and the product itself: C0 + A @ B within the f32 bound
+    A = torch.cat([torch.cat([Ach[I, s] for s in range(len(ks))], 1) for I in range(ti)], 0).double().cpu().numpy()
+    B = torch.cat([torch.cat([Bch[s, J] for J in range(tj)], 1) for s in range(len(ks))], 0).double().cpu().numpy()
+    Cin = torch.cat([torch.cat([C0[I, J] for J in range(tj)], 1) for I in range(ti)], 0).double().cpu().numpy()
+    got = torch.cat([torch.cat([outs[1][0][I, J] for J in range(tj)], 1) for I in range(ti)], 0).cpu().numpy()
+    exp = Cin + A @ B
+    bound = 8 * np.sqrt(sum(ks)) * U * (np.abs(Cin) + np.abs(A) @ np.abs(B))
+    assert np.all(np.abs(got - exp) <= bound)

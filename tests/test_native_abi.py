@@ -164,6 +164,48 @@ def test_gemm_chain_path_selection(built, case, in_dt, out_dt, expect):
     assert got == expect
 
 
+def _product_grid(ti, tj, cm, cn, ks, last_m=None, last_n=None):
+    """Tables of ONE chunked product: task (I, J), segment s = A(I, s) @ B(s, J)."""
+    from cubed_amd import _native as nat
+
+    ns = len(ks)
+    tasks = np.zeros(ti * tj, dtype=nat.CHAIN_DTYPE)
+    segs = np.zeros(ti * tj * ns, dtype=nat.SEG_DTYPE)
+    for I in range(ti):
+        for J in range(tj):
+            t = I * tj + J
+            m = last_m if (I == ti - 1 and last_m) else cm
+            n = last_n if (J == tj - 1 and last_n) else cn
+            tasks[t] = ((1 << 30) + t * (1 << 24), m, n, n, t * ns, ns, sum(ks), 0)
+            for s, k in enumerate(ks):
+                segs[t * ns + s] = ((1 << 32) + (I * ns + s) * (1 << 24), (1 << 36) + (s * tj + J) * (1 << 24),
+                                    k, k, n, 0)
+    return tasks, segs
+
+
+def test_gemm_pack_bytes(built):
+    """cubed_gemm_pack_bytes (host logic): the packed bf16 path's workspace
+    is (256-row panels over M + 256-column panels over N) x 64-k tiles x
+    32 KiB; sets that are not one chunked product of a regular grid, or not
+    bf16, are refused with a negative code."""
+    from cubed_amd import _native as nat
+    from cubed_amd import ir
+
+    L_ = nat.lib()
+    bf, f32 = ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)
+    tasks, segs = _product_grid(8, 8, 5000, 5000, [5000] * 8)  # config 5
+    args = (tasks.ctypes.data, 8, 8, segs.ctypes.data, len(segs))
+    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (157 + 157) * 625 * 32768
+    assert L_.cubed_gemm_pack_bytes(*args, bf, f32) == (157 + 157) * 625 * 32768
+    assert L_.cubed_gemm_pack_bytes(*args, f32, f32) < 0  # f32 inputs: the grid kernel instead
+    tasks, segs = _product_grid(3, 2, 300, 256, [520, 520, 104], last_m=100, last_n=136)
+    args = (tasks.ctypes.data, 3, 2, segs.ctypes.data, len(segs))
+    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (3 + 2) * 18 * 32768  # M 700, N 392, K 1144
+    segs["a"][len(segs) - 1] += 4096  # task (2, 1) reads another A chunk than (2, 0)
+    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) < 0
+    assert b"not one chunked product" in L_.cubed_last_error()
+
+
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     """No CPU fallback: a missing extension is an error, not a silent path."""
     from cubed_amd import _native as nat

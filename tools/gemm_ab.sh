@@ -1,20 +1,23 @@
 #!/bin/bash
 # A/B of the bf16 GEMM tilings on config 5 (bench.py --only matmul_bf16), on
 # one box, alternating so clock drift shows:  bash tools/gemm_ab.sh [rounds]
-#   chunk: default (per-chunk tiles)
-#   grid : GemmLaunch.GRID_INPUTS widened to bf16 (whole-matrix tiling)
+#   packed: default (operands packed, then whole-matrix tiles: gemm_bf16_w4p.h)
+#   chunk : GemmLaunch.PACKED off (the per-chunk w4l kernel)
+#   grid  : PACKED off, GRID_INPUTS widened to bf16 (w4l's whole-matrix form)
 # (the library reads no environment; the switch is made in-process here)
 set -e
 R=${1:-2}
 mkdir -p gpurun_out
 for r in $(seq $R); do
-  for v in chunk grid; do
+  for v in packed chunk grid; do
     timeout -k 10 240 python -u - "$v" > gpurun_out/ab_$v.json 2>gpurun_out/ab_$v.err <<'PY'
 import runpy, sys
 import numpy as np
 sys.path.insert(0, ".")
 from cubed_amd import ir
 from cubed_amd.lowering import GemmLaunch
+if sys.argv[1] != "packed":
+    GemmLaunch.PACKED = False
 if sys.argv[1] == "grid":
     GemmLaunch.GRID_INPUTS = GemmLaunch.GRID_INPUTS | {ir.dtype_code(ir.bfloat16)}
 sys.argv = ["bench.py", "--only", "matmul_bf16", "--no-cpu-baseline"]

@@ -19,6 +19,7 @@ thread_local char g_err[512];
 #include "../cubed_amd/csrc/gemm_chain.hip"
 #include "gemm_bf16_w4i.h"
 #include "gemm_bf16_w4t.h"
+#include "gemm_bf16_w4p.h"
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
@@ -233,6 +234,154 @@ int main(int argc, char** argv) {
            cyc / (steps * 32), (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (ms * 1e-3) / 1e9);
     fflush(stdout);
   };
+  if (only == 97) {  // packed operands (tools/gemm_bf16_w4p.h) vs the library w4l kernel
+    PackGeom pg{nb, nb, nb, Cc, Cc, Cc, N, tm, tn, (N + 63) / 64};
+    char *PA, *PB;
+    const size_t pbytes = (size_t)nb * tm * pg.KTL * 32768;
+    CHECK(hipMalloc(&PA, pbytes));
+    CHECK(hipMalloc(&PB, pbytes));
+    hipLaunchKernelGGL((k_gemm_bf16_w4l<false>), grid, dim3(256), 0, 0, dt0, ds, tm, tn, (const char*)Z, GemmGrid{},
+                       (unsigned long long*)nullptr);  // C0: the library kernel's result
+    CHECK(hipGetLastError());
+    for (int r = 0; r < 3; ++r) {
+      CHECK(hipEventRecord(e0));
+      k_packA<<<8192, 256>>>(A, slot_in, pg, PA);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ma, mb;
+      CHECK(hipEventElapsedTime(&ma, e0, e1));
+      CHECK(hipEventRecord(e0));
+      k_packBT<<<8192, 256>>>(B, slot_in, pg, PB);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipGetLastError());
+      CHECK(hipEventElapsedTime(&mb, e0, e1));
+      printf("pack A %.3f ms (%.0f GB/s)  pack B^T %.3f ms (%.0f GB/s)\n", ma, 2.0 * pbytes / ma / 1e6, mb,
+             2.0 * pbytes / mb / 1e6);
+    }
+    {  // the register-transpose B^T pack must give the same blocks
+      char* PB2;
+      CHECK(hipMalloc(&PB2, pbytes));
+      for (int r = 0; r < 3; ++r) {
+        CHECK(hipEventRecord(e0));
+        k_packBT8<<<8192, 256>>>(B, slot_in, pg, PB2);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipGetLastError());
+        float mb;
+        CHECK(hipEventElapsedTime(&mb, e0, e1));
+        printf("pack B^T (8x8 register transpose) %.3f ms (%.0f GB/s)\n", mb, 2.0 * pbytes / mb / 1e6);
+      }
+      CHECK(hipMemset(dmax, 0, 8));
+      k_diff<<<4096, 256>>>((const float*)PB, (const float*)PB2, pbytes / 4, dmax);
+      float m[2];
+      CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+      printf("   vs LDS transpose: max |diff| %g (bit patterns as f32)\n", m[0]);
+      CHECK(hipFree(PB2));
+    }
+    auto run_p = [&](const char* name, bool stamp) {
+      unsigned long long* st = nullptr;
+      if (stamp) CHECK(hipMalloc(&st, (size_t)grid.x * 4 * 2 * 8));
+      float best = 1e30f;
+      for (int r = 0; r < reps + 1; ++r) {
+        CHECK(hipMemset(C1, 0, slot_out * nb * nb));
+        CHECK(hipEventRecord(e0));
+        if (stamp)
+          hipLaunchKernelGGL((k_w4p_probe<false, true>), grid, dim3(256), 0, 0, dt1, (const char*)PA,
+                             (const char*)PB, pg, tm, tn, st);
+        else
+          hipLaunchKernelGGL((k_w4p_probe<false, false>), grid, dim3(256), 0, 0, dt1, (const char*)PA,
+                             (const char*)PB, pg, tm, tn, (unsigned long long*)nullptr);
+        CHECK(hipGetLastError());
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+      }
+      printf("%-40s best %9.3f ms %7.1f TF\n", name, best, flop / best / 1e9);
+      if (stamp) {
+        std::vector<unsigned long long> h((size_t)grid.x * 8);
+        CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+        double cyc = 0, steps = 0;
+        for (size_t i = 0; i < h.size(); i += 2) {
+          cyc += (double)h[i];
+          steps += (double)h[i + 1];
+        }
+        printf("   main loop %6.2f cyc/MFMA  clock ~%.2f GHz\n", cyc / (steps * 32),
+               (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (best * 1e-3) / 1e9);
+        CHECK(hipFree(st));
+      }
+      CHECK(hipMemset(dmax, 0, 8));
+      k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
+      float m[2];
+      CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+      printf("   vs library w4l: max |diff| %g, max rel %g\n", m[0], m[1]);
+      fflush(stdout);
+    };
+    for (const V& v : vs) {  // the library kernel timed in the same process
+      if (&v - vs != 1) continue;
+      float best = 1e30f;
+      for (int r = 0; r < reps + 1; ++r) {
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL(v.fs, grid, dim3(256), 0, 0, dt0, ds, tm, tn, (const char*)Z, GemmGrid{},
+                           (unsigned long long*)nullptr);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+      }
+      printf("%-40s best %9.3f ms %7.1f TF\n", "library w4l", best, flop / best / 1e9);
+    }
+    run_p("w4p: packed A and B^T", false);
+    run_p("w4p stamped", true);
+    run_p("w4p (again)", false);
+    {  // the library form: packed over the WHOLE matrix (157 panels), whole-matrix tiles
+      char* ws;
+      const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, CUBED_F32);
+      if (wsb <= 0) { printf("pack_bytes: %s\n", g_err); return 1; }
+      CHECK(hipMalloc(&ws, wsb));
+      PackPlan pp;
+      GemmGrid gg;
+      if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, CUBED_F32, pp, gg)) return 1;
+      for (int r = 0; r < reps + 1; ++r) {
+        CHECK(hipMemset(C1, 0, slot_out * nb * nb));
+        CHECK(hipEventRecord(e0));
+        if (cubed_gemm_chain_packed(tasks.data(), dt1, nb, nb, segs.data(), ds, segs.size(), CUBED_BF16, CUBED_F32, ws,
+                                    wsb, nullptr)) { printf("packed: %s\n", g_err); return 1; }
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        printf("library cubed_gemm_chain_packed (pack + GEMM) %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
+      }
+      CHECK(hipMemset(dmax, 0, 8));
+      k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot_out * nb * nb / 4, dmax);
+      float m[2];
+      CHECK(hipMemcpy(m, dmax, 8, hipMemcpyDeviceToHost));
+      printf("   vs library w4l: max |diff| %g\n", m[0]);
+      auto gemm_only = [&](const char* name, auto kern) {
+        float best = 1e30f;
+        for (int r = 0; r < reps + 1; ++r) {
+          CHECK(hipEventRecord(e0));
+          hipLaunchKernelGGL(kern, dim3((unsigned)(pp.TM * pp.TN)), dim3(256), 0, 0, dt1, (const char*)ws,
+                             (const char*)(ws + pp.TM * pp.KTL * 32768), pp, gg, (unsigned long long*)nullptr);
+          CHECK(hipEventRecord(e1));
+          CHECK(hipEventSynchronize(e1));
+          float ms;
+          CHECK(hipEventElapsedTime(&ms, e0, e1));
+          if (r > 0 && ms < best) best = ms;
+        }
+        printf("%-44s best %9.3f ms %7.1f TF\n", name, best, flop / best / 1e9);
+        fflush(stdout);
+      };
+      gemm_only("library w4p GEMM only (f32 out)", k_gemm_bf16_w4p<false>);
+      gemm_only("library w4p GEMM only (bf16 out)", k_gemm_bf16_w4p<true>);
+      gemm_only("library w4p GEMM only (f32 out, again)", k_gemm_bf16_w4p<false>);
+    }
+    return 0;
+  }
   if (only == 98 || only < 0) {
     {  // timing of the transpose (one-off per matmul)
       CHECK(hipEventRecord(e0));
