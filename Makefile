@@ -15,7 +15,7 @@ all: $(LIB) oracle
 $(CSRC)/%.o: $(CSRC)/%.hip $(CSRC)/common.h $(CSRC)/vm.h $(CSRC)/fused_common.h $(CSRC)/kernels.h $(CSRC)/stream_impl.h include/cubed_amd.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/gemm_chain.o: $(CSRC)/gemm_bf16_w4l.h $(CSRC)/gemm_bf16_w4p.h
+$(CSRC)/gemm_chain.o: $(CSRC)/gemm_bf16_w4l.h $(CSRC)/gemm_bf16_w4p.h $(CSRC)/gemm_f32_w4p.h
 
 $(CSRC)/%.o: $(CSRC)/%.cpp include/cubed_amd.h
 	g++ -O3 -fPIC -std=c++17 -Iinclude -c $< -o $@

@@ -883,6 +883,8 @@ __global__ __launch_bounds__(256) void k_gemm_any_chain(const cubed_gemm_chain_t
     }
 }
 
+#include "gemm_f32_w4p.h"
+
 int fail(const char* m) {
   snprintf(g_err, sizeof(g_err), "cubed_gemm_chain: %s", m);
   return CUBED_E_ARG;
@@ -1095,15 +1097,15 @@ extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cube
   return 0;
 }
 
-// ---- packed operands (bf16; gemm_bf16_w4p.h): the chain set must be a
+// ---- packed operands (bf16: gemm_bf16_w4p.h, f32: gemm_f32_w4p.h): the chain set must be a
 // regular chunk grid (cubed_gemm_grid_check) of ONE product -- segment s of
 // every task in chunk row I reads the same A chunk, of every task in chunk
 // column J the same B chunk.
 namespace {
 int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs, int64_t nsegs,
               int32_t in_dtype, int32_t out_dtype, PackPlan& pp, GemmGrid& gg) {
-  if (in_dtype != CUBED_BF16) {
-    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: bf16 inputs only");
+  if (in_dtype != CUBED_BF16 && in_dtype != CUBED_F32) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: bf16 or f32 inputs only");
     return CUBED_E_LAYOUT;
   }
   if (int rc = cubed_gemm_grid_check(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype)) return rc;
@@ -1133,10 +1135,13 @@ int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cub
   pp.K = tasks[0].ktot;
   pp.TM = (pp.M + HB_BM - 1) / HB_BM;
   pp.TN = (pp.N + HB_BN - 1) / HB_BN;
-  pp.KTL = (pp.K + 63) / 64;
+  // k blocks: bf16 64-deep tiles (32 KiB per panel), f32 16-deep steps (16 KiB)
+  pp.KTL = in_dtype == CUBED_BF16 ? (pp.K + 63) / 64 : (pp.K + WPF_BK - 1) / WPF_BK;
   if (pp.TM * pp.TN > 0x7fffffff) return fail("grid too large");
   return 0;
 }
+
+int64_t pack_block_bytes(int32_t in_dtype) { return in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA; }
 }  // namespace
 
 extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
@@ -1146,7 +1151,7 @@ extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_
   PackPlan pp;
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
-  return (pp.TM + pp.TN) * pp.KTL * (int64_t)WL_ATILE;
+  return (pp.TM + pp.TN) * pp.KTL * pack_block_bytes(in_dtype);
 }
 
 extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
@@ -1157,7 +1162,7 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
   PackPlan pp;
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
-  const int64_t bytesA = pp.TM * pp.KTL * (int64_t)WL_ATILE, bytesB = pp.TN * pp.KTL * (int64_t)WL_ATILE;
+  const int64_t bytesA = pp.TM * pp.KTL * pack_block_bytes(in_dtype), bytesB = pp.TN * pp.KTL * pack_block_bytes(in_dtype);
   if (!d_ws || ws_bytes < bytesA + bytesB || ((uintptr_t)d_ws & 255)) {
     snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: the workspace is missing, short or not 256-B aligned");
     return CUBED_E_WORKSPACE;
@@ -1166,15 +1171,23 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
   char* PB = PA + bytesA;
   hipStream_t st = (hipStream_t)stream;
   const int64_t na = pp.TM * pp.KTL, nb = pp.TN * pp.KTL;
-  hipLaunchKernelGGL(k_pack_a, dim3((unsigned)(na < 16384 ? na : 16384)), dim3(256), 0, st, d_tasks, d_segs, pp, PA);
-  hipLaunchKernelGGL(k_pack_bt, dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, st, d_tasks, d_segs, pp, PB);
+  const dim3 ga((unsigned)(na < 16384 ? na : 16384)), gb((unsigned)(nb < 16384 ? nb : 16384));
   const dim3 grid((unsigned)(pp.TM * pp.TN));
-  if (out_dtype == CUBED_BF16)
-    hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB, pp,
+  if (in_dtype == CUBED_F32) {
+    hipLaunchKernelGGL(k_pack_a_f32, ga, dim3(256), 0, st, d_tasks, d_segs, pp, PA);
+    hipLaunchKernelGGL(k_pack_b_f32, gb, dim3(256), 0, st, d_tasks, d_segs, pp, PB);
+    hipLaunchKernelGGL((k_gemm_f32_w4p<false>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB, pp,
                        gg, nullptr);
-  else
-    hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB, pp,
-                       gg, nullptr);
+  } else {
+    hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, st, d_tasks, d_segs, pp, PA);
+    hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, st, d_tasks, d_segs, pp, PB);
+    if (out_dtype == CUBED_BF16)
+      hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB,
+                         pp, gg, nullptr);
+    else
+      hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB,
+                         pp, gg, nullptr);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
   return 0;

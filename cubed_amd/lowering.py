@@ -768,11 +768,14 @@ class GemmLaunch:
     # (its grid form keeps per-lane chunk selects live through the K loop;
     # profiles/r05_gemm_bf16_ab.log, ping-pong grid 1048-1050)
     GRID_INPUTS = {ir.dtype_code(np.float32)}  # (tools/gemm_ab.sh widens it for A/B runs)
-    # bf16 chunk grids of one product take the packed-operand kernel
+    # bf16 / f32 chunk grids of one product take the packed-operand kernels
     # (cubed_gemm_chain_packed): both operands rewritten once into the GEMM's
-    # LDS image, then whole-matrix tiles -- config 5 GEMM 1330 TF vs 1214 for
-    # the per-chunk w4l kernel, + 2.6 ms of packing (profiles/r05_gemm_bf16_w4p.log)
-    PACKED = True  # probes set False to time the per-chunk kernel
+    # LDS image, then whole-matrix tiles -- config 5 bf16 GEMM 1316 TF vs 1214
+    # for the per-chunk w4l kernel (+ 2.6 ms of packing,
+    # profiles/r05_gemm_bf16_w4p.log); f32 143.3 TF incl. packing vs 132.5 for
+    # the grid kernel (profiles/r05_gemm_f32_w4p.log)
+    PACKED = True  # probes set False to time the unpacked kernels
+    PACKED_INPUTS = {ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)}
 
     def __init__(self, tasks, segs, in_code, out_code, device, zero_ptr, path=None, grid=None, scratch=None):
         import torch
@@ -794,7 +797,7 @@ class GemmLaunch:
         # packed: (workspace pointer, bytes) from scratch(nbytes), which returns
         # None when the workspace does not fit beside the plan's arrays
         self.packed = None
-        if grid is not None and self.GRID and self.PACKED and scratch is not None and in_code == ir.dtype_code(ir.bfloat16) and \
+        if grid is not None and self.GRID and self.PACKED and scratch is not None and in_code in self.PACKED_INPUTS and \
                 self.path == nat.GEMM_AUTO and grid[0] * grid[1] == self.n:
             nbytes = nat.lib().cubed_gemm_pack_bytes(self.tasks.ctypes.data, grid[0], grid[1], self.segs.ctypes.data,
                                                      len(self.segs), in_code, out_code)

@@ -420,14 +420,15 @@ int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cubed_gemm_chai
                           int64_t nsegs, int32_t in_dtype, int32_t out_dtype, const void* d_zero,
                           void* stream);
 
-/* Packed operands (bf16 in, f32 / bf16 out): the same chain set as
- * cubed_gemm_chain_grid, additionally ONE chunked product (segment s of every
- * task in chunk row I reads the same A chunk, in chunk column J the same B
- * chunk).  Both operands are first rewritten into the workspace as 32 KiB
- * blocks that are the GEMM's LDS image (A: 256-row panels x 64-k tiles; B
- * transposed, 256-column panels x 64-k tiles; K segments concatenated, pads
- * zero), then one launch tiles the whole output.  Same results contract as
- * cubed_gemm_chain (bit-identical to its bf16 MFMA path).
+/* Packed operands (bf16 in, f32 / bf16 out; f32 in, f32 out): the same chain
+ * set as cubed_gemm_chain_grid, additionally ONE chunked product (segment s of
+ * every task in chunk row I reads the same A chunk, in chunk column J the same
+ * B chunk).  Both operands are first rewritten into the workspace as blocks
+ * that are the GEMM's LDS image (bf16: 32 KiB per 256-row A panel / 256-column
+ * B^T panel and 64-k tile; f32: 16 KiB per 256-row A panel / 256-column B
+ * panel and 16-k step; K segments concatenated, pads zero), then one launch
+ * tiles the whole output.  Same results contract as cubed_gemm_chain
+ * (bit-identical to its MFMA paths).
  * cubed_gemm_pack_bytes (host only): workspace bytes the set needs, or a
  * negative CUBED_E_* with the message set when it does not pack.
  * cubed_gemm_chain_packed: d_ws 256-B aligned, ws_bytes >= that size

@@ -231,20 +231,24 @@ def test_grid_tiling_bit_identical(gpu_executor, shapes, dt, monkeypatch):
     x, y = _operands(sa, sb, 21)
     res = {}
     monkeypatch.setattr(L.GemmLaunch, "GRID_INPUTS", {ir.dtype_code(np.float32), ir.dtype_code(ir.bfloat16)})
-    for grid in (True, False):
+    # packed operands (the default), the unpacked grid kernels, per-chunk tiles
+    for variant, grid, packed in (("packed", True, True), ("grid", True, False), ("chunk", False, False)):
         monkeypatch.setattr(L.GemmLaunch, "GRID", grid)
+        monkeypatch.setattr(L.GemmLaunch, "PACKED", packed)
         e = GpuDagExecutor("cuda:0")
         spec = cubed.Spec(allowed_mem="2GB", executor=e)
         a = cubed.from_array(x, chunks=ca, spec=spec)
         b = cubed.from_array(y, chunks=cb, spec=spec)
         if dt == "bf16":
             a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
-        res[grid] = xp.matmul(a, b).compute()
+        res[variant] = xp.matmul(a, b).compute()
         gl = _launches(e)
-        assert len(gl) == 1 and (gl[0].grid is not None) == grid
+        assert len(gl) == 1 and (gl[0].grid is not None) == grid and (gl[0].packed is not None) == packed
         if grid:
             assert gl[0].grid == (-(-sa[0] // ca[0]), -(-sb[1] // cb[1]))
-    assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
+    for variant in ("grid", "chunk"):
+        assert np.array_equal(res["packed"].view(np.uint32), res[variant].view(np.uint32)), variant
+    res[True] = res["packed"]
     if dt == "bf16":
         x64, y64 = _bf16_round(x).astype(np.float64), _bf16_round(y).astype(np.float64)
     else:
@@ -299,21 +303,24 @@ def test_packed_bf16_bit_identical(gpu_executor, shapes, monkeypatch):
                  out_bf16=True)
 
 
-def test_packed_abi_accumulate_f32_out(gpu_executor):
+@pytest.mark.parametrize("in_dt", ["bf16", "f32"])
+def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
     """The C ABI directly: f32 output, accumulate = 1 (C += A @ B), chunk
     tables of one product (3 x 2 chunks, ragged last row / column, K
     segments 520 / 520 / 104): cubed_gemm_chain_packed equals
     cubed_gemm_chain bit for bit; a short workspace is refused."""
     import torch
 
+    cast = (lambda t: t.bfloat16()) if in_dt == "bf16" else (lambda t: t)
+
     ti, tj, cm, cn, ks = 3, 2, 300, 256, [520, 520, 104]
     ms = [cm, cm, 100]
     ns = [cn, 136]
     r = np.random.default_rng(31)
     dev = "cuda:0"
-    Ach = {(I, s): torch.from_numpy(r.random((ms[I], k), dtype=np.float32) - 0.5).to(dev).bfloat16()
+    Ach = {(I, s): cast(torch.from_numpy(r.random((ms[I], k), dtype=np.float32) - 0.5).to(dev))
            for I in range(ti) for s, k in enumerate(ks)}
-    Bch = {(s, J): torch.from_numpy(r.random((k, ns[J]), dtype=np.float32) - 0.5).to(dev).bfloat16()
+    Bch = {(s, J): cast(torch.from_numpy(r.random((k, ns[J]), dtype=np.float32) - 0.5).to(dev))
            for J in range(tj) for s, k in enumerate(ks)}
     C0 = {(I, J): torch.from_numpy(r.random((ms[I], ns[J]), dtype=np.float32)).to(dev)
           for I in range(ti) for J in range(tj)}
@@ -330,7 +337,8 @@ def test_packed_abi_accumulate_f32_out(gpu_executor):
                     segs[t * len(ks) + s] = (Ach[I, s].data_ptr(), Bch[s, J].data_ptr(), k, k, ns[J], 0)
         outs.append((C, tasks, segs))
     Lb = nat.lib()
-    bf, f32 = ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)
+    f32 = ir.dtype_code(np.float32)
+    bf = ir.dtype_code(ir.bfloat16) if in_dt == "bf16" else f32  # (the input code)
     zero = torch.zeros(64, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     C, tasks, segs = outs[0]
@@ -342,7 +350,7 @@ def test_packed_abi_accumulate_f32_out(gpu_executor):
     d_t2 = torch.from_numpy(tasks.view(np.uint8).copy()).to(dev)
     d_s2 = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
     nbytes = Lb.cubed_gemm_pack_bytes(tasks.ctypes.data, ti, tj, segs.ctypes.data, len(segs), bf, f32)
-    assert nbytes == (3 + 2) * 18 * 32768
+    assert nbytes == ((3 + 2) * 18 * 32768 if in_dt == "bf16" else (3 + 2) * 72 * 16384)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     assert ws.data_ptr() % 256 == 0
     rc = Lb.cubed_gemm_chain_packed(tasks.ctypes.data, d_t2.data_ptr(), ti, tj, segs.ctypes.data, d_s2.data_ptr(),

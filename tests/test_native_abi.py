@@ -184,10 +184,11 @@ def _product_grid(ti, tj, cm, cn, ks, last_m=None, last_n=None):
 
 
 def test_gemm_pack_bytes(built):
-    """cubed_gemm_pack_bytes (host logic): the packed bf16 path's workspace
-    is (256-row panels over M + 256-column panels over N) x 64-k tiles x
-    32 KiB; sets that are not one chunked product of a regular grid, or not
-    bf16, are refused with a negative code."""
+    """cubed_gemm_pack_bytes (host logic): the packed path's workspace is
+    (256-row panels over M + 256-column panels over N) x k blocks -- bf16
+    64-k tiles of 32 KiB, f32 16-k steps of 16 KiB; sets that are not one
+    chunked product of a regular grid, or not bf16 / f32, are refused with a
+    negative code."""
     from cubed_amd import _native as nat
     from cubed_amd import ir
 
@@ -197,7 +198,8 @@ def test_gemm_pack_bytes(built):
     args = (tasks.ctypes.data, 8, 8, segs.ctypes.data, len(segs))
     assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (157 + 157) * 625 * 32768
     assert L_.cubed_gemm_pack_bytes(*args, bf, f32) == (157 + 157) * 625 * 32768
-    assert L_.cubed_gemm_pack_bytes(*args, f32, f32) < 0  # f32 inputs: the grid kernel instead
+    assert L_.cubed_gemm_pack_bytes(*args, f32, f32) == (157 + 157) * 2500 * 16384  # f32: 16-k steps of 16 KiB
+    assert L_.cubed_gemm_pack_bytes(*args, ir.dtype_code(np.float64), ir.dtype_code(np.float64)) < 0
     tasks, segs = _product_grid(3, 2, 300, 256, [520, 520, 104], last_m=100, last_n=136)
     args = (tasks.ctypes.data, 3, 2, segs.ctypes.data, len(segs))
     assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (3 + 2) * 18 * 32768  # M 700, N 392, K 1144

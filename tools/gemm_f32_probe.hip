@@ -79,6 +79,57 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e1));
   float* dmax;
   CHECK(hipMalloc(&dmax, 4));
+  if (argc > 2 && argv[2][0] == 'p') {  // packed operands (csrc/gemm_f32_w4p.h) vs the library grid kernel
+    GemmGrid gg{nb, nb, Cc, Cc, N, N};
+    const int64_t gtm = (N + HF_BM - 1) / HF_BM;
+    const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_F32, CUBED_F32);
+    if (wsb <= 0) { printf("pack_bytes: %s\n", g_err); return 1; }
+    char* ws;
+    CHECK(hipMalloc(&ws, wsb));
+    PackPlan pp;
+    if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_F32, CUBED_F32, pp, gg)) return 1;
+    unsigned long long* st;
+    CHECK(hipMalloc(&st, (size_t)gtm * gtm * 8 * 8));
+    for (int r = 0; r < reps + 1; ++r) {
+      float ms;
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL((k_gemm_f32_chain<16, 4, false, true>), dim3((unsigned)(gtm * gtm)), dim3(512), 0, 0, dt0, ds,
+                         gtm, gtm, (const char*)Z, gg);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      printf("library f32 GRID                       %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
+      CHECK(hipEventRecord(e0));
+      if (cubed_gemm_chain_packed(tasks.data(), dt1, nb, nb, segs.data(), ds, segs.size(), CUBED_F32, CUBED_F32, ws, wsb,
+                                  nullptr)) { printf("packed: %s\n", g_err); return 1; }
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      printf("cubed_gemm_chain_packed (pack + GEMM)  %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL((k_gemm_f32_w4p<true>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0, dt1, (const char*)ws,
+                         (const char*)(ws + pp.TM * pp.KTL * WPF_SA), pp, gg, st);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      std::vector<unsigned long long> hs((size_t)gtm * gtm * 8);
+      CHECK(hipMemcpy(hs.data(), st, hs.size() * 8, hipMemcpyDeviceToHost));
+      double cyc = 0, steps = 0;
+      for (size_t i = 0; i < hs.size(); i += 2) {
+        cyc += (double)hs[i];
+        steps += (double)hs[i + 1];
+      }
+      printf("w4p GEMM only, stamped                 %9.3f ms %7.1f TF  main loop %.2f cyc/MFMA  clock ~%.2f GHz\n", ms,
+             flop / ms / 1e9, cyc / (steps * 128), (cyc / (hs.size() / 2)) * ((double)gtm * gtm / 256.0) / (ms * 1e-3) / 1e9);
+      CHECK(hipMemset(dmax, 0, 4));
+      k_diff<<<4096, 256>>>((const float*)C0, (const float*)C1, slot * nb * nb / 4, dmax);
+      float m;
+      CHECK(hipMemcpy(&m, dmax, 4, hipMemcpyDeviceToHost));
+      printf("   max |diff| packed vs library GRID: %g\n", m);
+      fflush(stdout);
+    }
+    return 0;
+  }
   struct V { const char* name; kfn f; bool check; kfn_s fs; };
   V vs[] = {
       {"BK16 NS4 (library)", k_gemm_f32_chain<16, 4>, false, nullptr},
