@@ -29,7 +29,8 @@
 // geometry of one packed chain set (host-validated, see cubed_gemm_pack_bytes)
 struct PackPlan {
   int64_t ti, tj, cm, cn, M, N, K;
-  int64_t TM, TN, KTL;  // 256-row / 256-column panels over M / N, 64-k tiles over K
+  int64_t TM, TN, KTL;  // 256-row / 256-column panels over M / N, k blocks over K
+  int64_t pstride;      // bytes from one panel's first block to the next panel's
 };
 
 // segment containing k (start ks), walking from (s, ks): every task has the
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(256) void k_pack_a(const cubed_gemm_chain_t* __rest
     const int64_t I0 = (mt * 256) / pp.cm, mb = (I0 + 1) * pp.cm;
     int64_t s0 = 0, ks0 = 0;
     if (kt * 64 < pp.K) seg_at(sg0, kt * 64, s0, ks0);
-    char* dst = PA + blk * 32768;
+    char* dst = PA + mt * pp.pstride + kt * 32768;
 #pragma unroll 2
     for (int j = 0; j < 8; ++j) {
       const int r = (threadIdx.x >> 3) + 32 * j, c = sl ^ ((r >> 1) & 7);
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256) void k_pack_bt(const cubed_gemm_chain_t* __res
 #pragma unroll
       for (int e = 0; e < 8; ++e) in[e] = uint4{0, 0, 0, 0};
     }
-    char* dst = PB + blk * 32768;
+    char* dst = PB + nt * pp.pstride + kt * 32768;
     const uint16_t(*w)[8] = (const uint16_t(*)[8])in;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -146,8 +147,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4p(const cubed_gemm_chain
   if (t != 0 || m0 >= M || n0 >= N) return;
   const int64_t ntile = pp.KTL, nst = (pp.K + HB_BK - 1) / HB_BK;
   // this tile's two streams of 32 KiB blocks
-  const char* sA = PA + ((m0 / 256) * ntile) * 32768;
-  const char* sB = PB + ((n0 / 256) * ntile) * 32768;
+  const char* sA = PA + (m0 / 256) * pp.pstride;
+  const char* sB = PB + (n0 / 256) * pp.pstride;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -1102,6 +1102,7 @@ extern "C" int cubed_gemm_chain_grid(const cubed_gemm_chain_t* tasks, const cube
 // every task in chunk row I reads the same A chunk, of every task in chunk
 // column J the same B chunk.
 namespace {
+constexpr int64_t PACK_SKEW = 0;  // bytes added to every panel's span (L2 set spread)
 int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs, int64_t nsegs,
               int32_t in_dtype, int32_t out_dtype, PackPlan& pp, GemmGrid& gg) {
   if (in_dtype != CUBED_BF16 && in_dtype != CUBED_F32) {
@@ -1138,10 +1139,9 @@ int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cub
   // k blocks: bf16 64-deep tiles (32 KiB per panel), f32 16-deep steps (16 KiB)
   pp.KTL = in_dtype == CUBED_BF16 ? (pp.K + 63) / 64 : (pp.K + WPF_BK - 1) / WPF_BK;
   if (pp.TM * pp.TN > 0x7fffffff) return fail("grid too large");
+  pp.pstride = pp.KTL * (in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA) + PACK_SKEW;
   return 0;
 }
-
-int64_t pack_block_bytes(int32_t in_dtype) { return in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA; }
 }  // namespace
 
 extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
@@ -1151,7 +1151,7 @@ extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_
   PackPlan pp;
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
-  return (pp.TM + pp.TN) * pp.KTL * pack_block_bytes(in_dtype);
+  return (pp.TM + pp.TN) * pp.pstride;
 }
 
 extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
@@ -1162,7 +1162,7 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
   PackPlan pp;
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
-  const int64_t bytesA = pp.TM * pp.KTL * pack_block_bytes(in_dtype), bytesB = pp.TN * pp.KTL * pack_block_bytes(in_dtype);
+  const int64_t bytesA = pp.TM * pp.pstride, bytesB = pp.TN * pp.pstride;
   if (!d_ws || ws_bytes < bytesA + bytesB || ((uintptr_t)d_ws & 255)) {
     snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: the workspace is missing, short or not 256-B aligned");
     return CUBED_E_WORKSPACE;

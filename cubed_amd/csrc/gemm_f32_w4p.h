@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_pack_a_f32(const cubed_gemm_chain_t* __
     const int64_t I0 = (mt * 256) / pp.cm, mb = (I0 + 1) * pp.cm;
     int64_t s0 = 0, ks0 = 0;
     if (kt * 16 < pp.K) seg_at(sg0, kt * 16, s0, ks0);
-    char* dst = PA + blk * WPF_SA;
+    char* dst = PA + mt * pp.pstride + kt * WPF_SA;
 #pragma unroll 2
     for (int j = 0; j < 4; ++j) {
       const int r = (threadIdx.x >> 2) + 64 * j, c = sl ^ ((r >> 2) & 3);
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_pack_b_f32(const cubed_gemm_chain_t* __
     const int64_t J = hi ? J0 + 1 : J0, ln = gn - J * pp.cn;
     int64_t s = 0, ks = 0;
     if (kt * 16 < pp.K) seg_at(sg0, kt * 16, s, ks);
-    char* dst = PB + blk * WPF_SB;
+    char* dst = PB + nt * pp.pstride + kt * WPF_SB;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int kr = (threadIdx.x >> 6) + 4 * j;
@@ -113,8 +113,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_
   const int wm = (w >> 1) * 128, wn = (w & 1) * 128;
   // pieces 0..3: A rows 64 w + 16 i .. +15 = block bytes (4 w + i) KiB; 4..7:
   // B k-row 4 w + i - 4 = block bytes (4 w + i - 4) KiB; lane-linear 16 B each
-  const char* const sA = PA + (m0 / 256) * nst * WPF_SA + (4 * w) * 1024 + lane * 16;
-  const char* const sB = PB + (n0 / 256) * nst * WPF_SB + (4 * w) * 1024 + lane * 16;
+  const char* const sA = PA + (m0 / 256) * pp.pstride + (4 * w) * 1024 + lane * 16;
+  const char* const sB = PB + (n0 / 256) * pp.pstride + (4 * w) * 1024 + lane * 16;
 #define WPF_PIECE(i, p, buf)                                                                    \
   do {                                                                                          \
     if constexpr ((i) < 4)                                                                      \

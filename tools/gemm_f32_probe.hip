@@ -90,6 +90,34 @@ int main(int argc, char** argv) {
     if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_F32, CUBED_F32, pp, gg)) return 1;
     unsigned long long* st;
     CHECK(hipMalloc(&st, (size_t)gtm * gtm * 8 * 8));
+    if (argv[2][1] == 's') {  // panel-stride skews: pack + GEMM launched here, each skew twice
+      char* ws2;
+      const int64_t extra = 1 << 20;
+      CHECK(hipMalloc(&ws2, wsb + (pp.TM + pp.TN) * extra));
+      const int64_t base_stride = pp.KTL * WPF_SA;
+      const int64_t skews[] = {0, 1024, 2048 + 128, 4096, 65536 + 1024, 0};
+      for (int64_t sk : skews) {
+        PackPlan q = pp;
+        q.pstride = base_stride + sk;
+        char* QA = ws2;
+        char* QB = ws2 + q.TM * q.pstride;
+        const int64_t na = q.TM * q.KTL, nbk = q.TN * q.KTL;
+        hipLaunchKernelGGL(k_pack_a_f32, dim3((unsigned)(na < 16384 ? na : 16384)), dim3(256), 0, 0, dt1, ds, q, QA);
+        hipLaunchKernelGGL(k_pack_b_f32, dim3((unsigned)(nbk < 16384 ? nbk : 16384)), dim3(256), 0, 0, dt1, ds, q, QB);
+        for (int r = 0; r < 2; ++r) {
+          float ms;
+          CHECK(hipEventRecord(e0));
+          hipLaunchKernelGGL((k_gemm_f32_w4p<false>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0, dt1, (const char*)QA,
+                             (const char*)QB, q, gg, (unsigned long long*)nullptr);
+          CHECK(hipEventRecord(e1));
+          CHECK(hipEventSynchronize(e1));
+          CHECK(hipEventElapsedTime(&ms, e0, e1));
+          printf("skew %6lld: w4p GEMM %9.3f ms %7.1f TF\n", (long long)sk, ms, flop / ms / 1e9);
+          fflush(stdout);
+        }
+      }
+      return 0;
+    }
     for (int r = 0; r < reps + 1; ++r) {
       float ms;
       CHECK(hipEventRecord(e0));
@@ -108,7 +136,7 @@ int main(int argc, char** argv) {
       printf("cubed_gemm_chain_packed (pack + GEMM)  %9.3f ms %7.1f TF\n", ms, flop / ms / 1e9);
       CHECK(hipEventRecord(e0));
       hipLaunchKernelGGL((k_gemm_f32_w4p<true>), dim3((unsigned)(gtm * gtm)), dim3(256), 0, 0, dt1, (const char*)ws,
-                         (const char*)(ws + pp.TM * pp.KTL * WPF_SA), pp, gg, st);
+                         (const char*)(ws + pp.TM * pp.pstride), pp, gg, st);
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       CHECK(hipEventElapsedTime(&ms, e0, e1));

@@ -366,7 +366,7 @@ int main(int argc, char** argv) {
         for (int r = 0; r < reps + 1; ++r) {
           CHECK(hipEventRecord(e0));
           hipLaunchKernelGGL(kern, dim3((unsigned)(pp.TM * pp.TN)), dim3(256), 0, 0, dt1, (const char*)ws,
-                             (const char*)(ws + pp.TM * pp.KTL * 32768), pp, gg, (unsigned long long*)nullptr);
+                             (const char*)(ws + pp.TM * pp.pstride), pp, gg, (unsigned long long*)nullptr);
           CHECK(hipEventRecord(e1));
           CHECK(hipEventSynchronize(e1));
           float ms;
