@@ -461,6 +461,38 @@ def test_matmul_and_k_sum_are_one_chained_gemm(built, dry):
     assert len({int(s["a"]) for s in seg}) == 4 and len({int(s["b"]) for s in seg}) == 4
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+def test_matmul_of_a_regular_grid_is_packed(built, dry, dt, monkeypatch):
+    """One GPU, a regular chunk grid of one product (chunks >= 256 wide):
+    the GemmLaunch takes the packed-operand path with its workspace from
+    the executor's scratch -- (3 + 3 panels) x k blocks (bf16 16 tiles of
+    32 KiB, f32 64 steps of 16 KiB); when the workspace does not fit beside
+    the plan's arrays it stays on the unpacked kernels."""
+    import cubed_amd.runtime.executors.gpu as G
+
+    def plan():
+        spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+        a = cubed.from_array(np.ones((600, 1024), np.float32), chunks=(300, 256), spec=spec)
+        b = cubed.from_array(np.ones((1024, 520), np.float32), chunks=(256, 264), spec=spec)
+        if dt == "bf16":
+            a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
+        dry.launched.clear()
+        arrays_to_plan(xp.matmul(a, b)).execute(executor=dry)
+        return [l for l in dry.launched if type(l).__name__ == "GemmLaunch"][0]
+
+    g = plan()
+    assert g.grid == (2, 2) and g.packed is not None
+    assert g.packed[1] == (3 + 3) * (16 * 32768 if dt == "bf16" else 64 * 16384)
+    # the executor's decision: a workspace only when it fits beside the plan
+    dry.check_memory = True
+    used = dry._resident_bytes + dry.owned_bytes()
+    monkeypatch.setattr(G, "HBM_BYTES_PER_GPU", used + 4096)
+    assert dry._gemm_workspace(8192) is None and dry._gemm_workspace(1024) is not None
+    # and a launch given no workspace keeps the unpacked kernels
+    g2 = type(g)(g.tasks, g.segs, g.in_code, g.out_code, "cpu", 0, grid=(2, 2), scratch=lambda n: None)
+    assert g2.packed is None
+
+
 def test_matmul_without_k_sum_fusion_is_per_chunk(built, dry):
     dry.fuse_gemm_sums = False
     spec = cubed.Spec(allowed_mem="2GB", executor=dry)
