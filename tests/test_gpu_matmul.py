@@ -371,3 +371,36 @@ def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
     exp = Cin + A @ B
     bound = 8 * np.sqrt(sum(ks)) * U * (np.abs(Cin) + np.abs(A) @ np.abs(B))
     assert np.all(np.abs(got - exp) <= bound)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("shapes", [
+    ((300, 32), (32, 264), (256, 32), (32, 256)),          # K = one 32-deep step, one segment
+    ((520, 200), (200, 520), (260, 40), (40, 264)),         # five 40-deep segments, K % 64 != 0
+    ((256, 1000), (1000, 256), (256, 1000), (1000, 256)),   # one output chunk (ti = tj = 1)
+    ((777, 3000), (3000, 600), (259, 600), (600, 296)),     # ragged everywhere, tiles straddle chunks
+])
+def test_packed_matches_unpacked_edge_shapes(gpu_executor, dt, shapes, monkeypatch):
+    """Packed vs unpacked kernels on edge geometries (a single K step,
+    short segments, a single chunk, ragged rows / columns / k): bit for bit."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    sa, sb, ca, cb = shapes
+    x, y = _operands(sa, sb, 41)
+    res = {}
+    for packed in (True, False):
+        monkeypatch.setattr(L.GemmLaunch, "PACKED", packed)
+        e = GpuDagExecutor("cuda:0")
+        spec = cubed.Spec(allowed_mem="2GB", executor=e)
+        a = cubed.from_array(x, chunks=ca, spec=spec)
+        b = cubed.from_array(y, chunks=cb, spec=spec)
+        if dt == "bf16":
+            a, b = xp.astype(a, xp.bfloat16), xp.astype(b, xp.bfloat16)
+        res[packed] = xp.matmul(a, b).compute()
+        gl = _launches(e)
+        n_tasks = (-(-sa[0] // ca[0])) * (-(-sb[1] // cb[1]))
+        if packed and n_tasks > 1 and sa[1] > ca[1]:  # (one k chunk: the per-chunk product lowering)
+            assert gl[0].packed is not None
+    assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
+    rnd = _bf16_round if dt == "bf16" else (lambda v: v)
+    _check_bound(res[True], rnd(x).astype(np.float64), rnd(y).astype(np.float64), sa[1], out_bf16=(dt == "bf16"))
