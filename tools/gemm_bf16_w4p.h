@@ -106,7 +106,18 @@ __global__ void k_packBT8(const char* __restrict__ B, int64_t slot, PackGeom g, 
   }
 }
 
-template <bool OUT_BF16, bool STAMP = false>
+// SYNC: soft lockstep between tiles that share a panel (probe): per-tile
+// progress words (zeroed before the launch), published every 8 steps by lane
+// 0 of wave 0 with vector stores; a tile whose partner (next tile down the
+// same column = same B^T panel, next tile along the row = same A panel, both
+// in this XCD's run) has started and trails it by 9..64 steps waits for it
+// (bounded spin: s_sleep, at most 4000 polls), so the group reads each block
+// while it is still in the XCD's L2.
+__device__ int* g_w4p_progress;
+
+// ABL (ablation, results wrong when nonzero): 1 = A sources stay on tiles
+// 0 / 1 (L2-resident fills), 2 = the same for B^T
+template <bool OUT_BF16, bool STAMP = false, int ABL = 0, bool SYNC = false, int SI = 8, int SL = 8, int SW = 64>
 __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* __restrict__ tasks,
                                                        const char* __restrict__ PA, const char* __restrict__ PB,
                                                        PackGeom pg, int64_t tiles_m, int64_t tiles_n,
@@ -116,10 +127,27 @@ __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* 
   CUBED_L char* ldsA = lds;
   CUBED_L char* ldsB = lds + WT_NA * WL_ATILE;
   int64_t t, m0, n0;
-  tile_of<HB_BM, HB_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, t, m0, n0);
+  const int64_t gt = xcd_remap(blockIdx.x, gridDim.x);
+  tile_of<HB_BM, HB_BN, 4>(gt, tiles_m, tiles_n, t, m0, n0);
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
   const int64_t M = T->m, N = T->n;
-  if (m0 >= M || n0 >= N) return;
+  // partners (SYNC): -1 where none
+  int64_t partB = -1, partA = -1;
+  if constexpr (SYNC) {
+    const int64_t nblk = gridDim.x, xcd = blockIdx.x & 7, q8 = nblk >> 3, r8 = nblk & 7;
+    const int64_t run_end = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + q8 + (xcd < r8 ? 1 : 0);
+    const int64_t tpt = tiles_m * tiles_n, tile = gt - t * tpt, per_group = 4 * tiles_n;
+    const int64_t grp = tile / per_group, first_m = grp * 4;
+    const int64_t gsz = (tiles_m - first_m) < 4 ? (tiles_m - first_m) : 4;
+    const int64_t in_g = tile - grp * per_group;
+    if (in_g % gsz < gsz - 1 && gt + 1 < run_end) partB = gt + 1;
+    if (in_g + gsz < gsz * tiles_n && gt + gsz < run_end) partA = gt + gsz;
+  }
+  if (m0 >= M || n0 >= N) {
+    if constexpr (SYNC)  // (a padded tile: let its partners see it as finished)
+      if (threadIdx.x == 0) __hip_atomic_store(g_w4p_progress + gt, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   const int64_t I = t / pg.nJ, J = t % pg.nJ;
   const int64_t KTL = pg.KTL, ntile = KTL, nst = 2 * KTL;
   // this tile's two streams of 32 KiB blocks
@@ -135,8 +163,10 @@ __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* 
   const char* const sBl = sB + loff;
   CUBED_L char* const dA = ldsA + (64 * w) * 128;
   CUBED_L char* const dB = ldsB + (64 * w) * 128;
-#define W4P_PIECE_A(i, tile) glds16(sAl + (tile) * 32768 + (i) * 1024, dA + ((tile) % WT_NA) * WL_ATILE + (i) * 1024)
-#define W4P_PIECE_B(i, tile) glds16(sBl + (tile) * 32768 + (i) * 1024, dB + ((tile) % WT_NB) * WL_ATILE + (i) * 1024)
+#define W4P_PIECE_A(i, tile) \
+  glds16(sAl + ((ABL & 1) ? ((tile) & 1) : (tile)) * 32768 + (i) * 1024, dA + ((tile) % WT_NA) * WL_ATILE + (i) * 1024)
+#define W4P_PIECE_B(i, tile) \
+  glds16(sBl + ((ABL & 2) ? ((tile) & 1) : (tile)) * 32768 + (i) * 1024, dB + ((tile) % WT_NB) * WL_ATILE + (i) * 1024)
 
   const int ra = wr * 128 + (lane & 31), rb = wc * 128 + (lane & 31);
   // fragment offsets of the two 32-k halves of a 64-k tile: h selects by
@@ -267,9 +297,29 @@ __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* 
   unsigned long long t0 = 0, t1 = 0;
   if constexpr (STAMP) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
   for (; p + 2 < nst && ((p + 5) >> 1) < ntile; p += 2) {
+    if constexpr (SYNC) {
+      if ((p & (SI - 1)) == 1 && w == 0) {
+        if (lane == 0) {
+          int* prog = g_w4p_progress;
+          __hip_atomic_store(prog + gt, (int)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int k = 0; k < 2; ++k) {
+            const int64_t pt = k ? partA : partB;
+            if (pt < 0) continue;
+            for (int it = 0; it < 4000; ++it) {
+              const int v = __hip_atomic_load(prog + pt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const int d = (int)p + 1 - v;
+              if (v == 0 || d <= SL || d > SW) break;
+              __builtin_amdgcn_s_sleep(2);
+            }
+          }
+        }
+      }
+    }
     full_step(p, f1, f0, std::integral_constant<int, 0>{});
     full_step(p + 1, f0, f1, std::integral_constant<int, 1>{});
   }
+  if constexpr (SYNC)
+    if (threadIdx.x == 0) __hip_atomic_store(g_w4p_progress + gt, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if constexpr (STAMP) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
     if (lane == 0) {

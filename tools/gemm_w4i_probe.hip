@@ -279,15 +279,19 @@ int main(int argc, char** argv) {
       printf("   vs LDS transpose: max |diff| %g (bit patterns as f32)\n", m[0]);
       CHECK(hipFree(PB2));
     }
-    auto run_p = [&](const char* name, bool stamp) {
+    typedef void (*kfn_p)(const cubed_gemm_chain_t*, const char*, const char*, PackGeom, int64_t, int64_t,
+                          unsigned long long*);
+    int* prog_host = nullptr;  // SYNC progress words, zeroed before every launch
+    auto run_p = [&](const char* name, bool stamp, kfn_p fst = nullptr) {
       unsigned long long* st = nullptr;
       if (stamp) CHECK(hipMalloc(&st, (size_t)grid.x * 4 * 2 * 8));
       float best = 1e30f;
       for (int r = 0; r < reps + 1; ++r) {
+        if (prog_host) CHECK(hipMemset(prog_host, 0, (size_t)grid.x * 4));
         CHECK(hipMemset(C1, 0, slot_out * nb * nb));
         CHECK(hipEventRecord(e0));
         if (stamp)
-          hipLaunchKernelGGL((k_w4p_probe<false, true>), grid, dim3(256), 0, 0, dt1, (const char*)PA,
+          hipLaunchKernelGGL(fst ? fst : (kfn_p)(k_w4p_probe<false, true>), grid, dim3(256), 0, 0, dt1, (const char*)PA,
                              (const char*)PB, pg, tm, tn, st);
         else
           hipLaunchKernelGGL((k_w4p_probe<false, false>), grid, dim3(256), 0, 0, dt1, (const char*)PA,
@@ -337,6 +341,20 @@ int main(int argc, char** argv) {
     run_p("w4p: packed A and B^T", false);
     run_p("w4p stamped", true);
     run_p("w4p (again)", false);
+    run_p("  w4p ABL A sources L2-resident", true, k_w4p_probe<false, true, 1>);
+    run_p("  w4p ABL B^T sources L2-resident", true, k_w4p_probe<false, true, 2>);
+    run_p("  w4p ABL both L2-resident", true, k_w4p_probe<false, true, 3>);
+    run_p("w4p stamped (again)", true);
+    {
+      CHECK(hipMalloc(&prog_host, (size_t)grid.x * 4));
+      CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_w4p_progress), &prog_host, sizeof(prog_host)));
+      run_p("w4p SYNC every 8 lag 8, stamped", true, k_w4p_probe<false, true, 0, true>);
+      run_p("w4p SYNC every 32 lag 32 window 128", true, k_w4p_probe<false, true, 0, true, 32, 32, 128>);
+      run_p("w4p SYNC every 16 lag 24 window 96", true, k_w4p_probe<false, true, 0, true, 16, 24, 96>);
+      run_p("w4p SYNC every 64 lag 48 window 192", true, k_w4p_probe<false, true, 0, true, 64, 48, 192>);
+      run_p("w4p SYNC every 32 lag 16 window 128", true, k_w4p_probe<false, true, 0, true, 32, 16, 128>);
+      run_p("w4p (no sync, again)", true);
+    }
     {  // the library form: packed over the WHOLE matrix (157 panels), whole-matrix tiles
       char* ws;
       const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, CUBED_F32);
