@@ -762,7 +762,8 @@ class GemmLaunch:
     kernels of csrc/gemm_chain.hip run every dtype (MFMA for bf16 / f32)."""
 
     GRID = True  # probes set False to time the per-chunk tiling
-    # input dtypes that take the grid tiling by default: f32 measured 133.6 TF
+    # input dtypes whose UNPACKED kernels take the grid tiling (when the packed
+    # path below is not taken): f32 measured 133.6 TF
     # grid vs 129-130 per chunk.  bf16 stays per chunk: on config 5 the
     # one-wave full-line kernel runs 1251-1256 TF per chunk vs 1076-1080 grid
     # (its grid form keeps per-lane chunk selects live through the K loop;
