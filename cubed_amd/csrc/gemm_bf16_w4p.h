@@ -342,26 +342,49 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4p(const cubed_gemm_chain
       const uint64_t c1 = hn ? cbase[1][1] : cbase[1][0];
       const int64_t l0 = hn ? cld[0][1] : cld[0][0];
       const int64_t l1 = hn ? cld[1][1] : cld[1][0];
-      wl_seq<16>([&](auto R) __attribute__((always_inline)) {
-        constexpr int r = decltype(R)::value;
-        const int64_t gm = gm0 + mb * 32 + (r & 3) + 8 * (r >> 2);
-        if (gm < M) {
-          const bool hm = gm >= gt.mb;
-          const int64_t lm = gm - (hm ? gt.mb : gt.I0 * gg.cm);
-          const uint64_t C = hm ? c1 : c0;
-          const int64_t ldc = hm ? l1 : l0;
-          float v = acc[mb][nb][r];
-          if constexpr (OUT_BF16) {
-            CUBED_G uint16_t* c = (CUBED_G uint16_t*)(uintptr_t)(C + (uint64_t)(lm * ldc + ln) * 2);
-            if (accum) v += bf16_to_f32(*c);
-            *c = f32_to_bf16(v);
-          } else {
+      if constexpr (OUT_BF16) {
+        // lanes 2i, 2i+1 hold columns 2i, 2i+1 of the same rows: per register
+        // pair (r0, r0 + 1) one lane exchange gives the even lane row r0 and
+        // the odd lane row r0 + 1 as two adjacent columns -- one 4-byte store
+        // per two elements (columns never straddle a chunk: cn % 8 == 0)
+        const bool odd = lane & 1;
+        const int64_t le = ln - (odd ? 1 : 0);
+        wl_seq<8>([&](auto P) __attribute__((always_inline)) {
+          constexpr int r0 = 2 * decltype(P)::value, r1 = r0 + 1;
+          const float x0 = acc[mb][nb][r0], x1 = acc[mb][nb][r1];
+          const float y = __shfl_xor(odd ? x0 : x1, 1);
+          float lo = odd ? y : x0, hi = odd ? x1 : y;
+          const int64_t gm = gm0 + mb * 32 + (r0 & 3) + 8 * (r0 >> 2) + (odd ? 1 : 0);
+          if (gm < M) {
+            const bool hm = gm >= gt.mb;
+            const int64_t lm = gm - (hm ? gt.mb : gt.I0 * gg.cm);
+            const uint64_t C = hm ? c1 : c0;
+            const int64_t ldc = hm ? l1 : l0;
+            CUBED_G uint32_t* c = (CUBED_G uint32_t*)(uintptr_t)(C + (uint64_t)(lm * ldc + le) * 2);
+            if (accum) {
+              const uint32_t o = *c;
+              lo += bf16_to_f32((uint16_t)(o & 0xffffu));
+              hi += bf16_to_f32((uint16_t)(o >> 16));
+            }
+            *c = (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+          }
+        });
+      } else {
+        wl_seq<16>([&](auto R) __attribute__((always_inline)) {
+          constexpr int r = decltype(R)::value;
+          const int64_t gm = gm0 + mb * 32 + (r & 3) + 8 * (r >> 2);
+          if (gm < M) {
+            const bool hm = gm >= gt.mb;
+            const int64_t lm = gm - (hm ? gt.mb : gt.I0 * gg.cm);
+            const uint64_t C = hm ? c1 : c0;
+            const int64_t ldc = hm ? l1 : l0;
+            float v = acc[mb][nb][r];
             CUBED_G float* c = (CUBED_G float*)(uintptr_t)(C + (uint64_t)(lm * ldc + ln) * 4);
             if (accum) v += *c;
             *c = v;
           }
-        }
-      });
+        });
+      }
     }
   });
 }

@@ -303,15 +303,17 @@ def test_packed_bf16_bit_identical(gpu_executor, shapes, monkeypatch):
                  out_bf16=True)
 
 
-@pytest.mark.parametrize("in_dt", ["bf16", "f32"])
-def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
-    """The C ABI directly: f32 output, accumulate = 1 (C += A @ B), chunk
-    tables of one product (3 x 2 chunks, ragged last row / column, K
-    segments 520 / 520 / 104): cubed_gemm_chain_packed equals
-    cubed_gemm_chain bit for bit; a short workspace is refused."""
+@pytest.mark.parametrize("in_dt,out_dt", [("bf16", "f32"), ("f32", "f32"), ("bf16", "bf16")])
+def test_packed_abi_accumulate(gpu_executor, in_dt, out_dt):
+    """The C ABI directly: accumulate = 1 (C += A @ B), chunk tables of one
+    product (3 x 2 chunks, ragged last row / column, K segments 520 / 520 /
+    104): cubed_gemm_chain_packed equals cubed_gemm_chain bit for bit (bf16
+    output: the paired-column stores of the packed epilogue); a short
+    workspace is refused."""
     import torch
 
     cast = (lambda t: t.bfloat16()) if in_dt == "bf16" else (lambda t: t)
+    ocast = (lambda t: t.bfloat16()) if out_dt == "bf16" else (lambda t: t)
 
     ti, tj, cm, cn, ks = 3, 2, 300, 256, [520, 520, 104]
     ms = [cm, cm, 100]
@@ -322,7 +324,7 @@ def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
            for I in range(ti) for s, k in enumerate(ks)}
     Bch = {(s, J): cast(torch.from_numpy(r.random((k, ns[J]), dtype=np.float32) - 0.5).to(dev))
            for J in range(tj) for s, k in enumerate(ks)}
-    C0 = {(I, J): torch.from_numpy(r.random((ms[I], ns[J]), dtype=np.float32)).to(dev)
+    C0 = {(I, J): ocast(torch.from_numpy(r.random((ms[I], ns[J]), dtype=np.float32)).to(dev))
           for I in range(ti) for J in range(tj)}
     outs = []
     for _ in range(2):
@@ -337,8 +339,8 @@ def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
                     segs[t * len(ks) + s] = (Ach[I, s].data_ptr(), Bch[s, J].data_ptr(), k, k, ns[J], 0)
         outs.append((C, tasks, segs))
     Lb = nat.lib()
-    f32 = ir.dtype_code(np.float32)
-    bf = ir.dtype_code(ir.bfloat16) if in_dt == "bf16" else f32  # (the input code)
+    bf = ir.dtype_code(ir.bfloat16) if in_dt == "bf16" else ir.dtype_code(np.float32)  # (the input code)
+    f32 = ir.dtype_code(ir.bfloat16) if out_dt == "bf16" else ir.dtype_code(np.float32)  # (the output code)
     zero = torch.zeros(64, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     C, tasks, segs = outs[0]
@@ -361,15 +363,17 @@ def test_packed_abi_accumulate_f32_out(gpu_executor, in_dt):
               "cubed_gemm_chain_packed")
     torch.cuda.synchronize()
     for key in C0:
-        a, b = outs[0][0][key].cpu().numpy(), outs[1][0][key].cpu().numpy()
+        a, b = outs[0][0][key].float().cpu().numpy(), outs[1][0][key].float().cpu().numpy()
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), key
     # and the product itself: C0 + A @ B within the f32 bound
     A = torch.cat([torch.cat([Ach[I, s] for s in range(len(ks))], 1) for I in range(ti)], 0).double().cpu().numpy()
     B = torch.cat([torch.cat([Bch[s, J] for J in range(tj)], 1) for s in range(len(ks))], 0).double().cpu().numpy()
     Cin = torch.cat([torch.cat([C0[I, J] for J in range(tj)], 1) for I in range(ti)], 0).double().cpu().numpy()
-    got = torch.cat([torch.cat([outs[1][0][I, J] for J in range(tj)], 1) for I in range(ti)], 0).cpu().numpy()
+    got = torch.cat([torch.cat([outs[1][0][I, J] for J in range(tj)], 1) for I in range(ti)], 0).double().cpu().numpy()
     exp = Cin + A @ B
     bound = 8 * np.sqrt(sum(ks)) * U * (np.abs(Cin) + np.abs(A) @ np.abs(B))
+    if out_dt == "bf16":
+        bound = bound + 2.0 ** -8 * np.abs(exp)
     assert np.all(np.abs(got - exp) <= bound)
 
 
