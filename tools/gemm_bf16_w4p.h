@@ -117,7 +117,7 @@ __device__ int* g_w4p_progress;
 
 // ABL (ablation, results wrong when nonzero): 1 = A sources stay on tiles
 // 0 / 1 (L2-resident fills), 2 = the same for B^T
-template <bool OUT_BF16, bool STAMP = false, int ABL = 0, bool SYNC = false, int SI = 8, int SL = 8, int SW = 64>
+template <bool OUT_BF16, bool STAMP = false, int ABL = 0, bool SYNC = false, int SI = 8, int SL = 8, int SW = 64, int GMT = 4>
 __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* __restrict__ tasks,
                                                        const char* __restrict__ PA, const char* __restrict__ PB,
                                                        PackGeom pg, int64_t tiles_m, int64_t tiles_n,
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256, 1) void k_w4p_probe(const cubed_gemm_chain_t* 
   CUBED_L char* ldsB = lds + WT_NA * WL_ATILE;
   int64_t t, m0, n0;
   const int64_t gt = xcd_remap(blockIdx.x, gridDim.x);
-  tile_of<HB_BM, HB_BN, 4>(gt, tiles_m, tiles_n, t, m0, n0);
+  tile_of<HB_BM, HB_BN, GMT>(gt, tiles_m, tiles_n, t, m0, n0);
   const cubed_gemm_chain_t* __restrict__ T = tasks + t;
   const int64_t M = T->m, N = T->n;
   // partners (SYNC): -1 where none

@@ -348,6 +348,15 @@ int main(int argc, char** argv) {
     {
       CHECK(hipMalloc(&prog_host, (size_t)grid.x * 4));
       CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_w4p_progress), &prog_host, sizeof(prog_host)));
+      if (argc > 5 && argv[5][0] == 'g') {  // tile-group rows (GM) of the packed kernel
+        run_p("w4p GM=2", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 2>);
+        run_p("w4p GM=4", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 4>);
+        run_p("w4p GM=8", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 8>);
+        run_p("w4p GM=16", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 16>);
+        run_p("w4p GM=1", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 1>);
+        run_p("w4p GM=4 (again)", true, k_w4p_probe<false, true, 0, false, 8, 8, 64, 4>);
+        return 0;
+      }
       run_p("w4p SYNC every 8 lag 8, stamped", true, k_w4p_probe<false, true, 0, true>);
       run_p("w4p SYNC every 32 lag 32 window 128", true, k_w4p_probe<false, true, 0, true, 32, 32, 128>);
       run_p("w4p SYNC every 16 lag 24 window 96", true, k_w4p_probe<false, true, 0, true, 16, 24, 96>);
