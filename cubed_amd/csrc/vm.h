@@ -368,6 +368,16 @@ CUBED_DEV void var_add(Acc& n, Acc& mu, Acc& m2, double x) {
   m2.f = m2.f + d * (x - mu.f);
 }
 
+// the same with the count's reciprocal given: the elements of one VEC group
+// fold the same rows, so one f64 division serves the group
+CUBED_DEV void var_add_inv(Acc& n, Acc& mu, Acc& m2, double x, int64_t n1, double inv) {
+#pragma clang fp contract(off)
+  n.i = n1;
+  const double d = x - mu.f;
+  mu.f = mu.f + d * inv;
+  m2.f = m2.f + d * (x - mu.f);
+}
+
 template <typename V>
 CUBED_DEV void pair_add(Acc& a0, Acc& a1, int rop, int acc_i, V v0, V v1) {
   Acc b0, b1;
@@ -463,8 +473,15 @@ CUBED_DEV void fields_add(Acc (&acc)[CUBED_MAX_FIELDS][VEC], const V (&src)[CUBE
                           const cubed_program_t& P) {
   if (triple_rop(P.field_rop[0])) {
     if (P.field_rop[0] == CUBED_R_VAR) {
+      if constexpr (VEC > 1) {
+        // (every element of the group has folded the same number of values)
+        const int64_t n1 = acc[0][0].i + 1;
+        const double inv = 1.0 / (double)n1;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) var_add(acc[0][j], acc[1][j], acc[2][j], (double)src[0][j]);
+        for (int j = 0; j < VEC; ++j) var_add_inv(acc[0][j], acc[1][j], acc[2][j], (double)src[0][j], n1, inv);
+      } else {
+        var_add(acc[0][0], acc[1][0], acc[2][0], (double)src[0][0]);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
