@@ -37,7 +37,7 @@ MAX_EPI = 16
 MAX_CONSTS = 16
 NREGS = 6
 
-ABI_VERSION = 14  # include/cubed_amd.h CUBED_ABI_VERSION
+ABI_VERSION = 15  # include/cubed_amd.h CUBED_ABI_VERSION
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcubed_amd.so")
 
 
@@ -141,6 +141,19 @@ def lib():
     L.cubed_gemm_chain_packed.argtypes = [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                           c_int32, c_int32, c_void_p, c_int64, c_void_p]
     L.cubed_gemm_chain_packed.restype = c_int
+    L.cubed_gemm_dist_image_bytes.argtypes = [c_int64, c_int64, c_int32]
+    L.cubed_gemm_dist_image_bytes.restype = c_int64
+    L.cubed_gemm_dist_pack_a.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
+                                         c_int64, c_int64, c_void_p, c_int64, c_void_p]
+    L.cubed_gemm_dist_pack_a.restype = c_int
+    L.cubed_gemm_dist_b_bytes.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_int32]
+    L.cubed_gemm_dist_b_bytes.restype = c_int64
+    L.cubed_gemm_dist_pack_b.argtypes = [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                                         c_int32, c_int32, c_void_p, c_int64, c_void_p]
+    L.cubed_gemm_dist_pack_b.restype = c_int
+    L.cubed_gemm_dist_gemm.argtypes = [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int32, c_int32,
+                                       c_void_p, c_int64, c_void_p, c_int64, c_void_p]
+    L.cubed_gemm_dist_gemm.restype = c_int
     L.cubed_gemm_chain.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                    c_void_p, c_int32, c_void_p]
     L.cubed_gemm_chain.restype = c_int
@@ -215,6 +228,8 @@ EXPORTED_SYMBOLS = (
     "cubed_blosc_header", "cubed_blosc_decompress", "cubed_blosc_max_compressed",
     "cubed_blosc_compress", "cubed_zstd_decompress", "cubed_lz4_chunk_decompress", "cubed_gemm_chain", "cubed_gemm_chain_path",
     "cubed_gemm_grid_check", "cubed_gemm_chain_grid", "cubed_gemm_pack_bytes", "cubed_gemm_chain_packed",
+    "cubed_gemm_dist_image_bytes", "cubed_gemm_dist_pack_a", "cubed_gemm_dist_b_bytes", "cubed_gemm_dist_pack_b",
+    "cubed_gemm_dist_gemm",
 )
 
 

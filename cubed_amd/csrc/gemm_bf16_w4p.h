@@ -30,7 +30,12 @@
 struct PackPlan {
   int64_t ti, tj, cm, cn, M, N, K;
   int64_t TM, TN, KTL;  // 256-row / 256-column panels over M / N, k blocks over K
-  int64_t pstride;      // bytes from one panel's first block to the next panel's
+  int64_t pstride;      // bytes from one panel's first block to the next panel's (B / B^T)
+  // the A image: block (mt, kt) at mt * apstride + kt * akstride (one GPU:
+  // panel-major, apstride = pstride; the multi-GPU image is k-major so every
+  // k chunk's tile range is one contiguous run, cubed_gemm_dist_*)
+  int64_t apstride, akstride;
+  int64_t kt0, kt1;     // k blocks [kt0, kt1) the A pack writes
 };
 
 // segment containing k (start ks), walking from (s, ks): every task has the
@@ -48,16 +53,16 @@ __device__ __forceinline__ void seg_at(const cubed_gemm_seg_t* __restrict__ sg, 
 __global__ __launch_bounds__(256) void k_pack_a(const cubed_gemm_chain_t* __restrict__ tasks,
                                                 const cubed_gemm_seg_t* __restrict__ segs, PackPlan pp,
                                                 char* __restrict__ PA) {
-  const int64_t nblk = pp.TM * pp.KTL;
+  const int64_t nkt = pp.kt1 - pp.kt0, nblk = pp.TM * nkt;
   const cubed_gemm_seg_t* __restrict__ sg0 = segs + tasks[0].seg0;
   const int sl = threadIdx.x & 7;
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t mt = blk / pp.KTL, kt = blk - mt * pp.KTL;
+    const int64_t mt = blk / nkt, kt = pp.kt0 + (blk - mt * nkt);
     // the panel's first chunk row (rows of a panel lie in at most two: cm >= 256)
     const int64_t I0 = (mt * 256) / pp.cm, mb = (I0 + 1) * pp.cm;
     int64_t s0 = 0, ks0 = 0;
     if (kt * 64 < pp.K) seg_at(sg0, kt * 64, s0, ks0);
-    char* dst = PA + mt * pp.pstride + kt * 32768;
+    char* dst = PA + mt * pp.apstride + kt * pp.akstride;
 #pragma unroll 2
     for (int j = 0; j < 8; ++j) {
       const int r = (threadIdx.x >> 3) + 32 * j, c = sl ^ ((r >> 1) & 7);
@@ -147,7 +152,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4p(const cubed_gemm_chain
   if (t != 0 || m0 >= M || n0 >= N) return;
   const int64_t ntile = pp.KTL, nst = (pp.K + HB_BK - 1) / HB_BK;
   // this tile's two streams of 32 KiB blocks
-  const char* sA = PA + (m0 / 256) * pp.pstride;
+  const char* sA = PA + (m0 / 256) * pp.apstride;
+  const int64_t aks = pp.akstride;
   const char* sB = PB + (n0 / 256) * pp.pstride;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16_w4p(const cubed_gemm_chain
   const char* const sBl = sB + (64 * w) * 128 + lane * 16;
   CUBED_L char* const dA = ldsA + (64 * w) * 128;
   CUBED_L char* const dB = ldsB + (64 * w) * 128;
-#define W4P_PIECE_A(i, tile) glds16(sAl + (tile) * 32768 + (i) * 1024, dA + ((tile) % WP_NA) * WL_ATILE + (i) * 1024)
+#define W4P_PIECE_A(i, tile) glds16(sAl + (tile) * aks + (i) * 1024, dA + ((tile) % WP_NA) * WL_ATILE + (i) * 1024)
 #define W4P_PIECE_B(i, tile) glds16(sBl + (tile) * 32768 + (i) * 1024, dB + ((tile) % WP_NB) * WL_ATILE + (i) * 1024)
 
   // fragment (mb|nb, kh) of half h: row ra (rb) + 32 mb, k chunk

@@ -1140,9 +1140,182 @@ int pack_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cub
   pp.KTL = in_dtype == CUBED_BF16 ? (pp.K + 63) / 64 : (pp.K + WPF_BK - 1) / WPF_BK;
   if (pp.TM * pp.TN > 0x7fffffff) return fail("grid too large");
   pp.pstride = pp.KTL * (in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA) + PACK_SKEW;
+  pp.apstride = pp.pstride;
+  pp.akstride = in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA;
+  pp.kt0 = 0;
+  pp.kt1 = pp.KTL;
+  return 0;
+}
+
+int64_t kblock_k(int32_t in_dtype) { return in_dtype == CUBED_BF16 ? 64 : WPF_BK; }
+int64_t kblock_bytes(int32_t in_dtype) { return in_dtype == CUBED_BF16 ? WL_ATILE : WPF_SA; }
+
+// the multi-GPU A image: k-major blocks of the whole A (K blocks x TM panels)
+void dist_image(PackPlan& pp, int32_t in_dtype) {
+  pp.apstride = kblock_bytes(in_dtype);
+  pp.akstride = pp.TM * pp.apstride;
+}
+
+// A pack plan of the multi-GPU matmul: ti tasks = A's chunk rows (task I:
+// m = rows of chunk row I, segments = the k chunks of that row, a = the
+// chunk -- or, where this rank does not hold it, 0 or a halo buffer of the
+// few columns its k blocks reach into), packing k blocks [kt0, kt1)
+int dist_a_plan(const cubed_gemm_chain_t* at, int64_t ti, const cubed_gemm_seg_t* as, int64_t nsegs,
+                int32_t in_dtype, int64_t kt0, int64_t kt1, PackPlan& pp) {
+  auto bad = [&](const char* why) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_dist_pack_a: %s", why);
+    return CUBED_E_LAYOUT;
+  };
+  if (in_dtype != CUBED_BF16 && in_dtype != CUBED_F32) return bad("bf16 or f32 inputs only");
+  const int64_t isz = in_dtype == CUBED_BF16 ? 2 : 4, kq = 16 / isz;
+  const cubed_gemm_chain_t& T0 = at[0];
+  const int64_t nseg = T0.nseg, cm = T0.m;
+  if (nseg < 1) return bad("no k chunks");
+  int64_t M = 0;
+  for (int64_t I = 0; I < ti; ++I) {
+    const cubed_gemm_chain_t& T = at[I];
+    if (T.seg0 < 0 || T.seg0 + T.nseg > nsegs || T.nseg != nseg) return bad("task out of range");
+    if ((I + 1 < ti && T.m != cm) || T.m > cm || T.m < 1) return bad("not a regular chunk column");
+    for (int64_t s = 0; s < nseg; ++s) {
+      const cubed_gemm_seg_t &g = as[T.seg0 + s], &g0 = as[T0.seg0 + s];
+      if (g.k != g0.k || g.k < 1 || g.k % kq) return bad("k chunks differ or are not 16-B multiples");
+      if ((g.a & 15) || g.lda < 1 || (g.lda * isz) % 16) return bad("A rows not 16-B aligned");
+    }
+    M += T.m;
+  }
+  if (ti > 1 && cm < 256) return bad("chunk rows narrower than a panel");
+  int64_t K = 0;
+  for (int64_t s = 0; s < nseg; ++s) K += as[T0.seg0 + s].k;
+  pp.ti = ti;
+  pp.tj = 1;
+  pp.cm = cm;
+  pp.cn = 1;
+  pp.M = M;
+  pp.N = 1;
+  pp.K = K;
+  pp.TM = (M + 255) / 256;
+  pp.TN = 1;
+  const int64_t kb = kblock_k(in_dtype);
+  pp.KTL = (K + kb - 1) / kb;
+  pp.pstride = 0;
+  dist_image(pp, in_dtype);
+  if (kt0 < 0 || kt1 > pp.KTL || kt0 >= kt1) return bad("k block range outside the image");
+  pp.kt0 = kt0;
+  pp.kt1 = kt1;
+  // every chunk the range reads must be present (a 0 address is a chunk this
+  // rank neither holds nor received: reading it would fault)
+  const int64_t k0 = kt0 * kb, k1 = kt1 * kb < K ? kt1 * kb : K;
+  int64_t ks = 0;
+  for (int64_t s = 0; s < nseg; ++s) {
+    const int64_t ke = ks + as[T0.seg0 + s].k;
+    if (ks < k1 && ke > k0)
+      for (int64_t I = 0; I < ti; ++I)
+        if (!as[at[I].seg0 + s].a) return bad("a k chunk the range reads is missing");
+    ks = ke;
+  }
   return 0;
 }
 }  // namespace
+
+extern "C" int64_t cubed_gemm_dist_image_bytes(int64_t M, int64_t K, int32_t in_dtype) {
+  if (M < 1 || K < 1 || (in_dtype != CUBED_BF16 && in_dtype != CUBED_F32)) return fail("dist image: bad argument");
+  const int64_t kb = kblock_k(in_dtype);
+  return ((M + 255) / 256) * ((K + kb - 1) / kb) * kblock_bytes(in_dtype);
+}
+
+extern "C" int cubed_gemm_dist_pack_a(const cubed_gemm_chain_t* a_tasks, const cubed_gemm_chain_t* d_a_tasks,
+                                      int64_t ti, const cubed_gemm_seg_t* a_segs, const cubed_gemm_seg_t* d_a_segs,
+                                      int64_t nsegs, int32_t in_dtype, int64_t kt0, int64_t kt1, void* d_image,
+                                      int64_t image_bytes, void* stream) {
+  if (!a_tasks || !d_a_tasks || !a_segs || !d_a_segs || ti < 1) return fail("dist pack: bad argument");
+  PackPlan pp;
+  if (int rc = dist_a_plan(a_tasks, ti, a_segs, nsegs, in_dtype, kt0, kt1, pp)) return rc;
+  if (!d_image || image_bytes < pp.KTL * pp.akstride || ((uintptr_t)d_image & 255)) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_dist_pack_a: the image is missing, short or not 256-B aligned");
+    return CUBED_E_WORKSPACE;
+  }
+  const int64_t na = pp.TM * (kt1 - kt0);
+  const dim3 ga((unsigned)(na < 16384 ? na : 16384));
+  hipStream_t st = (hipStream_t)stream;
+  if (in_dtype == CUBED_F32)
+    hipLaunchKernelGGL(k_pack_a_f32, ga, dim3(256), 0, st, d_a_tasks, d_a_segs, pp, (char*)d_image);
+  else
+    hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, st, d_a_tasks, d_a_segs, pp, (char*)d_image);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+// the rank's local product: its C chunks (ti x tj grid, columns it owns), B
+// from its own chunks, A from the k-major image all ranks filled
+static int dist_local_plan(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj, const cubed_gemm_seg_t* segs,
+                           int64_t nsegs, int32_t in_dtype, int32_t out_dtype, PackPlan& pp, GemmGrid& gg) {
+  if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  dist_image(pp, in_dtype);
+  return 0;
+}
+
+extern "C" int64_t cubed_gemm_dist_b_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                                           const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,
+                                           int32_t out_dtype) {
+  if (!tasks || !segs || ti < 1 || tj < 1) return fail("dist: bad argument");
+  PackPlan pp;
+  GemmGrid gg;
+  if (int rc = dist_local_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  return pp.TN * pp.pstride;
+}
+
+extern "C" int cubed_gemm_dist_pack_b(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti,
+                                      int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
+                                      int64_t nsegs, int32_t in_dtype, int32_t out_dtype, void* d_ws,
+                                      int64_t ws_bytes, void* stream) {
+  if (!tasks || !segs || !d_tasks || !d_segs || ti < 1 || tj < 1) return fail("dist: bad argument");
+  PackPlan pp;
+  GemmGrid gg;
+  if (int rc = dist_local_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  if (!d_ws || ws_bytes < pp.TN * pp.pstride || ((uintptr_t)d_ws & 255)) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_dist_pack_b: the workspace is missing, short or not 256-B aligned");
+    return CUBED_E_WORKSPACE;
+  }
+  const int64_t nb = pp.TN * pp.KTL;
+  const dim3 gb((unsigned)(nb < 16384 ? nb : 16384));
+  hipStream_t st = (hipStream_t)stream;
+  if (in_dtype == CUBED_F32)
+    hipLaunchKernelGGL(k_pack_b_f32, gb, dim3(256), 0, st, d_tasks, d_segs, pp, (char*)d_ws);
+  else
+    hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, st, d_tasks, d_segs, pp, (char*)d_ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
+
+extern "C" int cubed_gemm_dist_gemm(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti,
+                                    int64_t tj, const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,
+                                    int32_t out_dtype, const void* d_image, int64_t image_bytes, const void* d_ws,
+                                    int64_t ws_bytes, void* stream) {
+  if (!tasks || !segs || !d_tasks || ti < 1 || tj < 1) return fail("dist: bad argument");
+  PackPlan pp;
+  GemmGrid gg;
+  if (int rc = dist_local_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
+  if (!d_image || image_bytes < pp.KTL * pp.akstride || ((uintptr_t)d_image & 255) || !d_ws ||
+      ws_bytes < pp.TN * pp.pstride || ((uintptr_t)d_ws & 255)) {
+    snprintf(g_err, sizeof(g_err), "cubed_gemm_dist_gemm: the A image or B workspace is missing, short or misaligned");
+    return CUBED_E_WORKSPACE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(pp.TM * pp.TN));
+  const char* PA = (const char*)d_image;
+  const char* PB = (const char*)d_ws;
+  if (in_dtype == CUBED_F32)
+    hipLaunchKernelGGL((k_gemm_f32_w4p<false>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
+  else if (out_dtype == CUBED_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
+  return 0;
+}
 
 extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
                                          const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype,

@@ -27,15 +27,15 @@ constexpr int WPF_SA = HF_BM * WPF_BK * 4, WPF_SB = WPF_BK * HF_BN * 4, WPF_STAG
 __global__ __launch_bounds__(256) void k_pack_a_f32(const cubed_gemm_chain_t* __restrict__ tasks,
                                                     const cubed_gemm_seg_t* __restrict__ segs, PackPlan pp,
                                                     char* __restrict__ PA) {
-  const int64_t nblk = pp.TM * pp.KTL;
+  const int64_t nkt = pp.kt1 - pp.kt0, nblk = pp.TM * nkt;
   const cubed_gemm_seg_t* __restrict__ sg0 = segs + tasks[0].seg0;
   const int sl = threadIdx.x & 3;
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t mt = blk / pp.KTL, kt = blk - mt * pp.KTL;
+    const int64_t mt = blk / nkt, kt = pp.kt0 + (blk - mt * nkt);
     const int64_t I0 = (mt * 256) / pp.cm, mb = (I0 + 1) * pp.cm;
     int64_t s0 = 0, ks0 = 0;
     if (kt * 16 < pp.K) seg_at(sg0, kt * 16, s0, ks0);
-    char* dst = PA + mt * pp.pstride + kt * WPF_SA;
+    char* dst = PA + mt * pp.apstride + kt * pp.akstride;
 #pragma unroll 2
     for (int j = 0; j < 4; ++j) {
       const int r = (threadIdx.x >> 2) + 64 * j, c = sl ^ ((r >> 2) & 3);
@@ -113,12 +113,13 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_
   const int wm = (w >> 1) * 128, wn = (w & 1) * 128;
   // pieces 0..3: A rows 64 w + 16 i .. +15 = block bytes (4 w + i) KiB; 4..7:
   // B k-row 4 w + i - 4 = block bytes (4 w + i - 4) KiB; lane-linear 16 B each
-  const char* const sA = PA + (m0 / 256) * pp.pstride + (4 * w) * 1024 + lane * 16;
+  const char* const sA = PA + (m0 / 256) * pp.apstride + (4 * w) * 1024 + lane * 16;
+  const int64_t aks = pp.akstride;
   const char* const sB = PB + (n0 / 256) * pp.pstride + (4 * w) * 1024 + lane * 16;
 #define WPF_PIECE(i, p, buf)                                                                    \
   do {                                                                                          \
     if constexpr ((i) < 4)                                                                      \
-      glds16(sA + (p) * WPF_SA + (i) * 1024, (buf) + (4 * w + (i)) * 1024);                     \
+      glds16(sA + (p) * aks + (i) * 1024, (buf) + (4 * w + (i)) * 1024);                        \
     else                                                                                        \
       glds16(sB + (p) * WPF_SB + ((i) - 4) * 1024, (buf) + WPF_SA + (4 * w + (i) - 4) * 1024); \
   } while (0)

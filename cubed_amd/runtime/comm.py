@@ -210,17 +210,60 @@ class LoopbackMesh:
       that pair (a per-pair cursor that wraps, so every step of a rank
       consumes the pair's sequence once) -- the bytes land exactly where the
       peer's RCCL send would put them, so the assembled target of all ranks
-      can be checked bit for bit.  Sends are not copied again."""
+      can be checked bit for bit.  A replayed send overwrites its recorded
+      bytes (a send cursor per pair), so sends that depend on earlier
+      receives (a halo received, then packed into what is sent on) are
+      right after one more replay pass.
+
+    Collectives (all-reduce, reduce, reduce-scatter, all-gather, all-to-all,
+    broadcast) are matched by their per-rank issue index the same way: the
+    record pass keeps every rank's inputs, a replay pass overwrites the
+    rank's own input and computes its output from ALL ranks' inputs of that
+    index, summed in rank order (RCCL's association on a ring is not
+    specified; rank order is the reference association the tests use)."""
 
     def __init__(self, world: int):
         self.world = world
         self.phase = "record"
         self.box: Dict = {}
         self.cursor: Dict = {}
+        self.scursor: Dict = {}
+        self.coll: Dict = {}  # rank -> [(kind, {name: tensor or splits})] in issue order
+        self.ccursor: Dict = {}
         self.log: List = []  # (src, dst, nbytes) of every recorded send, in issue order
 
     def bytes_between(self, src: int, dst: int) -> int:
         return sum(t.numel() * t.element_size() for t in self.box.get((src, dst), ()))
+
+    def collective(self, rank: int, kind: str, parts: Dict):
+        """Record (record phase) or refresh (replay) rank ``rank``'s inputs of
+        its next collective; in replay returns every rank's inputs of that
+        index, in rank order (None while recording)."""
+        lst = self.coll.setdefault(rank, [])
+        if self.phase == "record":
+            lst.append((kind, {k: v.detach().clone() if hasattr(v, "detach") else v for k, v in parts.items()}))
+            return None
+        if not lst:
+            raise RuntimeError(f"rank {rank}: no collective recorded")
+        i = self.ccursor.get(rank, 0)
+        self.ccursor[rank] = (i + 1) % len(lst)
+        rk, rec = lst[i]
+        if rk != kind:
+            raise RuntimeError(f"rank {rank}: collective {i} is {kind}, recorded {rk}")
+        for k, v in parts.items():
+            if hasattr(v, "detach"):
+                if rec[k].shape != v.shape:
+                    raise RuntimeError(f"rank {rank}: collective {i} ({kind}) changed shape")
+                rec[k].copy_(v)
+            else:
+                rec[k] = v
+        out = []
+        for q in range(self.world):
+            ql = self.coll.get(q)
+            if not ql or len(ql) <= i or ql[i][0] != kind:
+                raise RuntimeError(f"rank {q} has no {kind} at index {i} (rank {rank} has)")
+            out.append(ql[i][1])
+        return out
 
 
 class LoopbackComm:
@@ -272,7 +315,21 @@ class LoopbackComm:
         pass
 
     def all_to_all(self, recv, send, recv_splits, send_splits):
-        n = min(sum(map(int, recv_splits)), sum(map(int, send_splits)))
+        rs, ss = list(map(int, recv_splits)), list(map(int, send_splits))
+        got = self._meshed("all_to_all", send=send[:sum(ss)], splits=ss)
+        if got is not None:
+            # the segment from rank q is q's send segment addressed to this rank
+            o = 0
+            for q in range(self.world):
+                qs = got[q]["splits"]
+                if qs[self.rank] != rs[q]:
+                    raise RuntimeError(f"rank {self.rank}: rank {q} sends {qs[self.rank]} B, "
+                                       f"{rs[q]} B expected")
+                s0 = sum(qs[:self.rank])
+                recv[o:o + rs[q]].copy_(got[q]["send"][s0:s0 + rs[q]])
+                o += rs[q]
+            return
+        n = min(sum(rs), sum(ss))
         if n:
             recv[:n].copy_(send[:n])
 
@@ -293,6 +350,16 @@ class LoopbackComm:
             if mesh is not None and mesh.phase == "record":
                 mesh.box.setdefault((self.rank, peer), []).append(t.detach().reshape(-1).clone())
                 mesh.log.append((self.rank, peer, nb))
+            elif mesh is not None:
+                key = (self.rank, peer)
+                box = mesh.box.get(key)
+                if not box:
+                    raise RuntimeError(f"rank {self.rank}: no send to rank {peer} recorded")
+                i = mesh.scursor.get(key, 0)
+                mesh.scursor[key] = (i + 1) % len(box)
+                if box[i].numel() * box[i].element_size() != nb:
+                    raise RuntimeError(f"rank {self.rank}: send {i} to rank {peer} changed size")
+                box[i].copy_(t.detach().reshape(-1))
         for t, peer in recvs:
             if not 0 <= peer < self.world or peer == self.rank:
                 raise ValueError(f"rank {self.rank} receives from {peer}")
@@ -327,29 +394,61 @@ class LoopbackComm:
     def _reduce(self, kind, t):
         if self.record:
             self.records.append((kind, t.detach().clone()))
-        if not self.skip_collectives:
+        if not self.skip_collectives and self.mesh is None:
             self._copy(t)
+
+    def _meshed(self, kind, **parts):
+        """Every rank's inputs of this collective (replay), else None."""
+        if self.mesh is None:
+            return None
+        return self.mesh.collective(self.rank, kind, parts)
+
+    @staticmethod
+    def _sum(ts):
+        acc = ts[0].clone()
+        for t in ts[1:]:
+            acc += t
+        return acc
 
     def all_reduce_sum(self, t):
         self._reduce("all_reduce_sum", t)
+        got = self._meshed("all_reduce_sum", t=t)
+        if got is not None:
+            t.copy_(self._sum([g["t"] for g in got]))
 
     def reduce_sum(self, t, dst: int):
         self._reduce("reduce_sum", t)
+        got = self._meshed("reduce_sum", t=t)
+        if got is not None and self.rank == dst:
+            t.copy_(self._sum([g["t"] for g in got]))
 
     def reduce_scatter_sum(self, out, t):
         self._reduce("reduce_scatter_sum", t)
-        if not self.skip_collectives:
+        got = self._meshed("reduce_scatter_sum", t=t)
+        if got is not None:
+            out.copy_(self._sum([g["t"] for g in got]).view(self.world, -1)[self.rank])
+        elif not self.skip_collectives:
             out.copy_(t.view(self.world, -1)[self.rank])
 
     def all_gather(self, out, t):
-        if self.skip_collectives:
-            return
+        got = self._meshed("all_gather", t=t)
         flat = t.reshape(-1)
         o = out.reshape(-1)
+        if got is not None:
+            for r in range(self.world):
+                o[r * flat.numel():(r + 1) * flat.numel()].copy_(got[r]["t"].reshape(-1))
+            return
+        if self.skip_collectives:
+            return
         for r in range(self.world):
             o[r * flat.numel():(r + 1) * flat.numel()].copy_(flat)
 
     def broadcast(self, t, src: int):
+        got = self._meshed("broadcast", t=t)
+        if got is not None:
+            if self.rank != src:
+                t.copy_(got[src]["t"])
+            return
         if not self.skip_collectives:
             self._copy(t)
 

@@ -471,6 +471,10 @@ class DistPiecesLaunch:
             for f in range(self.nf):
                 if self.host_count[f]:
                     self.field_view(f).view(self.ngroups, self.mko).copy_(hc[:, None].expand(self.ngroups, self.mko))
+        # owners: the rank finishing each GROUP (one entry per group; a key
+        # cut along a kept dim has several groups, all owned by its owner)
+        if len(owners) != self.ngroups:
+            raise ValueError(f"{len(owners)} owners for {self.ngroups} groups")
         uniq = sorted(set(owners))
         self.root = uniq[0] if len(uniq) == 1 else None
         self.finish_here = ctx.rank in uniq
@@ -528,3 +532,249 @@ class DistPiecesLaunch:
                           "cubed_combine_partials")
         if self.finish_here:
             fused_finish(F, self.group_table, self.ngroups, self.mko, self.gsoa, stream)
+
+
+# k block of the packed GEMM images (bf16: 64-deep tiles of 32 KiB per
+# 256-row panel; f32: 16-deep steps of 16 KiB), csrc/gemm_bf16_w4p.h / _f32_
+KBLOCK = {2: (64, 32768), 4: (16, 16384)}
+LINK_GBPS = 153.0  # ASSUMED xGMI rate per link and direction (MI355X_MICROARCH.md); rehearsal predictions only
+
+
+class DistGemmLaunch:
+    """A matmul's chunk products + k-sum (linear_algebra_functions.py:35-78)
+    on W ranks, when the block-cyclic ownership gives every k chunk q of A
+    ONE rank (q mod W: A's chunk columns nk % W == 0) and every chunk column j
+    of C and of B one rank (j mod W: nj % W == 0) -- config 5's 8 x 8 grid at
+    W = 1, 2, 4, 8.  Rank r computes its C columns from ALL of A and its own
+    B columns, so A is the only operand that moves:
+
+    1. halo: the owner of chunk q+1 sends the first h_q columns of its A
+       chunks (the part of the k block straddling the q / q+1 edge) to the
+       owner of q (h_q < one k block; one small box copy + p2p);
+    2. pack A: each rank packs the k blocks starting in its own chunks into
+       ONE k-major image of the whole packed A (cubed_gemm_dist_pack_a);
+    3. exchange: each rank sends its blocks (one contiguous run per owned k
+       chunk) to every peer, received in place into the same image (grouped
+       point-to-point: every peer pair on its own xGMI link, no pack and no
+       unpack); B's pack (its own chunks, cubed_gemm_dist_pack_b) runs
+       meanwhile;
+    4. GEMM: the single-GPU packed kernel over the rank's C columns
+       (cubed_gemm_dist_gemm).
+
+    The image holds exactly the single-GPU packed A (same blocks, same
+    order of k), so every element is the same f32 chain over K: the result
+    is bit-identical to one GPU's."""
+
+    def __init__(self, ctx, A, B, F, ti, nk, nj, in_code, out_code, isz):
+        import torch
+
+        from ... import ir
+
+        W, r = ctx.world, ctx.rank
+        self.ctx = ctx
+        self.in_code, self.out_code = in_code, out_code
+        T, blk = KBLOCK[isz]
+        kw = [A.chunk_extent((0, q))[1] for q in range(nk)]
+        ks = [sum(kw[:q]) for q in range(nk + 1)]
+        K = ks[-1]
+        M = A.shape[0]
+        rows = [A.chunk_extent((i, 0))[0] for i in range(ti)]
+        TM = -(-M // 256)
+        KTL = -(-K // T)
+        self.K, self.M, self.TM, self.KTL, self.blk = K, M, TM, KTL, blk
+        L = nat.lib()
+        self.image_bytes = int(L.cubed_gemm_dist_image_bytes(M, K, in_code))
+        assert self.image_bytes == KTL * TM * blk
+        dev = ctx.device
+        self.image = torch.empty(self.image_bytes, dtype=torch.uint8, device=dev)
+        ib = self.image.data_ptr()
+        # k blocks packed by the owner of chunk q: those starting inside it
+        self.ranges = [(-(-ks[q] // T), min(KTL, -(-ks[q + 1] // T))) for q in range(nk)]
+        self.halo_w = [min(K, self.ranges[q][1] * T) - ks[q + 1] for q in range(nk)]
+        self.owned = [q for q in range(nk) if q % W == r]
+        # -- halo buffers: [M][h_q] per owned q whose last block reaches into q+1
+        self.halo = {}
+        sends, recvs, hboxes = [], [], []
+        off = 0
+        need = {q: M * self.halo_w[q] * isz for q in self.owned if self.halo_w[q] > 0}
+        self.halo_buf = torch.empty(max(sum(need.values()), 16), dtype=torch.uint8, device=dev)
+        for q in self.owned:
+            if self.halo_w[q] > 0:
+                self.halo[q] = (self.halo_buf.data_ptr() + off, off)
+                off += need[q]
+        out_halo = [q for q in range(nk - 1) if (q + 1) % W == r and self.halo_w[q] > 0]
+        send_bytes = sum(M * self.halo_w[q] * isz for q in out_halo)
+        self.halo_send = torch.empty(max(send_bytes, 16), dtype=torch.uint8, device=dev)
+        so = 0
+        for q in out_halo:
+            h = self.halo_w[q]
+            base = self.halo_send.data_ptr() + so
+            row0 = 0
+            for i in range(ti):
+                src = A.chunk_addr((i, q + 1))
+                hboxes.append(Box(src, base + row0 * h * isz, [rows[i], h], [kw[q + 1], 1], [h, 1]))
+                row0 += rows[i]
+            sends.append((self.halo_send[so:so + M * h * isz], q % W))
+            so += M * h * isz
+        for q in self.owned:
+            if q in self.halo:
+                o = self.halo[q][1]
+                recvs.append((self.halo_buf[o:o + need[q]], (q + 1) % W))
+        self.halo_pack = CopyLaunch(hboxes, isz, dev)
+        self.halo_sends, self.halo_recvs = sends, recvs
+        # -- A pack tables: task I = chunk row I, segment q = A(I, q) here, the
+        # halo of q+1 where q is ours, else absent (0)
+        nat_tasks = np.zeros(ti, dtype=nat.CHAIN_DTYPE)
+        nat_segs = np.zeros(ti * nk, dtype=nat.SEG_DTYPE)
+        for i in range(ti):
+            row0 = sum(rows[:i])
+            for q in range(nk):
+                a, lda = 0, kw[q]
+                if q % W == r:
+                    a = A.chunk_addr((i, q))
+                elif q >= 1 and (q - 1) in self.halo:
+                    h = self.halo_w[q - 1]
+                    a, lda = self.halo[q - 1][0] + row0 * h * isz, h
+                nat_segs[i * nk + q] = (a, 0, kw[q], lda, 1, 0)
+            nat_tasks[i] = (0, rows[i], 1, 1, i * nk, nk, K, 0)
+        self.a_tasks, self.a_segs = nat_tasks, nat_segs
+        self.d_a_tasks = torch.from_numpy(nat_tasks.view(np.uint8).copy()).to(dev)
+        self.d_a_segs = torch.from_numpy(nat_segs.view(np.uint8).copy()).to(dev)
+        # -- the image's exchange: every owned range to every peer, in place
+        rs, rr = [], []
+        self.bytes_out = 0
+        for q in range(nk):
+            lo, hi = self.ranges[q]
+            view = self.image[lo * TM * blk:hi * TM * blk]
+            if q % W == r:
+                for p in range(W):
+                    if p != r:
+                        rs.append((view, p))
+                self.bytes_out += (W - 1) * view.numel()
+            else:
+                rr.append((view, q % W))
+        self.region_sends, self.region_recvs = rs, rr
+        self.bytes_in = sum(v.numel() for v, _ in rr)
+        self.own_bytes = {p: sum((self.ranges[q][1] - self.ranges[q][0]) * TM * blk
+                                 for q in range(nk) if q % W == p) for p in range(W)}
+        # -- the rank's C grid: rows I, its chunk columns j = r, r + W, ...
+        cols = [j for j in range(nj) if j % W == r]
+        self.ti, self.tj = ti, len(cols)
+        tasks = np.zeros(ti * len(cols), dtype=nat.CHAIN_DTYPE)
+        segs = np.zeros(ti * len(cols) * nk, dtype=nat.SEG_DTYPE)
+        self.flops = 0.0
+        for i in range(ti):
+            for jl, j in enumerate(cols):
+                t = i * len(cols) + jl
+                key = (i, j) if F.ndim == 2 else (i, 0, j)
+                m, n = F.chunk_extent(key)[0], F.chunk_extent(key)[-1]
+                for q in range(nk):
+                    a = A.chunk_addr((i, q)) if q % W == r else 0
+                    segs[t * nk + q] = (a, B.chunk_addr((q, j)), kw[q], kw[q], n, 0)
+                tasks[t] = (F.chunk_addr(key), m, n, n, t * nk, nk, K, 0)
+                self.flops += 2.0 * m * n * K
+        self.tasks, self.segs = tasks, segs
+        self.b_bytes = int(L.cubed_gemm_dist_b_bytes(tasks.ctypes.data, ti, len(cols), segs.ctypes.data,
+                                                     len(segs), in_code, out_code))
+        if self.b_bytes < 0:
+            nat.check(int(self.b_bytes), "cubed_gemm_dist_b_bytes")
+        self.bws = torch.empty(max(self.b_bytes, 256), dtype=torch.uint8, device=dev)
+        self.d_tasks = torch.from_numpy(tasks.view(np.uint8).copy()).to(dev)
+        self.d_segs = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+        self.collective = True
+        self.phase_ms = {}
+
+    def _pack_a(self, stream):
+        L = nat.lib()
+        for q in self.owned:
+            lo, hi = self.ranges[q]
+            nat.check(L.cubed_gemm_dist_pack_a(self.a_tasks.ctypes.data, self.d_a_tasks.data_ptr(), self.ti,
+                                               self.a_segs.ctypes.data, self.d_a_segs.data_ptr(),
+                                               len(self.a_segs), self.in_code, lo, hi, self.image.data_ptr(),
+                                               self.image_bytes, stream), "cubed_gemm_dist_pack_a")
+
+    def _pack_b(self, stream):
+        nat.check(nat.lib().cubed_gemm_dist_pack_b(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.ti,
+                                                   self.tj, self.segs.ctypes.data, self.d_segs.data_ptr(),
+                                                   len(self.segs), self.in_code, self.out_code,
+                                                   self.bws.data_ptr(), self.b_bytes, stream),
+                  "cubed_gemm_dist_pack_b")
+
+    def _gemm(self, stream):
+        nat.check(nat.lib().cubed_gemm_dist_gemm(self.tasks.ctypes.data, self.d_tasks.data_ptr(), self.ti, self.tj,
+                                                 self.segs.ctypes.data, len(self.segs), self.in_code,
+                                                 self.out_code, self.image.data_ptr(), self.image_bytes,
+                                                 self.bws.data_ptr(), self.b_bytes, stream),
+                  "cubed_gemm_dist_gemm")
+
+    def run(self, stream):
+        timing = getattr(self.ctx, "timing", None)
+        if timing is not None and getattr(self.ctx.comm, "backend", None) == "loopback":
+            return self._run_phases(stream, timing)
+        comm = self.ctx.comm
+        self.halo_pack.run(stream)
+        comm.exchange(self.halo_sends, self.halo_recvs).wait()
+        self._pack_a(stream)
+        pending = comm.exchange(self.region_sends, self.region_recvs)
+        self._pack_b(stream)  # overlaps the transfers
+        pending.wait()
+        self._gemm(stream)
+
+    def _run_phases(self, stream, timing):
+        """A rehearsed rank under bench timing: the same launches with HIP
+        events around each phase, back to back on one stream."""
+        import torch
+
+        cur = torch.cuda.current_stream()
+        comm = self.ctx.comm
+
+        def timed(name, fn):
+            e0, e1 = timing.events()
+            e0.record(cur)
+            fn()
+            e1.record(cur)
+            timing.add(("matmul", 0, name), e0, e1)
+
+        timed("halo", lambda: (self.halo_pack.run(stream), comm.exchange(self.halo_sends, self.halo_recvs).wait()))
+        timed("pack_a", lambda: self._pack_a(stream))
+        timed("slot_writes", lambda: comm.exchange(self.region_sends, self.region_recvs).wait())
+        timed("pack_b", lambda: self._pack_b(stream))
+        timed("gemm", lambda: self._gemm(stream))
+
+    def predicted_xfer_ms(self, gbps=LINK_GBPS):
+        """The exchange at ``gbps`` per link and direction, every peer pair
+        on its own link: the busiest link carries one rank's whole blocks."""
+        return max(self.own_bytes.values()) / (gbps * 1e9) * 1e3
+
+
+def dist_gemm_plan(ex, chain, F):
+    """(A, B, ti, nk, nj) when the chain runs as a DistGemmLaunch on ex's
+    ranks, else None (the fetch path runs it)."""
+    from ... import ir
+    from ...gemm_chains import K_AXIS
+    from ...storage import DeviceArray
+
+    W = ex.world
+    G = chain.gemm_target
+    nk = G.numblocks[K_AXIS]
+    ti, nj = F.numblocks[0], F.numblocks[-1]
+    args = chain.gemm_spec.block_function(("out", 0, 0, 0))
+    A = ex.device_source(chain.gemm_spec.reads_map[args[0][0]].array)
+    B = ex.device_source(chain.gemm_spec.reads_map[args[1][0]].array)
+    if not all(isinstance(x, DeviceArray) and x.world == W and x.ndim == 2 for x in (A, B)) or F.world != W:
+        return None
+    if A.dtype != B.dtype or A.dtype not in (np.dtype(np.float32), ir.bfloat16):
+        return None
+    if A.numblocks != (ti, nk) or B.numblocks != (nk, nj) or nk % W or nj % W:
+        return None
+    for i in (0, ti - 1):
+        for k in (0, nk - 1):
+            for j in (0, nj - 1):
+                a, b = chain.gemm_spec.block_function(("out", i, k, j))[:2]
+                if tuple(a[1:]) != (i, k) or tuple(b[1:]) != (k, j):
+                    return None
+    T, _ = KBLOCK[A.dtype.itemsize]
+    kw = [A.chunk_extent((0, q))[1] for q in range(nk)]
+    if min(kw) < T or any(w % (16 // A.dtype.itemsize) for w in kw):
+        return None
+    return A, B, ti, nk, nj

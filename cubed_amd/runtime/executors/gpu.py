@@ -64,6 +64,10 @@ from ..pipeline import visit_nodes
 from ..types import DagExecutor, TaskEndEvent
 
 HBM_BYTES_PER_GPU = 288 * 10**9
+# multi-GPU matmuls whose A k chunks / C columns each live on one rank run as
+# dist.DistGemmLaunch (packed A image exchanged in place); tests flip it to
+# compare with the whole-chunk fetch path
+DIST_GEMM = True
 
 
 def gather_to_host(arr: DeviceArray) -> np.ndarray:
@@ -533,6 +537,9 @@ class GpuDagExecutor(DagExecutor):
                                   for r in rows)
             meta["mko"] = mko
             meta["counts"] = [counts[gkeys[i]] for i in meta["starts"]]
+            # the output block of every group (several groups per key when the
+            # pieces cut a kept dim): the combine's owner of each group
+            meta["group_keys"] = [gkeys[i][0] for i in meta["starts"]]
             return rows, red
 
         def one_row_per_group():
@@ -557,7 +564,8 @@ class GpuDagExecutor(DagExecutor):
         out = [meta["fetch"]] if meta.get("fetch") is not None else []
         glay = dataclasses.replace(lay, rows=[lay.rows[i] for i in starts])
         out.append(DistPiecesLaunch(self, launch, np.array(starts + [len(lay.rows)], dtype=np.int64),
-                                    table, meta["mko"], rops, acc_int, [target.owner(k) for k in keys],
+                                    table, meta["mko"], rops, acc_int,
+                                    [target.owner(k) for k in meta["group_keys"]],
                                     soa_direct=soa_direct,
                                     host_counts=meta["counts"] if launch.prog.mode & MODE_HOST_COUNT else None,
                                     group_layout=glay, discard=meta["discard"], group_counts=meta["counts"]))
@@ -824,6 +832,23 @@ class GpuDagExecutor(DagExecutor):
             pre, tasks, segs, in_dt, out_dt = complex_chain_tables(self, chain, keys)
             return pre + [GemmLaunch(tasks, segs, ir.dtype_code(in_dt), ir.dtype_code(out_dt), self.device,
                                      self.zero_page())]
+        if self.world > 1 and DIST_GEMM:
+            from .dist import DistGemmLaunch, dist_gemm_plan
+
+            plan = dist_gemm_plan(self, chain, F)
+            ok = plan is not None
+            if ok:
+                A = plan[0]
+                need = nat.lib().cubed_gemm_dist_image_bytes(A.shape[0], A.shape[1],
+                                                             ir.dtype_code(A.dtype))
+                ok = not (self.check_memory and
+                          self._resident_bytes + self.owned_bytes() + need > HBM_BYTES_PER_GPU)
+            # every rank takes the same path (their transfers pair up)
+            if self.comm.all_ok(ok):
+                A, B, ti, nk, nj = plan
+                code = ir.dtype_code(A.dtype)
+                return [DistGemmLaunch(self, A, B, F, ti, nk, nj, code, ir.dtype_code(F.dtype),
+                                       A.dtype.itemsize)]
         if self.world > 1:
             def reads(k):
                 G = chain.gemm_target

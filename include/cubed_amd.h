@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 14
+#define CUBED_ABI_VERSION 15
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -440,6 +440,41 @@ int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_ch
                             int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs,
                             int64_t nsegs, int32_t in_dtype, int32_t out_dtype, void* d_ws, int64_t ws_bytes,
                             void* stream);
+
+/* Multi-GPU matmul on packed operands (ABI 15).  Replaces, on W ranks, the
+ * same _matmul chunk products + _sum_wo_cat k-sum
+ * (cubed/array_api/linear_algebra_functions.py:35-78) when the block-cyclic
+ * ownership gives every k chunk of A one rank and every chunk column of C
+ * (and of B) one rank.  A is packed into ONE k-major image of the whole A
+ * (block (mt, kt) at (kt * TM + mt) * block bytes; bf16: 32 KiB blocks of 256
+ * rows x 64 k, f32: 16 KiB of 256 rows x 16 k, the single-GPU packed blocks),
+ * so the k blocks a rank packs are one contiguous byte run it sends whole to
+ * every peer; the block straddling two k chunks is packed by the owner of
+ * the first one from a received halo of the next chunk's first columns.
+ * Every element stays the single-GPU packed path's f32 chain over K.
+ * cubed_gemm_dist_image_bytes (host only): the image's size.
+ * cubed_gemm_dist_pack_a: a_tasks = one task per A chunk row (m rows,
+ *   segments = its k chunks: a = the chunk, a halo buffer (lda = its width)
+ *   or 0 where the rank has neither); packs k blocks [kt0, kt1), which must
+ *   read only present segments (else CUBED_E_LAYOUT, nothing launched).
+ * cubed_gemm_dist_b_bytes / cubed_gemm_dist_pack_b: B (B^T for bf16) of the
+ *   rank's own C chunk grid (ti x tj tasks, as cubed_gemm_chain_packed; the
+ *   A addresses are not read) packed into d_ws.
+ * cubed_gemm_dist_gemm: the rank's C chunks from the filled image and d_ws. */
+int64_t cubed_gemm_dist_image_bytes(int64_t M, int64_t K, int32_t in_dtype);
+int cubed_gemm_dist_pack_a(const cubed_gemm_chain_t* a_tasks, const cubed_gemm_chain_t* d_a_tasks, int64_t ti,
+                           const cubed_gemm_seg_t* a_segs, const cubed_gemm_seg_t* d_a_segs, int64_t nsegs,
+                           int32_t in_dtype, int64_t kt0, int64_t kt1, void* d_image, int64_t image_bytes,
+                           void* stream);
+int64_t cubed_gemm_dist_b_bytes(const cubed_gemm_chain_t* tasks, int64_t ti, int64_t tj,
+                                const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype, int32_t out_dtype);
+int cubed_gemm_dist_pack_b(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti,
+                           int64_t tj, const cubed_gemm_seg_t* segs, const cubed_gemm_seg_t* d_segs, int64_t nsegs,
+                           int32_t in_dtype, int32_t out_dtype, void* d_ws, int64_t ws_bytes, void* stream);
+int cubed_gemm_dist_gemm(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks, int64_t ti, int64_t tj,
+                         const cubed_gemm_seg_t* segs, int64_t nsegs, int32_t in_dtype, int32_t out_dtype,
+                         const void* d_image, int64_t image_bytes, const void* d_ws, int64_t ws_bytes,
+                         void* stream);
 
 /* ---- Zarr v2 chunk codecs (host only; cubed_amd/csrc/codec.cpp) --------
  * Replace numcodecs.Blosc's decode/encode behind zarr's chunk reads and

@@ -41,7 +41,7 @@ class DryExecutor(g.GpuDagExecutor):
 
         saved = {}
         for cls in (L.FusedLaunch, L.CopyLaunch, L.GemmLaunch, D.FetchLaunch, D.RechunkLaunch,
-                    D.PartialsLaunch, D.DistPiecesLaunch):
+                    D.PartialsLaunch, D.DistPiecesLaunch, D.DistGemmLaunch):
             saved[cls] = cls.run
             cls.run = lambda launch, stream, _log=self.launched: _log.append(launch)
         try:

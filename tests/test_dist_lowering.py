@@ -248,6 +248,42 @@ def test_rechunk_mean_runs_pieces_where_chunks_live(built, monkeypatch, merge):
     assert total == (50 * 50 if not merge else 50 * world)
 
 
+def test_scatter_owners_are_per_group_when_pieces_cut_a_kept_dim(built):
+    """Source chunks (10, 7) rechunked to (500, 10) columns: every target
+    column block straddles two source column chunks, so a key has SEVERAL
+    groups (one per kept interval).  The combine's owner list is per group
+    (the owner of the group's key): the reduce-scatter permutation, the host
+    counts and the finish rows all follow it (a per-key list would slice the
+    partials at the wrong field stride)."""
+    world = 4
+    x = np.ones((500, 500), dtype=np.float32)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+        a = cubed.from_array(x, chunks=(10, 7), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        m = xp.mean(a.rechunk((500, 10)), axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        dps = [l for l in dry.launched if isinstance(l, DistPiecesLaunch)]
+        assert len(dps) == 1
+        dp = dps[0]
+        nkeys = m.zarray.numblocks[0]
+        assert dp.ngroups > nkeys  # pieces cut the kept dim
+        sc = dp.scatter
+        assert sc is not None and sc.G == dp.ngroups
+        # each group's owner is its key's owner, and the groups of one key are
+        # consecutive: owner-major slots of this rank = its keys' groups
+        tbl = sc.dst.view(sc.f1 - sc.f0, sc.G)[0].tolist()
+        owner_of = [t // ((sc.f1 - sc.f0) * sc.L) for t in tbl]
+        assert sorted(set(owner_of)) == sorted({k % world for k in range(nkeys)})
+        mine = [g for g in range(sc.G) if owner_of[g] == rank]
+        assert sc.mine == mine
+        # every group of this rank is counted over all 500 rows
+        cnt = sc.fin.view(torch.int64)[:sc.L * sc.mko].view(sc.L, sc.mko)[:len(mine), 0]
+        assert (cnt == 500).all()
+
+
 def test_rechunk_mean_combines_by_reduce_scatter(built):
     """Several owners of the output blocks: the group partials combine by
     ONE reduce-scatter in owner-major order (each rank receives only its own
@@ -270,3 +306,67 @@ def test_rechunk_mean_combines_by_reduce_scatter(built):
         cnt = sc.fin.view(torch.int64)[:13 * 10].view(13, 10)
         k = len(sc.mine)  # the counts of this rank's blocks, then padding slots
         assert (cnt[:k] == 500).all() and (cnt[k:] == 1).all()
+
+
+# ------------------------------------------------ multi-GPU matmul (packed A image)
+
+
+def _matmul_dry(rank, world, dtype, shape=(700, 1600, 2048), chunks=(300, 200, 264)):
+    from cubed_amd.runtime.executors.dist import DistGemmLaunch
+
+    M, K, N = shape
+    dry = DryExecutor(FakeComm(rank, world))
+    spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+    random.seed(3)
+    A = xp.astype(crandom.random((M, K), chunks=(chunks[0], chunks[1]), spec=spec), dtype)
+    B = xp.astype(crandom.random((K, N), chunks=(chunks[1], chunks[2]), spec=spec), dtype)
+    arrays_to_plan(A, B).execute(executor=dry, array_names=[A.name, B.name])
+    dry.launched.clear()
+    C = xp.matmul(A, B)
+    arrays_to_plan(C).execute(executor=dry, resume=True, array_names=[C.name])
+    return [l for l in dry.launched if isinstance(l, DistGemmLaunch)], dry.launched
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_matmul_packs_and_exchanges_the_a_image(built, world, dtype):
+    """Config 5's shape of work (8 x 8 chunk grid), reduced: every rank packs
+    the k blocks starting in its own A chunks into the k-major image, sends
+    each owned block run to every peer and receives the others' in place;
+    the block ranges tile the image exactly, halos reach < one block into
+    the next chunk, and every transfer pairs with the peer's."""
+    dt = xp.bfloat16 if dtype == "bfloat16" else xp.float32
+    T = 64 if dtype == "bfloat16" else 16
+    launches = [_matmul_dry(r, world, dt) for r in range(world)]
+    plans = []
+    for r, (dg, all_l) in enumerate(launches):
+        assert len(dg) == 1 and [type(l).__name__ for l in all_l] == ["DistGemmLaunch"]
+        d = dg[0]
+        plans.append(d)
+        assert d.K == 1600 and d.KTL == -(-1600 // T) and d.TM == 3
+        cover = sorted(x for q in range(8) for x in range(*d.ranges[q]))
+        assert cover == list(range(d.KTL))
+        for q in range(7):
+            assert 0 <= d.halo_w[q] < T and (200 * (q + 1) + d.halo_w[q]) % T == 0
+        assert d.owned == [q for q in range(8) if q % world == r]
+        assert d.tj == 8 // world and d.ti == 3
+        assert d.bytes_out == (world - 1) * d.own_bytes[r]
+        assert d.bytes_in == sum(d.own_bytes[p] for p in range(world) if p != r)
+    # transfers pair up: per (sender, receiver) the same sizes in the same order
+    for s in range(world):
+        for p in range(world):
+            if s == p:
+                continue
+            sent = [v.numel() for v, peer in plans[s].region_sends if peer == p]
+            got = [v.numel() for v, peer in plans[p].region_recvs if peer == s]
+            assert sent == got and sent
+            hs = [v.numel() for v, peer in plans[s].halo_sends if peer == p]
+            hr = [v.numel() for v, peer in plans[p].halo_recvs if peer == s]
+            assert hs == hr
+
+
+def test_matmul_off_the_regular_ownership_fetches_chunks(built):
+    """3 ranks do not divide an 8 x 8 chunk grid: the whole-chunk fetch path
+    (FetchLaunch + the chained GEMM) runs instead."""
+    dg, all_l = _matmul_dry(0, 3, xp.float32)
+    assert not dg and "FetchLaunch" in [type(l).__name__ for l in all_l]

@@ -88,9 +88,10 @@ def test_eight_rehearsed_ranks_fold_to_one_gpu_result(gpu_executor, shape, cols)
 def _targets_unwritten(plan, keep):
     from cubed_amd.storage import DeviceArray
 
+    keep_ids = keep if isinstance(keep, set) else {id(keep)}
     for _, d in plan._finalize_dag().nodes(data=True):
         t = d.get("target")
-        if isinstance(t, DeviceArray) and t is not keep:
+        if isinstance(t, DeviceArray) and id(t) not in keep_ids:
             t.written = False
 
 
@@ -156,4 +157,120 @@ def test_eight_rehearsed_ranks_rechunk_bit_exact(gpu_executor, shape, rows, cols
         assert Yo.rank == owner
         st, ext = Yo.chunk_start(tc), Yo.chunk_extent(tc)
         got[st[0]:st[0] + ext[0], st[1]:st[1] + ext[1]] = Yo.read_chunk(tc)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def _mesh_rehearsal(world, build, passes=2):
+    """Run ``build(ex) -> (inputs, out, plan)`` on every rank of a rehearsed
+    ``world`` whose collectives and transfers go through ONE LoopbackMesh:
+    a record pass, then ``passes`` replay passes (each combines every rank's
+    inputs of the same collective).  Returns the ranks' (executor, out)."""
+    import torch
+
+    from cubed_amd.runtime.comm import LoopbackComm, LoopbackMesh
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    mesh = LoopbackMesh(world)
+    ranks = []
+    for r in range(world):
+        ex = GpuDagExecutor("cuda:0", comm=LoopbackComm(r, world, mesh=mesh))
+        ins, out, plan = build(ex)
+        plan.execute(executor=ex, array_names=[out.name], resume=True)
+        ranks.append((ex, ins, out, plan))
+    torch.cuda.synchronize()
+    mesh.phase = "replay"
+    for _ in range(passes):
+        for ex, ins, out, plan in ranks:
+            _targets_unwritten(plan, set(id(a.zarray) for a in ins))
+            plan.execute(executor=ex, array_names=[out.name], resume=True)
+        torch.cuda.synchronize()
+    return ranks
+
+
+def _assemble(ranks, world):
+    """The array each rank holds a block-cyclic share of, from the owners."""
+    import itertools
+
+    Y = ranks[0][2].zarray
+    got = np.empty(Y.shape, Y.dtype)
+    for tc in itertools.product(*[range(n) for n in Y.numblocks]):
+        owner = Y.chunk_offset(tc) % world
+        Yo = ranks[owner][2].zarray
+        st, ext = Yo.chunk_start(tc), Yo.chunk_extent(tc)
+        got[tuple(slice(s, s + e) for s, e in zip(st, ext))] = Yo.read_chunk(tc)
+    return got
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_rehearsed_mean_when_pieces_cut_kept_dims(gpu_executor, world):
+    """mean(x.rechunk(cols), axis=0) whose source chunks (40, 70) cut every
+    100-wide target column block: each output block has several groups.  All
+    ranks rehearsed through one mesh (reduce-scatter combining every rank's
+    partials), the output assembled from its owners' slots equals the 1-GPU
+    result (rtol 1e-6, the f32 output of f64 sums in another association).
+    Reference: cubed/core/ops.py:849-892, primitive/rechunk.py:23-98."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.executors.dist import DistPiecesLaunch
+
+    shape = (800, 1000)
+
+    def build(ex):
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2010)
+        x = xp.astype(crandom.random(shape, chunks=(40, 70), spec=spec), xp.float32)
+        arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+        m = xp.mean(x.rechunk((shape[0], 100)), axis=0)
+        return [x], m, arrays_to_plan(m)
+
+    _, m1, p1 = build(gpu_executor)
+    want = m1.compute(resume=True)
+    ranks = _mesh_rehearsal(world, build)
+    for ex, _, _, _ in ranks:
+        dps = [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistPiecesLaunch)]
+        assert len(dps) == 1 and dps[0].ngroups > 10 and dps[0].scatter is not None
+    got = _assemble(ranks, world)
+    np.testing.assert_allclose(got, want, rtol=1e-6)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_rehearsed_matmul_bit_identical_to_one_gpu(gpu_executor, world, dtype):
+    """Config 5's matmul, reduced (8 x 8 chunk grid, ragged last chunk row and
+    column, 200-wide k chunks so every chunk edge falls inside a k block):
+    all ranks rehearsed through one mesh -- halo transfers, each rank's A
+    blocks packed into the k-major image and sent to every peer, B packed
+    locally, the packed GEMM over the rank's C columns.  C assembled from
+    its owners equals the 1-GPU result bit for bit: the image is the 1-GPU
+    packed A, so every element is the same f32 chain over K.
+    Reference: cubed/array_api/linear_algebra_functions.py:35-78."""
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.executors.dist import DistGemmLaunch
+
+    dt = xp.bfloat16 if dtype == "bfloat16" else xp.float32
+
+    def build(ex):
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(2020)
+        A = xp.astype(crandom.random((700, 1600), chunks=(300, 200), spec=spec), dt)
+        B = xp.astype(crandom.random((1600, 2048), chunks=(200, 264), spec=spec), dt)
+        arrays_to_plan(A, B).execute(executor=ex, array_names=[A.name, B.name])
+        C = xp.matmul(A, B)
+        return [A, B], C, arrays_to_plan(C)
+
+    _, C1, p1 = build(gpu_executor)
+    p1.execute(executor=gpu_executor, array_names=[C1.name], resume=True)
+    want = C1.compute(resume=True)
+    ranks = _mesh_rehearsal(world, build)
+    for ex, _, _, _ in ranks:
+        assert [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistGemmLaunch)]
+    got = _assemble(ranks, world)
+    if dtype == "bfloat16":  # compute() widens bf16 exactly to f32
+        got = (got.view(np.uint16).astype(np.uint32) << 16).view(np.float32)
+    assert got.dtype == want.dtype == np.float32
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -109,3 +109,81 @@ def test_mesh_matches_transfers_by_peer_and_order():
     bad = [(torch.zeros(5, dtype=torch.uint8), 1)]
     with pytest.raises(RuntimeError, match="B, the receive"):
         comms[0].exchange([], bad)
+
+
+def test_mesh_collectives_combine_every_rank():
+    """With a LoopbackMesh the collectives of rehearsed ranks are matched by
+    issue index: a replay pass combines ALL ranks' inputs (sums in rank
+    order), so a multi-rank reduction or all-gather rehearsed in one process
+    gives every rank what RCCL would."""
+    from cubed_amd.runtime.comm import LoopbackMesh
+
+    W = 3
+    mesh = LoopbackMesh(W)
+    comms = [LoopbackComm(r, W, mesh=mesh) for r in range(W)]
+
+    def step(r):
+        c = comms[r]
+        a = torch.arange(6, dtype=torch.float64) + 10 * r
+        c.all_reduce_sum(a)
+        red = torch.full((2,), float(r + 1), dtype=torch.float64)
+        c.reduce_sum(red, 1)
+        rs_in = torch.arange(W * 2, dtype=torch.int64) * (r + 1)
+        rs_out = torch.zeros(2, dtype=torch.int64)
+        c.reduce_scatter_sum(rs_out, rs_in)
+        g = torch.zeros(W * 2, dtype=torch.int64)
+        c.all_gather(g, torch.tensor([r, -r], dtype=torch.int64))
+        b = torch.tensor([r * 7], dtype=torch.int64)
+        c.broadcast(b, 2)
+        # all-to-all: rank r sends r+1 bytes of value 10r + q to rank q
+        ss = [r + 1] * W
+        send = torch.cat([torch.full((r + 1,), 10 * r + q, dtype=torch.uint8) for q in range(W)])
+        rsp = [q + 1 for q in range(W)]
+        recv = torch.zeros(sum(rsp), dtype=torch.uint8)
+        c.all_to_all(recv, send, rsp, ss)
+        return a, red, rs_out, g, b, recv
+
+    for r in range(W):
+        step(r)
+    mesh.phase = "replay"
+    for _ in range(2):
+        for r in range(W):
+            a, red, rs_out, g, b, recv = step(r)
+            assert a.tolist() == [3 * i + 30 for i in range(6)]
+            assert red.tolist() == ([6.0, 6.0] if r == 1 else [float(r + 1)] * 2)
+            assert rs_out.tolist() == [6 * (2 * r), 6 * (2 * r + 1)]
+            assert g.tolist() == [0, 0, 1, -1, 2, -2]
+            assert b.tolist() == [14]
+            want = []
+            for q in range(W):
+                want += [10 * q + r] * (q + 1)
+            assert recv.tolist() == want
+
+
+def test_mesh_replay_refreshes_sends_that_depend_on_receives():
+    """A send whose bytes come from an earlier receive (a halo received,
+    then forwarded) is right after a second replay pass: replayed sends
+    overwrite what the record pass kept."""
+    from cubed_amd.runtime.comm import LoopbackMesh
+
+    mesh = LoopbackMesh(2)
+    comms = [LoopbackComm(r, 2, mesh=mesh) for r in range(2)]
+    own = [torch.tensor([5], dtype=torch.uint8), torch.tensor([9], dtype=torch.uint8)]
+    got = {}
+
+    def step(r):
+        c = comms[r]
+        halo = torch.zeros(1, dtype=torch.uint8)
+        c.exchange([(own[r], 1 - r)], [(halo, 1 - r)])
+        fwd = own[r] + halo  # depends on the receive
+        out = torch.zeros(1, dtype=torch.uint8)
+        c.exchange([(fwd, 1 - r)], [(out, 1 - r)])
+        got[r] = out.item()
+
+    for r in range(2):
+        step(r)
+    mesh.phase = "replay"
+    for _ in range(2):
+        for r in range(2):
+            step(r)
+    assert got == {0: 14, 1: 14}
