@@ -60,7 +60,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MFMA_PEAK_TFS = {"f32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
 EXTRAS = ("rechunk", "rechunk_rehearsal", "rechunk_mean", "rechunk_mean_share", "rechunk_mean_rehearsal",
-          "config1", "vorticity", "var", "matmul_f32", "matmul_bf16")
+          "config1", "vorticity", "var", "matmul_f32", "matmul_bf16", "matmul_rehearsal")
 # RCCL all-reduce of the rehearsed ranks' group partials (50000 f64 totals =
 # 400 KB, + 50 int64 counts) over 8 GPUs: NOT measured here (one GPU per box);
 # an allowance added to the rehearsed per-rank step for the 8-GPU prediction
@@ -1160,6 +1160,106 @@ def matmul_extra(args, ex, rank, world, dt_name):
     return r
 
 
+def matmul_rehearsal_extra(args, dt_name, t1_ms=None):
+    """Config 5 on N GPUs, every rank rehearsed on this one GPU through ONE
+    LoopbackMesh (dist.DistGemmLaunch): each rank allocates its block-cyclic
+    share of A and B (40000^2 in 5000^2 chunks: rank r owns A's k chunk
+    column r, B's and C's chunk column r), receives the halo columns of the
+    next k chunk, packs its k blocks into the k-major A image, sends them to
+    every peer (the mesh writes each receive from the peer's recorded send),
+    packs its B^T and runs the packed GEMM over its C columns.  After a
+    record pass and two replay passes every rank holds its true C columns:
+    64 sampled entries of C are checked against f64 dot products of the
+    resident operands (the matmul bound).  Per rank: HIP-event time of each
+    phase, bytes in / out.  Predicted N-GPU step (busiest rank) = halo +
+    pack A + max(transfers at a STATED link rate -- XGMI_LINK_GBS per
+    direction on each peer pair's own link, not measured --, pack B) + GEMM;
+    the mesh's slot writes stand in for RCCL's receive-side writes and are
+    reported, not charged."""
+    import torch
+
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.comm import LoopbackComm, LoopbackMesh
+    from cubed_amd.runtime.executors.dist import DistGemmLaunch
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    W = args.rehearse_world
+    n, c = args.matmul_n, 5000
+    xdt = xp.bfloat16 if dt_name == "bf16" else xp.float32
+    mesh = LoopbackMesh(W)
+    ranks = []
+    for r in range(W):
+        ex = GpuDagExecutor(comm=LoopbackComm(r, W, mesh=mesh))
+        spec = cubed.Spec(allowed_mem="288GB", executor=ex)
+        random.seed(4000)
+        A = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xdt)
+        B = xp.astype(crandom.random((n, n), chunks=(c, c), spec=spec), xdt)
+        arrays_to_plan(A, B).execute(executor=ex, array_names=[A.name, B.name])
+        m = xp.matmul(A, B)
+        step = step_fn(arrays_to_plan(m), ex, [m], (A, B))
+        step()  # record pass
+        ranks.append((ex, A, B, m, step))
+    sync()
+    mesh.phase = "replay"
+    for _ in range(2):  # halos, then the blocks packed from them, reach every rank
+        for ex, A, B, m, step in ranks:
+            step()
+        sync()
+    out = {"world": W, "dtype": dt_name, "n": n, "chunk": c, "xgmi_link_gbs_assumed": XGMI_LINK_GBS, "ranks": {}}
+    for r, (ex, A, B, m, step) in enumerate(ranks):
+        dt, summ = timed_launches(ex, step, 2, 1)
+        dg = [l for v in ex._cache.values() for l in v[1] if isinstance(l, DistGemmLaunch)]
+        if len(dg) != 1:
+            raise RuntimeError(f"rank {r}: {len(dg)} DistGemmLaunch")
+        d = dg[0]
+        ph = {k[2]: round(cnt * ms / 2, 4) for k, (cnt, ms) in summ.items() if k[0] == "matmul"}
+        xfer = d.predicted_xfer_ms(XGMI_LINK_GBS)
+        pred = ph.get("halo", 0) + ph.get("pack_a", 0) + max(xfer, ph.get("pack_b", 0)) + ph.get("gemm", 0)
+        gtf = d.flops / (ph["gemm"] * 1e-3) / 1e12 if ph.get("gemm") else None
+        out["ranks"][r] = dict(ms=round(dt * 1e3, 4), phases_ms=ph, bytes_out=d.bytes_out, bytes_in=d.bytes_in,
+                               halo_cols=[d.halo_w[q] for q in d.owned], xgmi_ms_assumed=round(xfer, 4),
+                               gemm_tflops=round(gtf, 1) if gtf else None,
+                               predicted_ms=round(pred, 4))
+    busiest = max(v["predicted_ms"] for v in out["ranks"].values())
+    out["predicted_step_ms"] = busiest
+    out["predicted"] = ("busiest rank: halo + pack A + max(xGMI transfers at the assumed link rate, pack B) + "
+                        "GEMM; the mesh's slot writes are not charged")
+    if t1_ms:
+        out["one_gpu_step_ms"] = t1_ms
+        out["predicted_speedup"] = round(t1_ms / busiest, 2)
+    # 64 sampled entries of the rehearsed C against f64 products of the
+    # operands, each chunk read from the rank that owns it
+    rng = np.random.default_rng(5)
+    rows = np.sort(rng.choice(n, 8, replace=False))
+    cols = np.sort(rng.choice(n, 8, replace=False))
+    nk = -(-n // c)
+
+    def chunk(i_arr, coords):
+        return device_chunk(ranks[ranks[0][i_arr].zarray.chunk_offset(coords) % W][i_arr].zarray, coords)
+
+    Ar = np.stack([np.concatenate([chunk(1, (i // c, q))[i % c].double().cpu().numpy() for q in range(nk)])
+                   for i in rows])
+    Bc = np.stack([np.concatenate([chunk(2, (q, j // c))[:, j % c].double().cpu().numpy() for q in range(nk)])
+                   for j in cols], axis=1)
+    got = np.array([[chunk(3, (i // c, j // c))[i % c, j % c].double().item() for j in cols] for i in rows])
+    exp = Ar @ Bc
+    bound = 8.0 * np.sqrt(n) * 2.0 ** -24 * (np.abs(Ar) @ np.abs(Bc))
+    if dt_name == "bf16":
+        bound = bound + 2.0 ** -8 * np.abs(exp)
+    err = np.abs(got - exp)
+    out["check"] = {"kind": "bound", "pass": bool(np.all(err <= bound)), "entries": int(got.size),
+                    "max_err_over_bound": float(np.max(err / bound)),
+                    "what": f"64 sampled entries of C assembled from {W} rehearsed ranks vs f64 products"}
+    CHECKS.append((f"matmul_rehearsal_{dt_name}", out["check"]))
+    del ranks
+    torch.cuda.synchronize()
+    free_gpu()
+    return out
+
+
 def matmul_check(A, B, C, n, c, bf16):
     """64 output entries (8 rows x 8 columns, seeded) against f64 dot products
     of the copied-back operand rows / columns.  Bound (tests/test_gpu_matmul.py):
@@ -1352,6 +1452,12 @@ def main(argv=None):
                 extra[name] = var_extra(args, ex, rank, world)
             elif name == "vorticity":
                 extra[name] = vorticity_extra(args, ex, rank, world)
+            elif name == "matmul_rehearsal":
+                if world == 1:
+                    extra[name] = {}
+                    for dn in ("bf16", "f32"):
+                        t1 = extra.get(f"matmul_{dn}", {}).get("ms")
+                        extra[name][dn] = matmul_rehearsal_extra(args, dn, t1)
             elif name.startswith("matmul"):
                 extra[name] = matmul_extra(args, ex, rank, world, name.split("_")[1])
         except Exception as e:  # pragma: no cover - reported, then fails the run

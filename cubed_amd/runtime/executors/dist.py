@@ -777,4 +777,23 @@ def dist_gemm_plan(ex, chain, F):
     kw = [A.chunk_extent((0, q))[1] for q in range(nk)]
     if min(kw) < T or any(w % (16 // A.dtype.itemsize) for w in kw):
         return None
+    # the packed kernels' own geometry rules (tile vs chunk widths, row
+    # alignment), asked of the native check on the rank's C grid with zero
+    # addresses: the same answer on every rank
+    cols = [j for j in range(nj) if j % W == ex.rank]
+    K = sum(kw)
+    tasks = np.zeros(ti * len(cols), dtype=nat.CHAIN_DTYPE)
+    segs = np.zeros(ti * len(cols) * nk, dtype=nat.SEG_DTYPE)
+    for i in range(ti):
+        for jl, j in enumerate(cols):
+            t = i * len(cols) + jl
+            key = (i, j) if F.ndim == 2 else (i, 0, j)
+            m, n = F.chunk_extent(key)[0], F.chunk_extent(key)[-1]
+            for q in range(nk):
+                segs[t * nk + q] = (0, 0, kw[q], kw[q], n, 0)
+            tasks[t] = (0, m, n, n, t * nk, nk, K, 0)
+    code = ir.dtype_code(A.dtype)
+    if nat.lib().cubed_gemm_dist_b_bytes(tasks.ctypes.data, ti, len(cols), segs.ctypes.data, len(segs), code,
+                                         ir.dtype_code(F.dtype)) < 0:
+        return None
     return A, B, ti, nk, nj
