@@ -210,7 +210,7 @@ class ScatterCombine:
     needs only their sums).
 
     The SoA partials ([field][group][kept], group = output block) are
-    scattered by one ``index_copy_`` into owner-major order, [rank][field]
+    scattered by one box copy (cubed_copy_boxes) into owner-major order, [rank][field]
     [slot][kept] with ``L`` slots per rank (the most blocks any rank owns;
     unused slots stay zero), and ``reduce_scatter`` leaves each rank the
     summed [field][slot][kept] of its own blocks -- straight in the finish's
@@ -223,7 +223,7 @@ class ScatterCombine:
     values are known on the host (geometry: the same on every rank) and the
     summed fields are one contiguous run of one accumulator dtype."""
 
-    def __init__(self, ctx, fused, rows, group_owner, nf, mko, f0, f1, acc_int, host_counts, discard):
+    def __init__(self, ctx, fused, rows, group_owner, nf, mko, f0, f1, acc_int, host_counts, discard, src):
         import dataclasses
 
         import torch
@@ -238,9 +238,14 @@ class ScatterCombine:
         self.G, self.L, self.mko, self.nf, self.f0, self.f1 = G, L, mko, nf, f0, f1
         self.mine = per[rank]
         dt = torch.int64 if acc_int else torch.float64
-        self.dst = torch.tensor([(group_owner[g] * nfr + fr) * L + pos[g] for fr in range(nfr) for g in range(G)],
-                                dtype=torch.int64, device=ctx.device)
+        dst = [(group_owner[g] * nfr + fr) * L + pos[g] for fr in range(nfr) for g in range(G)]
+        self.dst = torch.tensor(dst, dtype=torch.int64, device=ctx.device)  # (unpermute: tests)
         self.perm = torch.zeros(W * nfr * L * mko, dtype=dt, device=ctx.device)
+        # the owner-major scatter: one row of mko 8-B words per (field, group),
+        # one cubed_copy_boxes launch (src: the [field][group][kept] partials)
+        pb, rb = self.perm.data_ptr(), mko * 8
+        self.permute = CopyLaunch([Box(src + ((f0 + fr) * G + g) * rb, pb + dst[fr * G + g] * rb, [mko], [1], [1])
+                                   for fr in range(nfr) for g in range(G)], 8, ctx.device)
         self.fin = torch.zeros(max(nf * L * mko, 2), dtype=torch.int64, device=ctx.device).view(torch.uint8)
         self.fin_red = self.fin[f0 * L * mko * 8:f1 * L * mko * 8].view(dt)
         for f, counts in (host_counts or {}).items():
@@ -267,19 +272,54 @@ class ScatterCombine:
             return None
         return red[0], red[-1] + 1
 
-    def run(self, soa_bytes, stream):
-        """``soa_bytes``: the [field][group][kept] partials (8-B words)."""
-        G, mko = self.G, self.mko
-        src = soa_bytes[self.f0 * G * mko * 8:self.f1 * G * mko * 8].view(self.perm.dtype).view(-1, mko)
-        self.perm.view(-1, mko).index_copy_(0, self.dst, src)
+    def run(self, stream):
+        """The partials at ``src`` ([field][group][kept], 8-B words) to every
+        rank's owned blocks, then the finish."""
+        self.permute.run(stream)
         self.ctx.comm.reduce_scatter_sum(self.fin_red, self.perm)
         if self.finish_here:
-            fused_finish(self.fused, self.table, self.L, mko, self.fin, stream)
+            fused_finish(self.fused, self.table, self.L, self.mko, self.fin, stream)
 
     def unpermute(self, perm_sum):
         """[field][group][kept] from an owner-major buffer (tests: the sum of
         every rank's recorded reduce-scatter input)."""
         return perm_sum.view(-1, self.mko)[self.dst].view(self.f1 - self.f0, self.G, self.mko)
+
+
+
+class BlockCount:
+    """A plain COUNT field (mean's n) holds one value per output block --
+    every kept element of a block counts the same rows -- so only that value
+    crosses the ranks (8 B per block instead of 8 B per element).  Two
+    cubed_copy_boxes launches: the first word of every block into a compact
+    vector before the collective, and that vector back over the block's
+    words after it."""
+
+    def __init__(self, view, mk, device):
+        import torch
+
+        self.nblk = view.numel() // mk
+        self.view = view
+        self.compact = torch.empty(self.nblk, dtype=view.dtype, device=device)
+        src, dst = view.data_ptr(), self.compact.data_ptr()
+        self.gather = CopyLaunch([Box(src, dst, [self.nblk], [mk], [1])], 8, device)
+        self.spread = CopyLaunch([Box(dst, src, [self.nblk, mk], [1, 0], [mk, 1])], 8, device)
+
+
+def _sum_fields(ctx, fields, root, stream):
+    """The SUM combine of a sum-only reduction's partial fields: (view,
+    BlockCount or None) per field, reduced to ``root`` (or all-reduced)."""
+    comm = ctx.comm
+    for v, bc in fields:
+        if bc is not None:
+            bc.gather.run(stream)
+            v = bc.compact
+        if root is not None:
+            comm.reduce_sum(v, root)
+        else:
+            comm.all_reduce_sum(v)
+        if bc is not None and (root is None or ctx.rank == root):
+            bc.spread.run(stream)
 
 
 class PartialsLaunch:
@@ -324,8 +364,13 @@ class PartialsLaunch:
             self.scatter = ScatterCombine(
                 ctx, fused, fused.layout, group_owner, self.nf, fused.max_kept, fr[0], fr[1], acc_int[fr[0]],
                 {f: [int(host_count)] * len(group_owner) for f, r in enumerate(rops) if r == "count"},
-                discard)
+                discard, fused.ws.data_ptr())
             self.finish_here = self.scatter.finish_here
+        if self.sum_only and self.scatter is None:
+            mk = fused.max_kept
+            self.sum_views = [(self.field_view(f), BlockCount(self.field_view(f), mk, ctx.device)
+                               if self.uniform[f] and mk > 1 else None)
+                              for f in range(self.nf) if not self.host_count[f]]
         if not self.sum_only:
             self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8,
                                         device=ctx.device)
@@ -343,24 +388,10 @@ class PartialsLaunch:
         comm = self.ctx.comm
         L = nat.lib()
         if self.scatter is not None:
-            self.scatter.run(self.fused.ws, stream)
+            self.scatter.run(stream)
             return
         if self.sum_only:
-            mk = self.fused.max_kept
-            for f in range(self.nf):
-                if self.host_count[f]:
-                    continue
-                v = self.field_view(f)
-                per_block = self.uniform[f] and mk > 1
-                if per_block:
-                    blocks = v.view(-1, mk)
-                    v = blocks[:, 0].contiguous()
-                if self.root is not None:
-                    comm.reduce_sum(v, self.root)
-                else:
-                    comm.all_reduce_sum(v)
-                if per_block and (self.root is None or self.ctx.rank == self.root):
-                    blocks.copy_(v[:, None].expand_as(blocks))
+            _sum_fields(self.ctx, self.sum_views, self.root, stream)
         else:
             comm.all_gather(self.gathered, self.soa())
             if self.finish_here:
@@ -485,8 +516,14 @@ class DistPiecesLaunch:
         if fr is not None:
             self.scatter = ScatterCombine(
                 ctx, fused, group_layout, list(owners), self.nf, max_kept_out, fr[0], fr[1], acc_int[fr[0]],
-                {f: list(group_counts) for f, r in enumerate(rops) if r == "count"}, discard)
+                {f: list(group_counts) for f, r in enumerate(rops) if r == "count"}, discard,
+                self.gsoa.data_ptr())
             self.finish_here = self.scatter.finish_here
+        if self.sum_only and self.scatter is None:
+            mk = self.mko
+            self.sum_views = [(self.field_view(f), BlockCount(self.field_view(f), mk, ctx.device)
+                               if self.uniform[f] and mk > 1 else None)
+                              for f in range(self.nf) if not self.host_count[f]]
         if not self.sum_only:
             self.gathered = torch.empty(ctx.world * self.nf * self.n * 8, dtype=torch.uint8, device=ctx.device)
 
@@ -506,24 +543,10 @@ class DistPiecesLaunch:
                                              self.mko, self.gsoa.data_ptr(), stream), "cubed_combine_groups")
         comm = self.ctx.comm
         if self.scatter is not None:
-            self.scatter.run(self.gsoa, stream)
+            self.scatter.run(stream)
             return
         if self.sum_only:
-            mk = self.mko
-            for f in range(self.nf):
-                if self.host_count[f]:
-                    continue
-                v = self.field_view(f)
-                per_group = self.uniform[f] and mk > 1
-                if per_group:
-                    blocks = v.view(-1, mk)
-                    v = blocks[:, 0].contiguous()
-                if self.root is not None:
-                    comm.reduce_sum(v, self.root)
-                else:
-                    comm.all_reduce_sum(v)
-                if per_group and (self.root is None or self.ctx.rank == self.root):
-                    blocks.copy_(v[:, None].expand_as(blocks))
+            _sum_fields(self.ctx, self.sum_views, self.root, stream)
         else:
             comm.all_gather(self.gathered, self.gsoa[: self.nf * self.n * 8])
             if self.finish_here:

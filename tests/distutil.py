@@ -54,3 +54,20 @@ def run_ranks(fn, world, *args, backend="gloo", timeout=240):
             if p.is_alive():
                 p.kill()
     return [results[r] for r in range(world)]
+
+
+def host_copy(cl):
+    """Run a CopyLaunch's boxes on the HOST (CPU-tensor tests of launches
+    whose copies the library runs on the GPU): element by element, with the
+    canonical boxes' strides."""
+    import ctypes
+    import itertools
+
+    if cl.nboxes == 0:
+        return
+    isz = cl.itemsize
+    for b in cl.boxes:
+        for idx in itertools.product(*[range(e) for e in b.extent]):
+            so = sum(i * s for i, s in zip(idx, b.sstride)) * isz
+            do = sum(i * s for i, s in zip(idx, b.dstride)) * isz
+            ctypes.memmove(b.dst + do, b.src + so, isz)
