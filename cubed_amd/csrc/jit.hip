@@ -68,7 +68,14 @@ std::string jit_kernel_name(const cubed_program_t& P) {
     snprintf(buf, sizeof(buf), "cubed_reduce_%s_%s_v%d_r%d", kernel == 0 ? "a" : "b", vtag(P.vtype), vec, P.nred);
   std::string s = buf;
   if (P.mode & CUBED_MODE_PARTIALS) s += "_partials";
-  return s;
+  // + a digest of the program (FNV-1a over its bytes): every program's
+  // kernels carry their own symbol, so a kernel trace separates programs of
+  // the same shape (quad-means' mean and the var / std of u*v)
+  uint32_t h = 2166136261u;
+  const unsigned char* b = (const unsigned char*)&P;
+  for (size_t i = 0; i < sizeof(P); ++i) h = (h ^ b[i]) * 16777619u;
+  snprintf(buf, sizeof(buf), "_p%08x", h);
+  return s + buf;
 }
 
 // Partials mode: the SoA finish (cubed_fused_finish_compiled) -- the
