@@ -17,8 +17,13 @@ reductions whose inputs are single chunks at the task's own block (the
 per-chunk stage of ``reduction``, core/ops.py:838-847).  A program drawing
 from more than one random stream (the VM carries one Philox key per task)
 materialises all but one stream the same way: ``mean(u * v)`` of two
-unmaterialised ``random`` arrays (the reference's own quad_means test).  Anything else keeps
-raising LoweringError (there is no host path).
+unmaterialised ``random`` arrays (the reference's own quad_means test).  On
+several GPUs the temporaries are block-cyclic like every array: the task
+space's block grid is the temporary's, so each rank computes and reads only
+the chunks of the tasks it owns (inputs it lacks are fetched first, as for
+any pipeline), and the reduction rounds after a split per-chunk stage combine
+across ranks as usual.  Anything else keeps raising LoweringError (there is
+no host path).
 """
 
 from __future__ import annotations
@@ -182,8 +187,6 @@ def _space_geometry(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys)
 def split_launches(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys):
     """Launches computing ``program`` over ``keys`` as several fused
     programs through HBM temporaries (see the module docstring)."""
-    if ex.world > 1:
-        raise LoweringError(f"{program.name}: splitting an oversized chunk program is single-GPU only")
     parts, rest = split_program(program)
     shape, chunks, coords = _space_geometry(ex, program, cfg, target, keys)
     launches = []
@@ -195,6 +198,13 @@ def split_launches(ex, program: ir.ExprProgram, cfg, target: DeviceArray, keys):
         T = DeviceArray(shape, dt, chunks, name=name)
         ex.own(T)  # fits next to the plan? then it lives as long as the cached launches
         ex.allocate(T)
+        # several GPUs: the temporary is block-cyclic like every array; the
+        # chunk a task writes must be one this rank holds (it is when the
+        # space's block grid is the task grid: the same C-order offsets)
+        for k in keys:
+            if T.owner(coords[tuple(k)]) != ex.rank:
+                raise LoweringError(f"{program.name}: split temporary chunk {coords[tuple(k)]} of task {k} "
+                                    f"lives on rank {T.owner(coords[tuple(k)])}")
         prev = list(temps)
 
         def bf_sub(out_key, _prev=prev, _inv={v: k for k, v in coords.items()}):

@@ -370,3 +370,27 @@ def test_matmul_off_the_regular_ownership_fetches_chunks(built):
     (FetchLaunch + the chained GEMM) runs instead."""
     dg, all_l = _matmul_dry(0, 3, xp.float32)
     assert not dg and "FetchLaunch" in [type(l).__name__ for l in all_l]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_oversized_program_splits_on_every_rank(built, world):
+    """A chunk function over five inputs is split into HBM temporaries on
+    several GPUs too: each temporary is block-cyclic like the task space, so
+    every rank computes and reads only the chunks of its own tasks; the
+    reduction over several chunks per output block then combines across
+    ranks as usual."""
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="2GB", executor=dry)
+        random.seed(21)
+        five = [crandom.random((60, 40), chunks=(10, 20), spec=spec) for _ in range(5)]
+        arrays_to_plan(*five).execute(executor=dry, array_names=[a.name for a in five])
+        dry.launched.clear()
+        y5 = cubed.map_blocks(lambda a, b, c, d, e: a * b + c * d - e, *five, dtype=np.float64)
+        m = xp.mean(y5, axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        kinds = [type(l).__name__ for l in dry.launched]
+        assert kinds.count("FusedLaunch") >= 2 and kinds[-1] in ("DistPiecesLaunch", "PartialsLaunch"), kinds
+        mine = [c for c in range(12) if c % world == rank]  # 6 x 2 chunk grid, block-cyclic
+        split = [l for l in dry.launched if isinstance(l, FusedLaunch)]
+        assert all(l.ntasks <= len(mine) for l in split)

@@ -143,6 +143,18 @@ def _cases(rank, world, zdir):
     out["par_forked"] = np.array([getattr(ex, "parallel_forks", 0) > forks])
     note("parallel")
 
+    # a chunk function over FIVE inputs (more than one fused program holds):
+    # split into HBM temporaries that follow the block-cyclic ownership, then
+    # reduced over several chunks per output block
+    random.seed(21)
+    five = [crandom.random((60, 40), chunks=(10, 20), spec=spec) for _ in range(5)]
+    arrays_to_plan(*five).execute(executor=ex, array_names=[a.name for a in five])
+    y5 = cubed.map_blocks(lambda a, b, c, d, e: a * b + c * d - e, *five, dtype=np.float64)
+    out["five_map"] = y5.compute(resume=True)
+    out["five_mean0"] = xp.mean(y5, axis=0).compute(resume=True)
+    out["five_sum"] = xp.sum(y5).compute(resume=True)
+    note("five")
+
     # Zarr sink written by every rank (its own chunks), read back as a source
     zpath = os.path.join(zdir, "w.zarr")
     cubed.to_zarr(zc * 3, zpath)
@@ -212,3 +224,9 @@ def test_distributed_executor_matches_oracle(world, tmp_path):
     assert np.array_equal(got["stack"], np.stack([a70, a70 * 2], axis=1))
     assert np.array_equal(got["reshape"], np.arange(24.0).reshape(4, 6))
     assert np.array_equal(got["zarr"], z * 3)
+
+    F = [R.random_array((60, 40), (10, 20), sd) for sd in _seeds(21, 5)]
+    y5 = F[0] * F[1] + F[2] * F[3] - F[4]
+    assert np.array_equal(got["five_map"], y5)  # one IEEE op per node, stored at f64: bit-exact
+    assert np.allclose(got["five_mean0"], y5.mean(axis=0), rtol=1e-12, atol=0)
+    assert np.isclose(got["five_sum"], y5.sum(), rtol=1e-12, atol=0)
