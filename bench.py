@@ -328,7 +328,9 @@ def free_gpu():
 
 
 # --------------------------------------------------------------------------- value checks
-# Full-size checks of every benchmarked output, at every world size.  The
+# Full-size checks of every benchmarked output, at every world size: every
+# output position of the reductions (the rechunk: 3 x 3 bands bit for bit,
+# the matmul: 64 entries against f64 dot products).  The
 # expected values are restated with torch f64 arithmetic over the SAME
 # resident inputs (independent of this repo's kernels): each rank reduces
 # the chunks it owns, one f64 all-reduce sums the ranks' shares (each output
@@ -439,32 +441,36 @@ def sample_columns(shape, k, seed):
     return np.stack(np.unravel_index(flat, shape), axis=1) if shape else np.zeros((1, 0), np.int64)
 
 
-def owned_column_sums(arrs, fn, cols, center=None):
-    """f64 sums over axis 0 of ``fn(*chunks)`` at the sampled trailing
-    multi-indices ``cols`` (k, ndim - 1), over the chunks of ``arrs`` (equal
-    chunking) this rank owns.  ``fn`` gets the chunks in their own dtype
-    (numpy's arithmetic: f32 * f32 stays f32) and its result is summed in f64
-    (statistical_functions.py:57, ``dtype=float64``).  ``center`` (k,): sum
-    the squared deviations from it instead (a two-pass variance)."""
+def owned_axis0_sums(arrs, fn, center=None):
+    """f64 sums over axis 0 of ``fn(*chunks)`` at EVERY output position, over
+    the chunks of ``arrs`` (equal chunking) this rank owns (0 elsewhere).
+    ``fn`` gets the chunks in their own dtype (numpy's arithmetic: f32 * f32
+    stays f32) and its result is summed in f64 (statistical_functions.py:57,
+    ``dtype=float64``).  ``center`` (the output's shape): sum the squared
+    deviations from it instead (a two-pass variance)."""
     import torch
 
     A = arrs[0]
-    acc = torch.zeros(len(cols), dtype=torch.float64, device=A.device)
+    acc = torch.zeros(A.shape[1:], dtype=torch.float64, device=A.device)
     for coords in owned_chunks(A):
-        st, ext = np.array(A.chunk_start(coords)[1:]), np.array(A.chunk_extent(coords)[1:])
-        inside = np.all((cols >= st) & (cols < st + ext), axis=1)
-        if not inside.any():
-            continue
-        sel = np.nonzero(inside)[0]
-        local = np.ravel_multi_index(tuple((cols[sel] - st).T), tuple(ext))
-        li = torch.as_tensor(local, device=A.device)
-        vals = [device_chunk(a, coords).reshape(A.chunk_extent(coords)[0], -1)[:, li] for a in arrs]
-        ts = torch.as_tensor(sel, device=A.device)
-        val = fn(*vals).double()
+        st, ext = A.chunk_start(coords)[1:], A.chunk_extent(coords)[1:]
+        sl = tuple(slice(a, a + e) for a, e in zip(st, ext))
+        val = fn(*[device_chunk(a, coords) for a in arrs]).double()
         if center is not None:
-            val = (val - center[ts]) ** 2
-        acc[ts] += val.sum(0)
+            val = (val - center[sl]) ** 2
+        acc[sl] += val.sum(0)
     return acc
+
+
+def owned_output_full(M):
+    """Every computed output of ``M`` this rank owns (f64, 0 elsewhere)."""
+    import torch
+
+    got = torch.zeros(M.shape, dtype=torch.float64, device=M.device)
+    for coords in owned_chunks(M):
+        st, ext = M.chunk_start(coords), M.chunk_extent(coords)
+        got[tuple(slice(a, a + e) for a, e in zip(st, ext))] = device_chunk(M, coords).double()
+    return got
 
 
 def owned_output_values(M, cols):
@@ -483,14 +489,16 @@ def owned_output_values(M, cols):
     return got
 
 
-def column_mean_check(inputs, out, fn, rtol, what, k=64, seed=11):
-    """mean over axis 0 of fn(*inputs), checked at k sampled output
-    positions on every world size (one f64 all-reduce)."""
+def column_mean_check(inputs, out, fn, rtol, what):
+    """mean over axis 0 of fn(*inputs), checked at EVERY output position on
+    every world size: each rank sums its own input chunks and fills its own
+    output chunks, one f64 all-reduce of the two output-sized vectors."""
     M = out.zarray
-    cols = sample_columns(M.shape, k, seed)
-    exp = owned_column_sums([a.zarray for a in inputs], fn, cols)
-    got = owned_output_values(M, cols)
-    return sampled_check(exp, got, inputs[0].shape[0], rtol, what)
+    exp = owned_axis0_sums([a.zarray for a in inputs], fn)
+    got = owned_output_full(M)
+    r = sampled_check(exp, got, inputs[0].shape[0], rtol, what)
+    r["kind"] = "full"
+    return r
 
 
 def full_host(arr):
@@ -701,7 +709,7 @@ def rechunk_mean_extra(args, ex, rank, world):
         elif mode.startswith("rechunk"):
             r["roofline"] = roofline_step(x.nbytes // world, dt)
         r["check"] = column_mean_check([x], m, lambda c: c, 1e-6,
-                                       "64 sampled column means vs f64 sums of the resident input")
+                                       "every column mean vs f64 sums of the resident input")
         CHECKS.append((f"rechunk_mean {mode}", r["check"]))
         out["elided" if mode.startswith("rechunk") else "materialised"] = r
         del m, plan
@@ -739,7 +747,7 @@ def rechunk_mean_share_extra(args, ex, rank, world):
                  value=round(x.nbytes / dt / 1e9, 1), ms=round(dt * 1e3, 4),
                  launches_ms=fmt_launches(summ), **overhead(dt, summ, 20))
         r["check"] = column_mean_check([x], m, lambda c: c, 1e-6,
-                                       "64 sampled column means vs f64 sums of the resident input")
+                                       "every column mean vs f64 sums of the resident input")
         CHECKS.append((f"rechunk_mean_share {rows}", r["check"]))
         out[f"rows_{rows}"] = r
         del x, m, plan
@@ -944,25 +952,24 @@ def var_extra(args, ex, rank, world):
     return out
 
 
-def column_var_check(u, v, m, sqrt, k=64, seed=13):
-    """Two-pass f64 var over axis 0 of u*v (f32 products) at k sampled
-    columns: every rank sums its chunks, one all-reduce for the sums, one
+def column_var_check(u, v, m, sqrt):
+    """Two-pass f64 var over axis 0 of u*v (f32 products) at every output
+    position: every rank sums its chunks, one all-reduce for the sums, one
     for the squared deviations from the mean; rtol 1e-6 (f32 output)."""
     import torch
 
     M = m.zarray
-    cols = sample_columns(M.shape, k, seed)
     U, V = u.zarray, v.zarray
     n = u.shape[0]
-    s1 = allreduce_(owned_column_sums([U, V], lambda a, b: a * b, cols))
-    s2 = allreduce_(owned_column_sums([U, V], lambda a, b: a * b, cols, center=s1 / n))
+    s1 = allreduce_(owned_axis0_sums([U, V], lambda a, b: a * b))
+    s2 = allreduce_(owned_axis0_sums([U, V], lambda a, b: a * b, center=s1 / n))
     exp = s2 / n
     if sqrt:
         exp = torch.sqrt(exp)
-    got = allreduce_(owned_output_values(M, cols))
+    got = allreduce_(owned_output_full(M))
     r = check_close(got.cpu().numpy(), exp.cpu().numpy(), 1e-6,
-                    f"64 sampled {'std' if sqrt else 'var'} vs a two-pass f64 var of the resident inputs")
-    r.update(kind="sampled", entries=len(cols), world=world_size())
+                    f"every {'std' if sqrt else 'var'} output vs a two-pass f64 var of the resident inputs")
+    r.update(kind="full", entries=int(got.numel()), world=world_size())
     return r
 
 
@@ -993,14 +1000,14 @@ def config1_extra(args, ex, rank, world):
     else:
         r["roofline"] = roofline_step(a.nbytes // world, dt)
     r["check"] = column_mean_check([a], m, lambda c: (c + 1) * 2, 1e-12,
-                                   "64 sampled column means vs f64 sums of (a+1)*2 over the resident input")
+                                   "every column mean vs f64 sums of (a+1)*2 over the resident input")
     CHECKS.append(("config1", r["check"]))
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
         r["cpu_baseline"] = cpu_config1_baseline(a)
     return r
 
 
-def cpu_config1_baseline(a, row_blocks=2):
+def cpu_config1_baseline(a, row_blocks=None):
     """BASELINE config 1 as the reference runs it: the sequential
     PythonDagExecutor over the finalized plan (add; multiply + _mean_func;
     merge + combine + aggregate) with every intermediate in a LOCAL ZARR
@@ -1008,7 +1015,8 @@ def cpu_config1_baseline(a, row_blocks=2):
     numcodecs' default compressor).  ``a`` (the random op's output) is first
     written to the work_dir from HBM (untimed, as its generation is untimed
     on the GPU); the timed sample is the first ``row_blocks`` row bands of
-    chunks (all four column chunks), bounded to ~10-30 s."""
+    chunks (all four column chunks; default: every band), median of CPU_REPS runs after a
+    warm-up."""
     import shutil
     import tempfile
 
@@ -1016,13 +1024,12 @@ def cpu_config1_baseline(a, row_blocks=2):
     from cubed_amd.zarr_io import ZarrV2Array, write_device_array
 
     A = a.zarray
+    row_blocks = A.numblocks[0] if row_blocks is None else row_blocks
     work = tempfile.mkdtemp(prefix="cubed_cpu_work_")
     try:
         src = ZarrV2Array.create(os.path.join(work, "a"), A.shape, A.dtype, A.chunks)
         write_device_array(A, src)
-        t0 = time.perf_counter()
-        got = R.config1_python_zarr(src, work, row_blocks=row_blocks)
-        dt = time.perf_counter() - t0
+        dt, runs, got = median_run(lambda: R.config1_python_zarr(src, work, row_blocks=row_blocks))
         # the sample's mean over its rows, checked against the resident input
         rows = row_blocks * A.chunks[0]
         import itertools
@@ -1043,8 +1050,8 @@ def cpu_config1_baseline(a, row_blocks=2):
                       f"_mean_func; merge + combine + aggregate), every intermediate written to and read "
                       f"from a local Zarr v2 work_dir (blosc-lz4 + byte shuffle, this repo's host codec, "
                       f"{{n, total}} partials as two arrays); input a already in the work_dir (untimed); "
-                      f"one timed pass; {_cpu_info(1)}",
-            "seconds": round(dt, 3), "values_match": ok}
+                      f"median of {CPU_REPS} timed passes after a warm-up; {_cpu_info(1)}",
+            "seconds": round(dt, 3), "runs_s": runs, "values_match": ok}
 
 
 def vorticity_extra(args, ex, rank, world, T=1000):
@@ -1136,22 +1143,22 @@ def cpu_vorticity_baseline(A, B, X, Y, t_blocks=2):
     a, b = host(A, nrows), host(B, nrows)
     x, y = X.to_numpy(), Y.to_numpy()
     threads = min(32, (os.cpu_count() or 1) + 4)
-    res = {}
+    res, runs = {}, {}
     with threadpool_limits(1):
         for name, th in (("sequential", 1), ("threads", threads)):
-            R.vorticity_python(a, b, x, y, c, t_blocks=1, threads=th)  # warm-up
-            t0 = time.perf_counter()
-            got = R.vorticity_python(a, b, x, y, c, t_blocks=t_blocks, threads=th)
-            res[name] = time.perf_counter() - t0
+            res[name], runs[name], got = median_run(
+                lambda: R.vorticity_python(a, b, x, y, c, t_blocks=t_blocks, threads=th))
     exp = float(np.mean(a[1:1 + t_blocks * c] * x + b[1:1 + t_blocks * c] * y, dtype=np.float64))
     nbytes = 2 * t_blocks * c * x.size * 8 + 2 * x.size * 8
     return {"value": round(nbytes / res["threads"] / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"{t_blocks} of {-(-(A.shape[0] - 1) // c)} time blocks of a[1:], b[1:] "
                       f"({t_blocks * 72} chunk tasks per op): oracle restatement of the reference's finalized "
                       f"plan (index a[1:], b[1:]; * x, * y; add + _mean_func; combine + aggregate) on the "
-                      f"threaded executor, in-memory intermediates (no Zarr/Blosc: optimistic), one timed "
-                      f"pass after a warm-up; {_cpu_info(threads)}",
-            "sequential": {"value": round(nbytes / res["sequential"] / 1e9, 3), "cores": 1},
+                      f"threaded executor, in-memory intermediates (no Zarr/Blosc: optimistic), median "
+                      f"of {CPU_REPS} timed passes after a warm-up; {_cpu_info(threads)}",
+            "runs_s": runs["threads"],
+            "sequential": {"value": round(nbytes / res["sequential"] / 1e9, 3), "cores": 1,
+                           "runs_s": runs["sequential"]},
             "values_match": bool(abs(got - exp) <= 1e-12 * abs(exp))}
 
 
@@ -1338,6 +1345,22 @@ def matmul_check(A, B, C, n, c, bf16):
 # --------------------------------------------------------------------------- CPU baselines
 
 
+CPU_REPS = 5  # BASELINE.md's protocol: median of >= 5 timed runs after a warm-up
+
+
+def median_run(fn, reps=CPU_REPS, warmup=True):
+    """(median seconds, every run's seconds, the last result) of ``fn()``
+    over ``reps`` timed runs after one untimed warm-up run."""
+    if warmup:
+        fn()
+    ts, out = [], None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), [round(t, 4) for t in ts], out
+
+
 def _cpu_info(threads):
     return (f"numpy {np.__version__}, host cpus {os.cpu_count()}, affinity "
             f"{len(os.sched_getaffinity(0))}, worker threads {threads}, BLAS threads 1")
@@ -1357,25 +1380,22 @@ def cpu_baseline(res, ex):
     threads = min(32, (os.cpu_count() or 1) + 4)
     out = {}
     with threadpool_limits(1):
-        for name, th, reps in (("sequential", 1, 2), ("threads", threads, 3)):
-            R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=th)  # warm-up
-            ts = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                exp = R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=th)
-                ts.append(time.perf_counter() - t0)
-            out[name] = (float(np.median(ts)), th)
+        for name, th in (("sequential", 1), ("threads", threads)):
+            med, runs, exp = median_run(lambda: R.quad_means_cpu(u, v, 10, 2_000_000_000, 100_000_000, threads=th))
+            out[name] = (med, th, runs)
     got = res["m"].compute()
     parity = bool(np.allclose(got, exp, rtol=1e-6, atol=0))
     nbytes = u.nbytes + v.nbytes
-    dt, th = out["threads"]
+    dt, th, runs = out["threads"]
     return {"value": round(nbytes / dt / 1e9, 3), "unit": "GB/s", "cores": th, "kind": "port",
             "sample": f"full config 2: quad-means ({u.shape[0]},720,1440) f32 u,v, chunks (10,720,1440), "
                       f"oracle restatement of the reference threads executor (AsyncPythonDagExecutor "
-                      f"ThreadPoolExecutor), median of 3 after a warm-up; {_cpu_info(th)}; excludes "
+                      f"ThreadPoolExecutor), median of {CPU_REPS} after a warm-up; {_cpu_info(th)}; excludes "
                       f"Zarr/Blosc I/O (optimistic)",
+            "runs_s": runs,
             "sequential": {"value": round(nbytes / out["sequential"][0] / 1e9, 3), "cores": 1,
-                           "sample": "same inputs, PythonDagExecutor restatement, median of 2"},
+                           "sample": f"same inputs, PythonDagExecutor restatement, median of {CPU_REPS} after a "
+                                     f"warm-up", "runs_s": out["sequential"][2]},
             "gpu_matches_oracle_full_size": parity}
 
 
@@ -1407,23 +1427,20 @@ def cpu_rechunk_baseline(x, ex):
 
     I = np.empty_like(X)
     Y = np.empty_like(X)
-    out = {}
+    out, runs = {}, {}
     for name, th in (("sequential", 1), ("threads", threads)):
         pool = ThreadPoolExecutor(th) if th > 1 else None
-        copy_op(X, I, inter, pool)  # warm-up (page faults of I, Y)
-        copy_op(I, Y, write, pool)
-        t0 = time.perf_counter()
-        copy_op(X, I, inter, pool)
-        copy_op(I, Y, write, pool)
-        out[name] = time.perf_counter() - t0
+        out[name], runs[name], _ = median_run(lambda: (copy_op(X, I, inter, pool), copy_op(I, Y, write, pool)))
         if pool:
             pool.shutdown()
     ok = bool(np.array_equal(Y.view(np.uint32), X.view(np.uint32)))
     return {"value": round(X.nbytes / out["threads"] / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"full config 3: 50000^2 f32, reference 2 GB plan read {read} -> int {inter} -> "
-                      f"write {write}, in-memory numpy region copies (no Zarr/Blosc: optimistic), one "
-                      f"timed pass after a warm-up; {_cpu_info(threads)}",
-            "sequential": {"value": round(X.nbytes / out["sequential"] / 1e9, 3), "cores": 1},
+                      f"write {write}, in-memory numpy region copies (no Zarr/Blosc: optimistic), median "
+                      f"of {CPU_REPS} timed passes after a warm-up; {_cpu_info(threads)}",
+            "runs_s": runs["threads"],
+            "sequential": {"value": round(X.nbytes / out["sequential"] / 1e9, 3), "cores": 1,
+                           "runs_s": runs["sequential"]},
             "values_unchanged": ok}
 
 
@@ -1455,9 +1472,9 @@ def main(argv=None):
     algo = in_bytes // world
     symbols = res["symbols"]
     extra = {"launches_ms": fmt_launches(res["summ"]), **overhead(dt, res["summ"], args.steps)}
-    # every world size: 64 sampled outputs vs f64 sums of u*v over every rank's chunks
+    # every world size: every output vs f64 sums of u*v over every rank's chunks
     extra["check"] = column_mean_check([res["u"], res["v"]], res["m"], lambda a, b: a * b, 1e-6,
-                                       "64 sampled means vs f64 sums of u*v (f32 products) over the resident inputs")
+                                       "every mean vs f64 sums of u*v (f32 products) over the resident inputs")
     CHECKS.append(("quad-means sampled", extra["check"]))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
