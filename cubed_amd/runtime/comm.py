@@ -141,8 +141,7 @@ class Comm:
             t = torch.tensor([1 if ok else 0], dtype=torch.int32)
             self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.ctrl)
             return bool(t.item())
-        dev = "cpu" if self.staged else "cuda"
-        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=collective_device(self.dist, self.group))
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
         return bool(t.item())
 
@@ -153,6 +152,23 @@ class Comm:
 
 
 _CTRL: dict = {}
+
+
+def collective_device(dist, group=None):
+    """The device a device-group collective of this process runs on: CPU
+    for gloo, else the GPU the process group was bound to at init
+    (``init_process_group(device_id=...)``), else the current device -- never
+    a bare "cuda" that would put every rank of a launcher that skipped
+    ``torch.cuda.set_device`` on GPU 0."""
+    import torch
+
+    if str(dist.get_backend(group)).lower() == "gloo":
+        return torch.device("cpu")
+    pg = group if group is not None else dist.group.WORLD
+    bound = getattr(pg, "bound_device_id", None)
+    if bound is not None:
+        return bound
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def control_group(dist):
@@ -172,8 +188,7 @@ def control_group(dist):
         ctrl = dist.new_group(backend="gloo")
     except Exception:  # noqa: BLE001 -- agreed below
         ctrl = None
-    dev = "cuda" if str(dist.get_backend()).lower() != "gloo" else "cpu"
-    t = torch.tensor([0 if ctrl is None else 1], dtype=torch.int32, device=dev)
+    t = torch.tensor([0 if ctrl is None else 1], dtype=torch.int32, device=collective_device(dist))
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     if not int(t.item()):
         ctrl = None

@@ -880,12 +880,16 @@ class GpuDagExecutor(DagExecutor):
         return out
 
     def _gemm_workspace(self, nbytes):
-        """HBM workspace of the packed bf16 GEMM (both operands rewritten
-        once), or None when it would not fit beside the plan's arrays -- the
-        chain set then runs on the per-chunk kernel, which needs none."""
+        """HBM workspace of the packed GEMMs (both operands rewritten once),
+        or None when it would not fit beside the plan's arrays -- the chain
+        set then runs on the per-chunk kernel, which needs none -- or when
+        lowering only for geometry (no address exists).  Each packed launch
+        owns its workspace for the life of its cached plan: a repeated step
+        allocates nothing, and launches that run concurrently
+        (compute_arrays_in_parallel) never share one."""
         if self.check_memory and self._resident_bytes + self.owned_bytes() + nbytes > HBM_BYTES_PER_GPU:
             return None
-        return self.scratch(nbytes)
+        return self.scratch(nbytes) or None
 
     def _compiled_chain_dist(self, chain, target, keys):
         """A reduction chain over chunks spread across the ranks: each rank

@@ -7,6 +7,14 @@ Parity is UNPINNED against the reference: cubed v0.12.0 has no var / std
 (api_status.md:72,74); the semantics are numpy's, computed in f64 as the
 reference computes mean (statistical_functions.py:28-100 is the pattern).
 Tolerances: rtol 1e-12 for f64 results, 1e-6 for f32 results.
+
+Rounding note (round 5): in the vectorised streaming kernel the Welford
+update of a 4-element group multiplies by one shared 1/n (vm.h
+``var_add_inv``) instead of dividing every element by n -- the group's
+elements fold the same rows, so n is common -- which moves var / std by a
+few ulp against the per-element division (the scalar path and earlier
+builds).  The tolerances above cover it; no test compares var bit for bit
+across builds.
 """
 
 import random
