@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 profile session (as round 4) on a 1-GPU MI355X box: kernel-trace stats of the
+# Round-6 profile session (as rounds 4-5) on a 1-GPU MI355X box: kernel-trace stats of the
 # whole bench, then FETCH_SIZE / WRITE_SIZE passes (separate runs, kernel
 # trace only) whose per-dispatch CSVs come back under gpurun_out/ and are
 # folded per kernel by tools/traffic.py on the host, then the default bench
@@ -24,11 +24,11 @@ cd "$R"
 # keep the kernel stats; the per-dispatch traces stay on the box
 python3 tools/traffic.py --compact gpurun_out/pmc_fetch FETCH_SIZE > gpurun_out/pmc_fetch.json &&
 python3 tools/traffic.py --compact gpurun_out/pmc_write WRITE_SIZE > gpurun_out/pmc_write.json || { echo fold failed; exit 1; }
-cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/r05_kernel_stats.csv
+cp gpurun_out/prof/run_kernel_stats.csv gpurun_out/r06_kernel_stats.csv
 python3 - <<'PY'
 import csv
 rows = list(csv.DictReader(open("gpurun_out/prof/run_kernel_trace.csv")))
-with open("gpurun_out/r05_kernel_sequence.txt", "w") as f:
+with open("gpurun_out/r06_kernel_sequence.txt", "w") as f:
     for r in rows:
         n = r["Kernel_Name"][:100]
         f.write(f"{(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:10.2f} {r.get('Grid_Size', r.get('Grid_Size_X', ''))} {n}\n")
