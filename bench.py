@@ -1029,7 +1029,13 @@ def cpu_config1_baseline(a, row_blocks=None):
     try:
         src = ZarrV2Array.create(os.path.join(work, "a"), A.shape, A.dtype, A.chunks)
         write_device_array(A, src)
-        dt, runs, got = median_run(lambda: R.config1_python_zarr(src, work, row_blocks=row_blocks))
+        run_dir = os.path.join(work, "run")
+
+        def fresh():  # every run writes its intermediates into an empty work_dir
+            shutil.rmtree(run_dir, ignore_errors=True)
+            os.makedirs(run_dir)
+
+        dt, runs, got = median_run(lambda: R.config1_python_zarr(src, run_dir, row_blocks=row_blocks), setup=fresh)
         # the sample's mean over its rows, checked against the resident input
         rows = row_blocks * A.chunks[0]
         import itertools
@@ -1348,13 +1354,18 @@ def matmul_check(A, B, C, n, c, bf16):
 CPU_REPS = 5  # BASELINE.md's protocol: median of >= 5 timed runs after a warm-up
 
 
-def median_run(fn, reps=CPU_REPS, warmup=True):
+def median_run(fn, reps=CPU_REPS, warmup=True, setup=None):
     """(median seconds, every run's seconds, the last result) of ``fn()``
-    over ``reps`` timed runs after one untimed warm-up run."""
+    over ``reps`` timed runs after one untimed warm-up run; ``setup()`` runs
+    untimed before every run."""
     if warmup:
+        if setup:
+            setup()
         fn()
     ts, out = [], None
     for _ in range(reps):
+        if setup:
+            setup()
         t0 = time.perf_counter()
         out = fn()
         ts.append(time.perf_counter() - t0)
@@ -1470,7 +1481,7 @@ def main(argv=None):
     # algorithmic bytes of the dominant launch: the fused u*v -> mean kernel
     # reads this rank's u and v once (2 x 4.147e9 B at T=1000)
     algo = in_bytes // world
-    symbols = res["symbols"]
+    symbols = [x for x in res["symbols"] if not x.startswith("cubed_map_")]  # the reduction's kernel, not the inputs' astype
     extra = {"launches_ms": fmt_launches(res["summ"]), **overhead(dt, res["summ"], args.steps)}
     # every world size: every output vs f64 sums of u*v over every rank's chunks
     extra["check"] = column_mean_check([res["u"], res["v"]], res["m"], lambda a, b: a * b, 1e-6,
