@@ -513,6 +513,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_bf16_chain(const cubed_gemm_cha
 
 #include "gemm_bf16_w4l.h"
 #include "gemm_bf16_w4p.h"
+#include "gemm_bf16_8p.h"
 
 // ------------------------------------------------------------------ f32 MFMA
 // v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulate): lane l gives
@@ -1309,9 +1310,9 @@ extern "C" int cubed_gemm_dist_gemm(const cubed_gemm_chain_t* tasks, const cubed
   if (in_dtype == CUBED_F32)
     hipLaunchKernelGGL((k_gemm_f32_w4p<false>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
   else if (out_dtype == CUBED_BF16)
-    hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
+    hipLaunchKernelGGL((k_gemm_bf16_8p<true>), grid, dim3(512), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
   else
-    hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
+    hipLaunchKernelGGL((k_gemm_bf16_8p<false>), grid, dim3(512), 0, st, d_tasks, PA, PB, pp, gg, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }
   return 0;
@@ -1354,11 +1355,13 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
   } else {
     hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, st, d_tasks, d_segs, pp, PA);
     hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, st, d_tasks, d_segs, pp, PB);
+    // two waves per SIMD on the packed image (gemm_bf16_8p.h; round 6:
+    // 1410-1424 TF against the one-wave w4p kernel's 1301-1317, bit-identical)
     if (out_dtype == CUBED_BF16)
-      hipLaunchKernelGGL((k_gemm_bf16_w4p<true>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB,
+      hipLaunchKernelGGL((k_gemm_bf16_8p<true>), grid, dim3(512), 0, st, d_tasks, (const char*)PA, (const char*)PB,
                          pp, gg, nullptr);
     else
-      hipLaunchKernelGGL((k_gemm_bf16_w4p<false>), grid, dim3(256), 0, st, d_tasks, (const char*)PA, (const char*)PB,
+      hipLaunchKernelGGL((k_gemm_bf16_8p<false>), grid, dim3(512), 0, st, d_tasks, (const char*)PA, (const char*)PB,
                          pp, gg, nullptr);
   }
   hipError_t e = hipGetLastError();

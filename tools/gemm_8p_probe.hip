@@ -1,0 +1,158 @@
+// gemm_8p_probe.hip -- development probe (not part of the library): BASELINE
+// config 5's bf16 chained GEMM (40000^2 in 5000^2 chunks, f32 out) on the
+// library's packed operands, timed in ONE process on the one-wave kernel
+// (k_gemm_bf16_w4p) and the two-waves-per-SIMD kernel (k_gemm_bf16_8p,
+// csrc/gemm_bf16_8p.h), alternating; the outputs compared word for word.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude \
+//          -o tools/gemm_8p_probe tools/gemm_8p_probe.hip
+// Run:   tools/gemm_8p_probe [reps] [N] [out: 0 f32 / 1 bf16]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+namespace cubed {
+thread_local char g_err[512];
+}
+#include "../cubed_amd/csrc/gemm_chain.hip"
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void k_fill(uint16_t* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    const float v = (float)(h >> 8) * (1.0f / 16777216.0f);  // U[0, 1) as config 5
+    p[i] = (uint16_t)(__float_as_uint(v) >> 16);
+  }
+}
+
+__global__ void k_mismatch(const uint32_t* a, const uint32_t* b, int64_t n, unsigned long long* out) {
+  unsigned long long c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += a[i] != b[i];
+  atomicAdd(out, c);
+}
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 3;
+  const int64_t N = argc > 2 ? atoll(argv[2]) : 40000, Cc = 5000, nb = N / Cc;
+  const bool obf = argc > 3 && atoi(argv[3]) == 1;
+  const int64_t al = 32;  // the executor's slot alignment (storage.SLOT_ALIGN)
+  const int64_t slot_in = (Cc * Cc * 2 + al - 1) / al * al;
+  const int64_t slot_out = (Cc * Cc * (obf ? 2 : 4) + al - 1) / al * al;
+  char *A, *B, *C0, *C1;
+  CHECK(hipMalloc(&A, slot_in * nb * nb));
+  CHECK(hipMalloc(&B, slot_in * nb * nb));
+  CHECK(hipMalloc(&C0, slot_out * nb * nb));
+  CHECK(hipMalloc(&C1, slot_out * nb * nb));
+  k_fill<<<4096, 256>>>((uint16_t*)A, slot_in * nb * nb / 2, 12345u);
+  k_fill<<<4096, 256>>>((uint16_t*)B, slot_in * nb * nb / 2, 777u);
+  std::vector<cubed_gemm_chain_t> tasks(nb * nb);
+  std::vector<cubed_gemm_seg_t> segs(nb * nb * nb);
+  for (int64_t i = 0; i < nb; ++i)
+    for (int64_t j = 0; j < nb; ++j) {
+      const int64_t t = i * nb + j;
+      tasks[t] = {0, Cc, Cc, Cc, t * nb, nb, N, 0};
+      for (int64_t k = 0; k < nb; ++k)
+        segs[t * nb + k] = {(int64_t)(uintptr_t)(A + (i * nb + k) * slot_in),
+                            (int64_t)(uintptr_t)(B + (k * nb + j) * slot_in), Cc, Cc, Cc, 0};
+    }
+  cubed_gemm_chain_t *dt0, *dt1;
+  cubed_gemm_seg_t* ds;
+  CHECK(hipMalloc(&dt0, sizeof(cubed_gemm_chain_t) * tasks.size()));
+  CHECK(hipMalloc(&dt1, sizeof(cubed_gemm_chain_t) * tasks.size()));
+  CHECK(hipMalloc(&ds, sizeof(cubed_gemm_seg_t) * segs.size()));
+  for (auto& t : tasks) t.c = (int64_t)(uintptr_t)(C0 + (&t - &tasks[0]) * slot_out);
+  CHECK(hipMemcpy(dt0, tasks.data(), sizeof(cubed_gemm_chain_t) * tasks.size(), hipMemcpyHostToDevice));
+  for (auto& t : tasks) t.c = (int64_t)(uintptr_t)(C1 + (&t - &tasks[0]) * slot_out);
+  CHECK(hipMemcpy(dt1, tasks.data(), sizeof(cubed_gemm_chain_t) * tasks.size(), hipMemcpyHostToDevice));
+  CHECK(hipMemcpy(ds, segs.data(), sizeof(cubed_gemm_seg_t) * segs.size(), hipMemcpyHostToDevice));
+  const int32_t out_code = obf ? CUBED_BF16 : CUBED_F32;
+  const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, out_code);
+  if (wsb <= 0) { printf("pack_bytes: %s\n", g_err); return 1; }
+  char* ws;
+  CHECK(hipMalloc(&ws, wsb));
+  PackPlan pp;
+  GemmGrid gg;
+  if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, out_code, pp, gg)) return 1;
+  // the library entry: pack + w4p GEMM into C0 (the reference result)
+  if (cubed_gemm_chain_packed(tasks.data(), dt0, nb, nb, segs.data(), ds, segs.size(), CUBED_BF16, out_code, ws, wsb,
+                              nullptr)) { printf("packed: %s\n", g_err); return 1; }
+  CHECK(hipDeviceSynchronize());
+  const char* PA = ws;
+  const char* PB = ws + pp.TM * pp.pstride;
+  const dim3 grid((unsigned)(pp.TM * pp.TN));
+  const double flop = 2.0 * N * N * N;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  unsigned long long* dcnt;
+  CHECK(hipMalloc(&dcnt, 8));
+  unsigned long long* st;
+  CHECK(hipMalloc(&st, (size_t)grid.x * 8 * 2 * 8));
+  typedef void (*kfn)(const cubed_gemm_chain_t*, const char*, const char*, PackPlan, GemmGrid, unsigned long long*);
+  auto run = [&](const char* name, kfn f, int threads, bool stamp, int mfma_cyc, bool check) {
+    float best = 1e30f;
+    for (int r = 0; r < reps + 1; ++r) {
+      CHECK(hipMemset(C1, 0, slot_out * nb * nb));
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(f, grid, dim3(threads), 0, 0, dt1, PA, PB, pp, gg, stamp ? st : nullptr);
+      CHECK(hipGetLastError());
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-46s best %9.3f ms %7.1f TF", name, best, flop / best / 1e9);
+    if (stamp) {
+      const int nw = threads / 64;
+      std::vector<unsigned long long> h((size_t)grid.x * nw * 2);
+      CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+      double cyc = 0, units = 0;
+      for (size_t i = 0; i < h.size(); i += 2) {
+        cyc += (double)h[i];
+        units += (double)h[i + 1];
+      }
+      // cycles per MFMA of ONE wave (w4p: 32 per step of 32x32x16; 8p: 16 per
+      // phase of 16x16x32) and the clock from the mean wave's loop time
+      const double per = mfma_cyc == 32 ? 32.0 : 16.0;
+      printf("  loop %6.2f cyc per wave MFMA (ideal 32)  clock ~%.2f GHz", cyc / (units * per),
+             (cyc / (h.size() / 2)) * ((double)grid.x / 256.0) / (best * 1e-3) / 1e9);
+    }
+    printf("\n");
+    if (check) {
+      CHECK(hipMemset(dcnt, 0, 8));
+      k_mismatch<<<4096, 256>>>((const uint32_t*)C0, (const uint32_t*)C1, slot_out * nb * nb / 4, dcnt);
+      unsigned long long c;
+      CHECK(hipMemcpy(&c, dcnt, 8, hipMemcpyDeviceToHost));
+      printf("   words differing from the library result: %llu of %lld\n", c, (long long)(slot_out * nb * nb / 4));
+    }
+    fflush(stdout);
+  };
+  printf("# N %lld chunk %lld, %s out, TM %lld TN %lld KTL %lld\n", (long long)N, (long long)Cc, obf ? "bf16" : "f32",
+         (long long)pp.TM, (long long)pp.TN, (long long)pp.KTL);
+  kfn w4p = obf ? (kfn)k_gemm_bf16_w4p<true> : (kfn)k_gemm_bf16_w4p<false>;
+  kfn w4ps = obf ? (kfn)k_gemm_bf16_w4p<true, true> : (kfn)k_gemm_bf16_w4p<false, true>;
+  kfn e8 = obf ? (kfn)k_gemm_bf16_8p<true> : (kfn)k_gemm_bf16_8p<false>;
+  kfn e8s = obf ? (kfn)k_gemm_bf16_8p<true, true> : (kfn)k_gemm_bf16_8p<false, true>;
+  const int arms = argc > 4 ? atoi(argv[4]) : 0;
+  run("w4p (library, one wave per SIMD)", w4p, 256, false, 32, true);
+  run("8p  (two waves per SIMD, library form)", e8, 512, false, 16, true);
+  if (arms == 0) {
+    run("w4p stamped", w4ps, 256, true, 32, false);
+    run("8p  stamped", e8s, 512, true, 16, false);
+    run("w4p (again)", w4p, 256, false, 32, false);
+    run("8p  (again)", e8, 512, false, 16, true);
+    return 0;
+  }
+#define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
+  ARM("8p VAR 1 (staging before the reads)", 1, 4);
+  ARM("8p VAR 2 (setprio around MFMA clusters)", 2, 4);
+  ARM("8p VAR 4 (group 1 static priority)", 4, 4);
+  ARM("8p GM 8", 0, 8);
+  run("8p  (again)", e8, 512, false, 16, false);
+  run("w4p (again)", w4p, 256, false, 32, false);
+  return 0;
+}
