@@ -46,6 +46,9 @@ constexpr int E8_NSLOT = 10, E8_HALF = 16384, E8_LEAD = 7;
 // phase 2 with its B sub-tile 0 read in phase 3 (reads 8 / 4 / 8 / 4; 95.1-99.3
 // ms: the shorter lead of the last half-tile), phase 0's pieces split around
 // its B reads (99.6), tile groups of 2 / 8 / 16 rows (95.4 / 90.7 / 97.8).
+// Ablations (probe only, WRONG results): 8 = no staging in the K loop, 16 =
+// every half-tile staged from K tile 0's addresses (L2-resident fills), 32 =
+// no fragment reads in the K loop.
 template <bool OUT_BF16, bool STAMP = false, int VAR = 0, int GM = 4>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_t* __restrict__ tasks,
                                                       const char* __restrict__ PA, const char* __restrict__ PB,
@@ -71,7 +74,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
   const int64_t aks = pp.akstride;
   CUBED_L char* const dw = lds + (2 * w) * 1024;
   auto stage = [&](int u) __attribute__((always_inline)) {
-    const int kt = u >> 2, h = u & 3;
+    if constexpr ((VAR & 8) != 0) return;
+    const int kt = (VAR & 16) ? 0 : u >> 2, h = u & 3;
     const char* src = h < 2 ? sA + kt * aks + h * E8_HALF : sB + (int64_t)kt * 32768 + (h - 2) * E8_HALF;
     CUBED_L char* d = dw + (u % E8_NSLOT) * E8_HALF;
     glds16(src, d);
@@ -91,12 +95,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  bf16x8 a[4][2] = {}, b0[2][2] = {}, b1[2][2] = {};
 
   auto rd = [&](CUBED_L const char* base, int off) __attribute__((always_inline)) {
     return *(const CUBED_L bf16x8*)(base + off);
   };
   auto read_a = [&](int t, int qm) __attribute__((always_inline)) {
+    if constexpr ((VAR & 32) != 0) return;
     CUBED_L const char* base = lds + ((4 * t + g) % E8_NSLOT) * E8_HALF;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -104,6 +109,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
       for (int kq = 0; kq < 2; ++kq) a[mt][kq] = rd(base, lo[kq] + (qm * 64 + mt * 16) * 128);
   };
   auto read_b = [&](int t, int qn, bf16x8 (&b)[2][2]) __attribute__((always_inline)) {
+    if constexpr ((VAR & 32) != 0) return;
     CUBED_L const char* base = lds + ((4 * t + 2 + hb) % E8_NSLOT) * E8_HALF + bcol;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)

@@ -27,6 +27,43 @@ __global__ void k_fill(uint16_t* p, int64_t n, uint32_t seed) {
   }
 }
 
+// pack A with all 8 rows' loads of a block issued before its stores (the
+// library form unrolls by 2)
+__global__ __launch_bounds__(256) void k_pack_a8(const cubed_gemm_chain_t* __restrict__ tasks,
+                                                 const cubed_gemm_seg_t* __restrict__ segs, PackPlan pp,
+                                                 char* __restrict__ PA) {
+  const int64_t nkt = pp.kt1 - pp.kt0, nblk = pp.TM * nkt;
+  const cubed_gemm_seg_t* __restrict__ sg0 = segs + tasks[0].seg0;
+  const int sl = threadIdx.x & 7;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t mt = blk / nkt, kt = pp.kt0 + (blk - mt * nkt);
+    const int64_t I0 = (mt * 256) / pp.cm, mb = (I0 + 1) * pp.cm;
+    int64_t s0 = 0, ks0 = 0;
+    if (kt * 64 < pp.K) seg_at(sg0, kt * 64, s0, ks0);
+    char* dst = PA + mt * pp.apstride + kt * pp.akstride;
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = (threadIdx.x >> 3) + 32 * j, c = sl ^ ((r >> 1) & 7);
+      const int64_t gm = mt * 256 + r, k = kt * 64 + c * 8;
+      v[j] = uint4{0, 0, 0, 0};
+      if (gm < pp.M && k < pp.K) {
+        int64_t s = s0, ks = ks0;
+        seg_at(sg0, k, s, ks);
+        const bool hi = gm >= mb;
+        const int64_t I = hi ? I0 + 1 : I0, lm = gm - I * pp.cm;
+        const cubed_gemm_seg_t& S = segs[tasks[I * pp.tj].seg0 + s];
+        v[j] = __builtin_nontemporal_load((const uint4*)((const char*)(uintptr_t)S.a + (lm * S.lda + (k - ks)) * 2));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = (threadIdx.x >> 3) + 32 * j;
+      *(uint4*)(dst + r * 128 + sl * 16) = v[j];
+    }
+  }
+}
+
 __global__ void k_mismatch(const uint32_t* a, const uint32_t* b, int64_t n, unsigned long long* out) {
   unsigned long long c = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -138,6 +175,45 @@ int main(int argc, char** argv) {
   kfn e8 = obf ? (kfn)k_gemm_bf16_8p<true> : (kfn)k_gemm_bf16_8p<false>;
   kfn e8s = obf ? (kfn)k_gemm_bf16_8p<true, true> : (kfn)k_gemm_bf16_8p<false, true>;
   const int arms = argc > 4 ? atoi(argv[4]) : 0;
+  {  // the library's packs, timed alone
+    const int64_t na = pp.TM * pp.KTL, nbk = pp.TN * pp.KTL;
+    const dim3 ga((unsigned)(na < 16384 ? na : 16384)), gb((unsigned)(nbk < 16384 ? nbk : 16384));
+    char* PAw = ws;
+    char* PBw = ws + pp.TM * pp.pstride;
+    for (int r = 0; r < 3; ++r) {
+      float ma, mb;
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, 0, dt0, ds, pp, PAw);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ma, e0, e1));
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, 0, dt0, ds, pp, PBw);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&mb, e0, e1));
+      const double bytes = (double)pp.TM * pp.pstride;  // written (read ~ the same)
+      printf("pack A %.3f ms (%.0f GB/s moved)  pack B^T %.3f ms (%.0f GB/s moved)\n", ma, 2 * bytes / ma / 1e6, mb,
+             2 * bytes / mb / 1e6);
+    }
+    char* PA2;
+    CHECK(hipMalloc(&PA2, pp.TM * pp.pstride));
+    for (int r = 0; r < 3; ++r) {
+      float ma;
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_pack_a8, ga, dim3(256), 0, 0, dt0, ds, pp, PA2);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      CHECK(hipEventElapsedTime(&ma, e0, e1));
+      printf("pack A, 8 loads in flight (nt) %.3f ms (%.0f GB/s moved)\n", ma, 2.0 * pp.TM * pp.pstride / ma / 1e6);
+    }
+    CHECK(hipMemset(dcnt, 0, 8));
+    k_mismatch<<<4096, 256>>>((const uint32_t*)PAw, (const uint32_t*)PA2, pp.TM * pp.pstride / 4, dcnt);
+    unsigned long long c;
+    CHECK(hipMemcpy(&c, dcnt, 8, hipMemcpyDeviceToHost));
+    printf("   words differing from the library pack: %llu\n", c);
+    CHECK(hipFree(PA2));
+  }
   run("w4p (library, one wave per SIMD)", w4p, 256, false, 32, true);
   run("8p  (two waves per SIMD, library form)", e8, 512, false, 16, true);
   if (arms == 0) {
@@ -148,10 +224,17 @@ int main(int argc, char** argv) {
     return 0;
   }
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
-  ARM("8p VAR 1 (staging before the reads)", 1, 4);
-  ARM("8p VAR 2 (setprio around MFMA clusters)", 2, 4);
-  ARM("8p VAR 4 (group 1 static priority)", 4, 4);
-  ARM("8p GM 8", 0, 8);
+  if (arms == 2) {
+    ARM("8p ABL no staging", 8, 4);
+    ARM("8p ABL L2-resident staging", 16, 4);
+    ARM("8p ABL no fragment reads", 32, 4);
+    ARM("8p ABL neither staging nor reads", 40, 4);
+  } else {
+    ARM("8p VAR 1 (staging before the reads)", 1, 4);
+    ARM("8p VAR 2 (setprio around MFMA clusters)", 2, 4);
+    ARM("8p VAR 4 (group 1 static priority)", 4, 4);
+    ARM("8p GM 8", 0, 8);
+  }
   run("8p  (again)", e8, 512, false, 16, false);
   run("w4p (again)", w4p, 256, false, 32, false);
   return 0;
