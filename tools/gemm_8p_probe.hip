@@ -53,7 +53,9 @@ __global__ __launch_bounds__(256) void k_pack_a8(const cubed_gemm_chain_t* __res
         const bool hi = gm >= mb;
         const int64_t I = hi ? I0 + 1 : I0, lm = gm - I * pp.cm;
         const cubed_gemm_seg_t& S = segs[tasks[I * pp.tj].seg0 + s];
-        v[j] = __builtin_nontemporal_load((const uint4*)((const char*)(uintptr_t)S.a + (lm * S.lda + (k - ks)) * 2));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load((const u32x4*)((const char*)(uintptr_t)S.a + (lm * S.lda + (k - ks)) * 2));
+        v[j] = uint4{x.x, x.y, x.z, x.w};
       }
     }
 #pragma unroll
