@@ -155,6 +155,20 @@ def _cases(rank, world, zdir):
     out["five_sum"] = xp.sum(y5).compute(resume=True)
     note("five")
 
+    # matmul whose chunk grid divides by the world (6 x 6 at 2 and 3 ranks):
+    # A's packed image assembled by point-to-point transfers (DistGemmLaunch)
+    from cubed_amd.runtime.executors.dist import DistGemmLaunch
+
+    for name, dt in (("bf16", xp.bfloat16), ("f32", xp.float32)):
+        random.seed(31)
+        A6 = xp.astype(crandom.random((700, 1200), chunks=(300, 200), spec=spec), dt)
+        B6 = xp.astype(crandom.random((1200, 1584), chunks=(200, 264), spec=spec), dt)
+        arrays_to_plan(A6, B6).execute(executor=ex, array_names=[A6.name, B6.name])
+        out[f"mm6_{name}"] = xp.matmul(A6, B6).compute(resume=True)
+        out[f"mm6_{name}_dist"] = np.array([any(isinstance(l, DistGemmLaunch)
+                                               for v in ex._cache.values() for l in v[1])])
+    note("mm6")
+
     # Zarr sink written by every rank (its own chunks), read back as a source
     zpath = os.path.join(zdir, "w.zarr")
     cubed.to_zarr(zc * 3, zpath)
@@ -224,6 +238,27 @@ def test_distributed_executor_matches_oracle(world, tmp_path):
     assert np.array_equal(got["stack"], np.stack([a70, a70 * 2], axis=1))
     assert np.array_equal(got["reshape"], np.arange(24.0).reshape(4, 6))
     assert np.array_equal(got["zarr"], z * 3)
+
+    # the multi-GPU matmul is bit-identical to the 1-GPU chained GEMM
+    import torch
+
+    import cubed_amd as cubed
+    import cubed_amd.array_api as xp
+    import cubed_amd.random as crandom
+    from cubed_amd.core.plan import arrays_to_plan
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+
+    ex1 = GpuDagExecutor("cuda:0", comm=None)
+    spec1 = cubed.Spec(allowed_mem="2GB", reserved_mem="100MB", executor=ex1)
+    for name, dt in (("bf16", xp.bfloat16), ("f32", xp.float32)):
+        random.seed(31)
+        A6 = xp.astype(crandom.random((700, 1200), chunks=(300, 200), spec=spec1), dt)
+        B6 = xp.astype(crandom.random((1200, 1584), chunks=(200, 264), spec=spec1), dt)
+        arrays_to_plan(A6, B6).execute(executor=ex1, array_names=[A6.name, B6.name])
+        want = xp.matmul(A6, B6).compute(resume=True)
+        assert got[f"mm6_{name}_dist"].all(), name
+        assert np.array_equal(got[f"mm6_{name}"].view(np.uint32), want.view(np.uint32)), name
+    torch.cuda.synchronize()
 
     F = [R.random_array((60, 40), (10, 20), sd) for sd in _seeds(21, 5)]
     y5 = F[0] * F[1] + F[2] * F[3] - F[4]
