@@ -5,7 +5,8 @@
 // csrc/gemm_bf16_8p.h), alternating; the outputs compared word for word.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude \
 //          -o tools/gemm_8p_probe tools/gemm_8p_probe.hip
-// Run:   tools/gemm_8p_probe [reps] [N] [out: 0 f32 / 1 bf16]
+// Run:   tools/gemm_8p_probe [reps] [N] [out: 0 f32 / 1 bf16] [arms] -- arms 3: f32 INPUTS
+//        (k_gemm_f32_w4p vs k_gemm_f32_8p)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,6 +67,14 @@ __global__ __launch_bounds__(256) void k_pack_a8(const cubed_gemm_chain_t* __res
   }
 }
 
+__global__ void k_fill32(float* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    p[i] = (float)(h >> 8) * (1.0f / 16777216.0f);
+  }
+}
+
 __global__ void k_mismatch(const uint32_t* a, const uint32_t* b, int64_t n, unsigned long long* out) {
   unsigned long long c = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -77,16 +86,23 @@ int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 3;
   const int64_t N = argc > 2 ? atoll(argv[2]) : 40000, Cc = 5000, nb = N / Cc;
   const bool obf = argc > 3 && atoi(argv[3]) == 1;
+  const bool f32in = argc > 4 && atoi(argv[4]) == 3;
+  const int32_t in_code = f32in ? CUBED_F32 : CUBED_BF16;
   const int64_t al = 32;  // the executor's slot alignment (storage.SLOT_ALIGN)
-  const int64_t slot_in = (Cc * Cc * 2 + al - 1) / al * al;
+  const int64_t slot_in = (Cc * Cc * (f32in ? 4 : 2) + al - 1) / al * al;
   const int64_t slot_out = (Cc * Cc * (obf ? 2 : 4) + al - 1) / al * al;
   char *A, *B, *C0, *C1;
   CHECK(hipMalloc(&A, slot_in * nb * nb));
   CHECK(hipMalloc(&B, slot_in * nb * nb));
   CHECK(hipMalloc(&C0, slot_out * nb * nb));
   CHECK(hipMalloc(&C1, slot_out * nb * nb));
-  k_fill<<<4096, 256>>>((uint16_t*)A, slot_in * nb * nb / 2, 12345u);
-  k_fill<<<4096, 256>>>((uint16_t*)B, slot_in * nb * nb / 2, 777u);
+  if (f32in) {
+    k_fill32<<<4096, 256>>>((float*)A, slot_in * nb * nb / 4, 12345u);
+    k_fill32<<<4096, 256>>>((float*)B, slot_in * nb * nb / 4, 777u);
+  } else {
+    k_fill<<<4096, 256>>>((uint16_t*)A, slot_in * nb * nb / 2, 12345u);
+    k_fill<<<4096, 256>>>((uint16_t*)B, slot_in * nb * nb / 2, 777u);
+  }
   std::vector<cubed_gemm_chain_t> tasks(nb * nb);
   std::vector<cubed_gemm_seg_t> segs(nb * nb * nb);
   for (int64_t i = 0; i < nb; ++i)
@@ -108,15 +124,15 @@ int main(int argc, char** argv) {
   CHECK(hipMemcpy(dt1, tasks.data(), sizeof(cubed_gemm_chain_t) * tasks.size(), hipMemcpyHostToDevice));
   CHECK(hipMemcpy(ds, segs.data(), sizeof(cubed_gemm_seg_t) * segs.size(), hipMemcpyHostToDevice));
   const int32_t out_code = obf ? CUBED_BF16 : CUBED_F32;
-  const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, out_code);
+  const int64_t wsb = cubed_gemm_pack_bytes(tasks.data(), nb, nb, segs.data(), segs.size(), in_code, out_code);
   if (wsb <= 0) { printf("pack_bytes: %s\n", g_err); return 1; }
   char* ws;
   CHECK(hipMalloc(&ws, wsb));
   PackPlan pp;
   GemmGrid gg;
-  if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), CUBED_BF16, out_code, pp, gg)) return 1;
+  if (pack_plan(tasks.data(), nb, nb, segs.data(), segs.size(), in_code, out_code, pp, gg)) return 1;
   // the library entry: pack + w4p GEMM into C0 (the reference result)
-  if (cubed_gemm_chain_packed(tasks.data(), dt0, nb, nb, segs.data(), ds, segs.size(), CUBED_BF16, out_code, ws, wsb,
+  if (cubed_gemm_chain_packed(tasks.data(), dt0, nb, nb, segs.data(), ds, segs.size(), in_code, out_code, ws, wsb,
                               nullptr)) { printf("packed: %s\n", g_err); return 1; }
   CHECK(hipDeviceSynchronize());
   const char* PA = ws;
@@ -177,6 +193,18 @@ int main(int argc, char** argv) {
   kfn e8 = obf ? (kfn)k_gemm_bf16_8p<true> : (kfn)k_gemm_bf16_8p<false>;
   kfn e8s = obf ? (kfn)k_gemm_bf16_8p<true, true> : (kfn)k_gemm_bf16_8p<false, true>;
   const int arms = argc > 4 ? atoi(argv[4]) : 0;
+  if (f32in) {  // f32 inputs: the one-wave w4p kernel vs the two-wave 8p kernel
+    printf("# f32 inputs\n");
+    run("f32 w4p (one wave per SIMD)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
+    run("f32 8p (two waves per SIMD)", (kfn)k_gemm_f32_8p<0>, 512, false, 16, true);
+    run("f32 w4p stamped", (kfn)k_gemm_f32_w4p<true>, 256, true, 32, false);
+    run("f32 8p stamped", (kfn)k_gemm_f32_8p<1>, 512, true, 16, false);
+    run("f32 8p two phases per step", (kfn)k_gemm_f32_8p<2>, 512, false, 16, true);
+    run("f32 8p two phases per step, stamped", (kfn)k_gemm_f32_8p<3>, 512, true, 16, false);
+    run("f32 w4p (again)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, false);
+    run("f32 8p (again)", (kfn)k_gemm_f32_8p<0>, 512, false, 16, true);
+    return 0;
+  }
   {  // the library's packs, timed alone
     const int64_t na = pp.TM * pp.KTL, nbk = pp.TN * pp.KTL;
     const dim3 ga((unsigned)(na < 16384 ? na : 16384)), gb((unsigned)(nbk < 16384 ? nbk : 16384));
