@@ -885,7 +885,6 @@ __global__ __launch_bounds__(256) void k_gemm_any_chain(const cubed_gemm_chain_t
 }
 
 #include "gemm_f32_w4p.h"
-#include "gemm_f32_8p.h"
 
 int fail(const char* m) {
   snprintf(g_err, sizeof(g_err), "cubed_gemm_chain: %s", m);

@@ -193,16 +193,10 @@ int main(int argc, char** argv) {
   kfn e8 = obf ? (kfn)k_gemm_bf16_8p<true> : (kfn)k_gemm_bf16_8p<false>;
   kfn e8s = obf ? (kfn)k_gemm_bf16_8p<true, true> : (kfn)k_gemm_bf16_8p<false, true>;
   const int arms = argc > 4 ? atoi(argv[4]) : 0;
-  if (f32in) {  // f32 inputs: the one-wave w4p kernel vs the two-wave 8p kernel
-    printf("# f32 inputs\n");
+  if (f32in) {  // f32 inputs: the library's one-wave w4p kernel (the two-wave f32 form,
+    // gemm_f32_8p.h, lost: 943-959 ms vs 876; commit e0bc44c, profiles/r06_gemm_f32_8p.log)
     run("f32 w4p (one wave per SIMD)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
-    run("f32 8p (two waves per SIMD)", (kfn)k_gemm_f32_8p<0>, 512, false, 16, true);
     run("f32 w4p stamped", (kfn)k_gemm_f32_w4p<true>, 256, true, 32, false);
-    run("f32 8p stamped", (kfn)k_gemm_f32_8p<1>, 512, true, 16, false);
-    run("f32 8p two phases per step", (kfn)k_gemm_f32_8p<2>, 512, false, 16, true);
-    run("f32 8p two phases per step, stamped", (kfn)k_gemm_f32_8p<3>, 512, true, 16, false);
-    run("f32 w4p (again)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, false);
-    run("f32 8p (again)", (kfn)k_gemm_f32_8p<0>, 512, false, 16, true);
     return 0;
   }
   {  // the library's packs, timed alone
