@@ -6,6 +6,7 @@ performance: how many launches a pipeline becomes, whether the streaming
 fast path is taken, and that reduction chains are fused into one pass.
 """
 
+import re
 import ctypes
 import math
 import random
@@ -856,7 +857,8 @@ def test_partials_programs_compile_a_specialised_finish(built, dry):
     C.memmove(C.addressof(P), C.addressof(L.prog), C.sizeof(P))
     P.mode |= Lw.MODE_PARTIALS
     src = nat.program_source(nat.compile_program(P))
-    assert "_partials_finish(" in src and "cubed::finish_soa_body(JP," in src
+    # kernel names: <main>_partials_p<program digest>_finish / _fold
+    assert re.search(r"_partials_p[0-9a-f]{8}_finish\(", src) and "cubed::finish_soa_body(JP," in src
     # ... and the lifted fold with the program's own epilogue
-    assert "_partials_fold(" in src and "cubed::fold_groups_split_body<true>(JP," in src
+    assert re.search(r"_partials_p[0-9a-f]{8}_fold\(", src) and "cubed::fold_groups_split_body<true>(JP," in src
     assert {"cubed_fused_finish_compiled", "cubed_fold_groups_compiled"} <= set(nat.EXPORTED_SYMBOLS)

@@ -247,6 +247,44 @@ int main(int argc, char** argv) {
     run("8p  (again)", e8, 512, false, 16, true);
     return 0;
   }
+  if (arms == 4) {  // packing on a second stream while the 8p GEMM runs (into a separate image)
+    char* ws2;
+    CHECK(hipMalloc(&ws2, wsb));
+    hipStream_t s2;
+    CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t p0, p1, g1;
+    CHECK(hipEventCreate(&p0));
+    CHECK(hipEventCreate(&p1));
+    CHECK(hipEventCreate(&g1));
+    const int64_t na = pp.TM * pp.KTL, nbk = pp.TN * pp.KTL;
+    kfn f = obf ? (kfn)k_gemm_bf16_8p<true> : (kfn)k_gemm_bf16_8p<false>;
+    for (int pg : {16384, 2048, 512, 256}) {
+      const dim3 ga((unsigned)(na < pg ? na : pg)), gb((unsigned)(nbk < pg ? nbk : pg));
+      for (int order = 0; order < 2; ++order)
+        for (int r = 0; r < 3; ++r) {
+          CHECK(hipDeviceSynchronize());
+          CHECK(hipEventRecord(e0, 0));
+          CHECK(hipStreamWaitEvent(s2, e0, 0));
+          if (order == 1) hipLaunchKernelGGL(f, grid, dim3(512), 0, 0, dt1, PA, PB, pp, gg, nullptr);
+          CHECK(hipEventRecord(p0, s2));
+          hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, s2, dt0, ds, pp, ws2);
+          hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, s2, dt0, ds, pp, ws2 + pp.TM * pp.pstride);
+          CHECK(hipEventRecord(p1, s2));
+          if (order == 0) hipLaunchKernelGGL(f, grid, dim3(512), 0, 0, dt1, PA, PB, pp, gg, nullptr);
+          CHECK(hipEventRecord(g1, 0));
+          CHECK(hipDeviceSynchronize());
+          float mp, mg, mpp;
+          CHECK(hipEventElapsedTime(&mp, e0, p1));
+          CHECK(hipEventElapsedTime(&mpp, p0, p1));
+          CHECK(hipEventElapsedTime(&mg, e0, g1));
+          printf("concurrent pack grid %5d %s: packs done at %8.3f ms (own span %8.3f)  GEMM done at %8.3f ms\n", pg,
+                 order ? "GEMM first" : "pack first", mp, mpp, mg);
+          fflush(stdout);
+        }
+    }
+    run("8p alone", f, 512, false, 16, false);
+    return 0;
+  }
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
   if (arms == 2) {
     ARM("8p ABL no staging", 8, 4);
