@@ -65,6 +65,20 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + i;
 }
 
+// (probe) the 8 XCDs on different row groups of GM tile rows (per_group
+// tiles each) but at the same columns: XCD x's i-th workgroup takes group x + 8
+// (i / per_group) while every XCD has whole groups left, then a contiguous
+// share of the rest (as xcd_remap) -- B column panels read by all eight XCDs
+// at about the same time, for the memory-side cache to serve.
+__device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t per_group, int64_t full_groups) {
+  const int64_t main = (full_groups >> 3) * per_group;
+  const int64_t x = b & 7, i = b >> 3;
+  if (nblk < 8 || main == 0) return xcd_remap(b, nblk);
+  if (i < main) return (x + 8 * (i / per_group)) * per_group + i % per_group;
+  const int64_t S = nblk - 8 * main, q = S >> 3, r = S & 7;
+  return 8 * main + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (i - main);
+}
+
 // tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked
 // column by column, so the workgroups resident on one XCD share A row panels
 // and B column panels in its L2.

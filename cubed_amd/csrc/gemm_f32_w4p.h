@@ -94,7 +94,8 @@ __global__ __launch_bounds__(256) void k_pack_b_f32(const cubed_gemm_chain_t* __
 // and stages step p + 4 into stage p % 4 (free once every wave passed step p's
 // barrier).  The wait before step p's barrier leaves steps p + 2 and p + 3's
 // 16 pieces in flight.  STAMP: per-wave main-loop cycles (probe builds only).
-template <bool STAMP = false>
+// LOCK: tile order xcd_lockstep (probe: false = xcd_remap's contiguous ranges).
+template <bool STAMP = false, bool LOCK = true>
 __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_t* __restrict__ tasks,
                                                       const char* __restrict__ PA, const char* __restrict__ PB,
                                                       PackPlan pp, GemmGrid gg,
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_
   __shared__ __attribute__((aligned(1024))) char lds_[WPF_NS * WPF_STAGE];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t, m0, n0;
-  tile_of<HF_BM, HF_BN, 4>(xcd_remap(blockIdx.x, gridDim.x), pp.TM, pp.TN, t, m0, n0);
+  const int64_t lt = LOCK ? xcd_lockstep(blockIdx.x, gridDim.x, 4 * pp.TN, pp.TM / 4) : xcd_remap(blockIdx.x, gridDim.x);
+  tile_of<HF_BM, HF_BN, 4>(lt, pp.TM, pp.TN, t, m0, n0);
   const int64_t M = pp.M, N = pp.N;
   if (t != 0 || m0 >= M || n0 >= N) return;
   const int64_t nst = pp.KTL;

@@ -195,8 +195,10 @@ int main(int argc, char** argv) {
   const int arms = argc > 4 ? atoi(argv[4]) : 0;
   if (f32in) {  // f32 inputs: the library's one-wave w4p kernel (the two-wave f32 form,
     // gemm_f32_8p.h, lost: 943-959 ms vs 876; commit e0bc44c, profiles/r06_gemm_f32_8p.log)
-    run("f32 w4p (one wave per SIMD)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
-    run("f32 w4p stamped", (kfn)k_gemm_f32_w4p<true>, 256, true, 32, false);
+    run("f32 w4p (lockstep XCD order)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
+    run("f32 w4p (contiguous XCD ranges)", (kfn)k_gemm_f32_w4p<false, false>, 256, false, 32, true);
+    run("f32 w4p (lockstep XCD order)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, false);
+    run("f32 w4p (contiguous XCD ranges)", (kfn)k_gemm_f32_w4p<false, false>, 256, false, 32, false);
     return 0;
   }
   {  // the library's packs, timed alone
@@ -286,7 +288,11 @@ int main(int argc, char** argv) {
     return 0;
   }
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
-  if (arms == 2) {
+  if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
+    ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
+    ARM("8p lockstep GM 8", 0, 8);
+    ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
+  } else if (arms == 2) {
     ARM("8p ABL no staging", 8, 4);
     ARM("8p ABL L2-resident staging", 16, 4);
     ARM("8p ABL no fragment reads", 32, 4);
