@@ -70,13 +70,26 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblk) {
 // (i / per_group) while every XCD has whole groups left, then a contiguous
 // share of the rest (as xcd_remap) -- B column panels read by all eight XCDs
 // at about the same time, for the memory-side cache to serve.
+// The rest (rr_tail): runs of 32 tiles of the grouped order (GM x 8 of one
+// group) dealt round robin, so the eight XCDs work on neighbouring columns of
+// one row group (its A panels read by all eight together); the last < 256
+// tiles as contiguous shares.
+template <bool RR_TAIL = true>
 __device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t per_group, int64_t full_groups) {
   const int64_t main = (full_groups >> 3) * per_group;
   const int64_t x = b & 7, i = b >> 3;
   if (nblk < 8 || main == 0) return xcd_remap(b, nblk);
   if (i < main) return (x + 8 * (i / per_group)) * per_group + i % per_group;
-  const int64_t S = nblk - 8 * main, q = S >> 3, r = S & 7;
-  return 8 * main + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (i - main);
+  int64_t S = nblk - 8 * main, j = i - main, base = 8 * main;
+  if constexpr (RR_TAIL) {
+    const int64_t runs = (S >> 8) << 8 >> 5;  // whole rounds of 8 runs of 32
+    if (j < runs * 4) return base + ((j >> 5) * 8 + x) * 32 + (j & 31);
+    base += runs * 32;
+    S -= runs * 32;
+    j -= runs * 4;
+  }
+  const int64_t q = S >> 3, r = S & 7;
+  return base + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
 }
 
 // tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked

@@ -290,8 +290,9 @@ int main(int argc, char** argv) {
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
   if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
-    ARM("8p lockstep GM 8", 0, 8);
+    ARM("8p lockstep, contiguous tail", 128, 4);
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
+    ARM("8p lockstep, contiguous tail", 128, 4);
   } else if (arms == 2) {
     ARM("8p ABL no staging", 8, 4);
     ARM("8p ABL L2-resident staging", 16, 4);
