@@ -312,6 +312,18 @@ int check_program(const cubed_program_t& P) {
     set_err("cubed_fused_chunks: host-provided counts need partials mode");
     return CUBED_E_ARG;
   }
+  if (P.mode & CUBED_MODE_OWNER_MAJOR) {
+    int stored = 0;
+    for (int f = 0; f < P.nfields; ++f) stored += P.field_rop[f] != CUBED_R_COUNT;
+    const int64_t mko = P.consts[CUBED_MAX_CONSTS - 3].i, w = P.consts[CUBED_MAX_CONSTS - 2].i,
+                  l = P.consts[CUBED_MAX_CONSTS - 1].i;
+    if (!(P.mode & CUBED_MODE_STREAM) || !(P.mode & CUBED_MODE_PARTIALS) || !(P.mode & CUBED_MODE_HOST_COUNT) ||
+        stored != 1 || mko < 1 || w < 1 || l < 1) {
+      set_err("cubed_fused_chunks: owner-major partials need stream + partials + host counts, one stored field "
+              "and mko, W, L >= 1");
+      return CUBED_E_ARG;
+    }
+  }
   if ((P.mode & (CUBED_MODE_STREAM_W2 | CUBED_MODE_STREAM_W4)) &&
       (!(P.mode & CUBED_MODE_STREAM) || (P.mode & CUBED_MODE_STREAM_W2 && P.mode & CUBED_MODE_STREAM_W4))) {
     set_err("cubed_fused_chunks: stream group bits need stream mode (one of W2 / W4)");
@@ -356,6 +368,10 @@ extern "C" int cubed_fused_chunks(const cubed_program_t* prog, const cubed_progr
   if (L.ws_bytes > 0 && (d_workspace == nullptr || workspace_bytes < L.ws_bytes)) {
     set_err("cubed_fused_chunks: workspace too small");
     return CUBED_E_WORKSPACE;
+  }
+  if (!owner_major_fits(P, L.soa_elems)) {
+    set_err("cubed_fused_chunks: owner-major slots exceed the SoA block");
+    return CUBED_E_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
   Acc* ws = (Acc*)d_workspace + L.soa_elems;  // partials mode: SoA block first

@@ -131,6 +131,15 @@ int launch_collect(const cubed_program_t& P, const cubed_program_t* dP, const La
                    hipStream_t st);  // 0 or a CUBED_E_* code (message set)
 void set_error(const char* msg);
 
+// CUBED_MODE_OWNER_MAJOR: every owner-major slot (W x L groups of mko) lies
+// inside the launch's SoA block
+inline bool owner_major_fits(const cubed_program_t& P, int64_t soa_elems) {
+  if (!(P.mode & CUBED_MODE_OWNER_MAJOR)) return true;
+  const int64_t mko = P.consts[CUBED_MAX_CONSTS - 3].i, w = P.consts[CUBED_MAX_CONSTS - 2].i,
+                l = P.consts[CUBED_MAX_CONSTS - 1].i;
+  return mko * w * l <= soa_elems;
+}
+
 #endif  // __HIPCC_RTC__
 
 }  // namespace cubed

@@ -290,6 +290,10 @@ extern "C" int cubed_fused_chunks_compiled(void* handle, const cubed_program_t* 
     set_error("cubed_fused_chunks_compiled: workspace too small");
     return CUBED_E_WORKSPACE;
   }
+  if (!owner_major_fits(P, L.soa_elems)) {
+    set_error("cubed_fused_chunks_compiled: owner-major slots exceed the SoA block");
+    return CUBED_E_ARG;
+  }
   hipFunction_t fmain = nullptr, ffin = nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (int rc = load((JitKernel*)handle, st, &fmain, &ffin)) return rc;

@@ -1024,6 +1024,18 @@ CUBED_DEV void stream_body(
   const int64_t wslots = partials ? slots_max : slots;
   auto store_soa = [&](int64_t el, const Acc (&x)[CUBED_MAX_FIELDS], bool valid) {
     if (el >= max_kept) return;
+    if (P.mode & CUBED_MODE_OWNER_MAJOR) {
+      // straight into the reduce-scatter's owner-major order (dist.ScatterCombine):
+      // group g's elements to rank g % W's slot g / W
+      const int64_t mko = P.consts[CUBED_MAX_CONSTS - 3].i, wr = P.consts[CUBED_MAX_CONSTS - 2].i,
+                    lr = P.consts[CUBED_MAX_CONSTS - 1].i;
+      const int64_t i = t * max_kept + el, g = i / mko;
+      Acc* __restrict__ d = soa + ((g % wr) * lr + g / wr) * mko + (i - g * mko);
+#pragma unroll
+      for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
+        if (f < nf && P.field_rop[f] != CUBED_R_COUNT) *d = valid ? x[f] : acc_init(P.field_rop[f], P.field_acc[f]);
+      return;
+    }
 #pragma unroll
     for (int f = 0; f < CUBED_MAX_FIELDS; ++f)
       if (f < nf && (!(P.mode & CUBED_MODE_HOST_COUNT) || P.field_rop[f] != CUBED_R_COUNT))

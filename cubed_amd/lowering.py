@@ -680,6 +680,17 @@ class FusedLaunch:
         self.ws = torch.zeros(max(ws_bytes, 16), dtype=torch.uint8, device=device) if ws_bytes else None
         self.ws_bytes = ws_bytes
 
+    def reprogram(self):
+        """Re-upload and re-compile ``prog`` after the host changed it once
+        the launch's consumer was known (mode bits and consts set by
+        dist.DistPiecesLaunch for owner-major partials)."""
+        import torch
+
+        raw = np.frombuffer(ctypes.string_at(ctypes.addressof(self.prog), ctypes.sizeof(self.prog)),
+                            dtype=np.uint8)
+        self.d_prog = torch.from_numpy(raw.copy()).to(self.d_prog.device)
+        self.handle = nat.compile_program(self.prog) if nat.jit_enabled() else None
+
     groups = None
 
     fold = None
@@ -1729,6 +1740,7 @@ MODE_STREAM_W2 = 32  # include/cubed_amd.h CUBED_MODE_STREAM_W2
 MODE_STREAM_W4 = 64  # include/cubed_amd.h CUBED_MODE_STREAM_W4
 MODE_HOST_COUNT = 128  # include/cubed_amd.h CUBED_MODE_HOST_COUNT
 MODE_STREAM_EVEN = 256  # include/cubed_amd.h CUBED_MODE_STREAM_EVEN
+MODE_OWNER_MAJOR = 512  # include/cubed_amd.h CUBED_MODE_OWNER_MAJOR
 # The balanced split keeps all 256 CUs streaming where the uniform split of
 # 49 column blocks x 5 leaves 11 idle, but measured 4-8 % SLOWER on every
 # split workload (per-rank share 0.221 vs 0.203 ms, config 1 0.464 vs 0.456,

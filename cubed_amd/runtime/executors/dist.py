@@ -37,6 +37,16 @@ from ..exchange import FetchExchange, RechunkExchange, box_offset
 
 FETCH_ROW = 4096  # bytes per row of a whole-chunk pack copy (one wave moves 4 KiB)
 SCATTER = True  # multi-owner sum reductions combine by reduce-scatter (ScatterCombine); tests flip it
+OWNER_MAJOR = True  # ... with the stream kernel writing the owner-major order itself; tests flip it
+ROP_COUNT = 3  # ir.ROPS["count"], include/cubed_amd.h CUBED_R_COUNT
+OP_CONST = 1  # include/cubed_amd.h CUBED_OP_CONST (r[a] = consts[imm])
+
+
+def consts_used(P):
+    """Const slots a fused program reads (CONST instructions of its prologue
+    and epilogue)."""
+    ins = list(P.insns[:P.ninsns]) + list(P.epi[:max(P.nepi, 0)])
+    return max([i.imm + 1 for i in ins if i.op == OP_CONST], default=0)
 
 
 def _round(n, a):
@@ -221,7 +231,10 @@ class ScatterCombine:
 
     Used when every field sums (SUM_ROPS), the plain COUNT fields' global
     values are known on the host (geometry: the same on every rank) and the
-    summed fields are one contiguous run of one accumulator dtype."""
+    summed fields are one contiguous run of one accumulator dtype.  When the
+    partials come from a streaming program with ONE summed field and the
+    owners are block-cyclic, the stream kernel writes the owner-major order
+    itself (``use_direct``, CUBED_MODE_OWNER_MAJOR) and the permute goes."""
 
     def __init__(self, ctx, fused, rows, group_owner, nf, mko, f0, f1, acc_int, host_counts, discard, src):
         import dataclasses
@@ -272,10 +285,42 @@ class ScatterCombine:
             return None
         return red[0], red[-1] + 1
 
+    def direct_ok(self, fused, owners, n):
+        """True when the partials kernel can write the owner-major order
+        itself (CUBED_MODE_OWNER_MAJOR): a streaming partials program with ONE
+        summed field (every COUNT host-filled), block-cyclic group owners (g
+        mod W, so a group's slot is g // W), three free const slots and the
+        W x L x mko slots inside the SoA block (nf x n words)."""
+        from ...lowering import MODE_HOST_COUNT, MODE_PARTIALS, MODE_STREAM
+
+        P, W = fused.prog, self.ctx.world
+        need = MODE_STREAM | MODE_PARTIALS | MODE_HOST_COUNT
+        return (P.mode & need) == need and self.f1 - self.f0 == 1 and \
+            sum(P.field_rop[f] != ROP_COUNT for f in range(P.nfields)) == 1 and \
+            all(o == g % W for g, o in enumerate(owners)) and \
+            consts_used(P) <= nat.MAX_CONSTS - 3 and W * self.L * self.mko <= self.nf * n
+
+    def use_direct(self, fused, gsoa):
+        """The stream kernel writes field f0's partials owner-major into the
+        start of its SoA block (``gsoa``): that block is the reduce-scatter's
+        input and the box-copy permute goes."""
+        from ...lowering import MODE_OWNER_MAJOR
+
+        P, W = fused.prog, self.ctx.world
+        P.mode |= MODE_OWNER_MAJOR
+        P.consts[nat.MAX_CONSTS - 3].i = self.mko
+        P.consts[nat.MAX_CONSTS - 2].i = W
+        P.consts[nat.MAX_CONSTS - 1].i = self.L
+        fused.reprogram()
+        self.perm = gsoa[: W * self.L * self.mko * 8].view(self.perm.dtype)
+        self.perm.zero_()  # padding slots (groups >= G) are never written
+        self.permute = None
+
     def run(self, stream):
         """The partials at ``src`` ([field][group][kept], 8-B words) to every
         rank's owned blocks, then the finish."""
-        self.permute.run(stream)
+        if self.permute is not None:
+            self.permute.run(stream)
         self.ctx.comm.reduce_scatter_sum(self.fin_red, self.perm)
         if self.finish_here:
             fused_finish(self.fused, self.table, self.L, self.mko, self.fin, stream)
@@ -366,6 +411,8 @@ class PartialsLaunch:
                 {f: [int(host_count)] * len(group_owner) for f, r in enumerate(rops) if r == "count"},
                 discard, fused.ws.data_ptr())
             self.finish_here = self.scatter.finish_here
+            if OWNER_MAJOR and self.scatter.direct_ok(fused, group_owner, fused.ntasks * fused.max_kept):
+                self.scatter.use_direct(fused, fused.ws)
         if self.sum_only and self.scatter is None:
             mk = fused.max_kept
             self.sum_views = [(self.field_view(f), BlockCount(self.field_view(f), mk, ctx.device)
@@ -519,6 +566,8 @@ class DistPiecesLaunch:
                 {f: list(group_counts) for f, r in enumerate(rops) if r == "count"}, discard,
                 self.gsoa.data_ptr())
             self.finish_here = self.scatter.finish_here
+            if OWNER_MAJOR and soa_direct and self.scatter.direct_ok(fused, owners, self.n):
+                self.scatter.use_direct(fused, self.gsoa)
         if self.sum_only and self.scatter is None:
             mk = self.mko
             self.sum_views = [(self.field_view(f), BlockCount(self.field_view(f), mk, ctx.device)

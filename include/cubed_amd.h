@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CUBED_ABI_VERSION 15
+#define CUBED_ABI_VERSION 16
 
 #define CUBED_MAX_DIMS 6   /* iteration dims of one task after coalescing   */
 #define CUBED_MAX_LEAVES 4 /* array/philox/const-array inputs of a program  */
@@ -63,6 +63,12 @@ extern "C" {
 #define CUBED_MODE_STREAM_W4 64
 #define CUBED_MODE_HOST_COUNT 128 /* partials: COUNT fields are left to the host */
 #define CUBED_MODE_STREAM_EVEN 256 /* stream: every task the same reduced extent */
+/* stream + partials, multi-GPU reduce-scatter (ABI 16): the ONE stored field's
+ * partial of SoA element i (group g = i / mko) is written to owner-major slot
+ * ((g % W) * L + g / W) * mko + i % mko of the SoA region, with mko, W, L in
+ * consts[CUBED_MAX_CONSTS - 3 .. - 1] (host-checked: block-cyclic owners, one
+ * summed field, every other field host-counted) */
+#define CUBED_MODE_OWNER_MAJOR 512
 
 #define CUBED_E_ARG (-1)
 #define CUBED_E_DTYPE (-2)
@@ -177,6 +183,8 @@ typedef struct {
                                  /* mode leaves plain COUNT fields unwritten*/
                                  /* in the SoA block -- the host fills them */
                                  /* with the (geometry-known) global count  */
+                                 /* +256 (CUBED_MODE_STREAM_EVEN), +512     */
+                                 /* (CUBED_MODE_OWNER_MAJOR): see above     */
   int32_t nleaves;
   uint8_t leaf_kind[CUBED_MAX_LEAVES];
   uint8_t leaf_dtype[CUBED_MAX_LEAVES];

@@ -12,6 +12,8 @@ import cubed_amd as cubed
 import cubed_amd.array_api as xp
 import cubed_amd.random as crandom
 from cubed_amd.core.plan import arrays_to_plan
+import cubed_amd._native as nat
+import cubed_amd.lowering as Lw
 from cubed_amd.lowering import MODE_PARTIALS, MODE_STREAM, FusedLaunch
 from cubed_amd.runtime.executors.dist import (
     DistPiecesLaunch,
@@ -272,6 +274,8 @@ def test_scatter_owners_are_per_group_when_pieces_cut_a_kept_dim(built):
         assert dp.ngroups > nkeys  # pieces cut the kept dim
         sc = dp.scatter
         assert sc is not None and sc.G == dp.ngroups
+        # several groups per key (owners are not g mod W): the box-copy permute stays
+        assert sc.permute is not None and not dp.fused.prog.mode & Lw.MODE_OWNER_MAJOR
         # each group's owner is its key's owner, and the groups of one key are
         # consecutive: owner-major slots of this rank = its keys' groups
         tbl = sc.dst.view(sc.f1 - sc.f0, sc.G)[0].tolist()
@@ -303,9 +307,38 @@ def test_rechunk_mean_combines_by_reduce_scatter(built):
         assert sc is not None and sc.L == 13 and sc.mine == [g for g in range(50) if g % world == rank]
         assert (sc.f0, sc.f1) == (1, 2)  # n is host-filled; only the totals cross the ranks
         assert sc.perm.numel() == world * 13 * 10
+        # 10-wide blocks are no streaming program: the box-copy permute stays
+        assert sc.permute is not None and not dp.fused.prog.mode & Lw.MODE_OWNER_MAJOR
         cnt = sc.fin.view(torch.int64)[:13 * 10].view(13, 10)
         k = len(sc.mine)  # the counts of this rank's blocks, then padding slots
         assert (cnt[:k] == 500).all() and (cnt[k:] == 1).all()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_stream_partials_write_owner_major(built, world):
+    """A streaming partials program with one summed field and block-cyclic
+    owners writes its SoA partials straight into the reduce-scatter's
+    owner-major order (CUBED_MODE_OWNER_MAJOR; mko, W, L in the last three
+    const slots): no box-copy permute, the reduce-scatter reads the SoA block."""
+    x = np.ones((500, 512), dtype=np.float32)
+    for rank in range(world):
+        dry = DryExecutor(FakeComm(rank, world))
+        spec = cubed.Spec(allowed_mem="288GB", executor=dry)
+        a = cubed.from_array(x, chunks=(10, 512), spec=spec)
+        arrays_to_plan(a).execute(executor=dry, array_names=[a.name])
+        dry.launched.clear()
+        m = xp.mean(a.rechunk((500, 16)), axis=0)
+        arrays_to_plan(m).execute(executor=dry, resume=True, array_names=[m.name])
+        (dp,) = [l for l in dry.launched if isinstance(l, DistPiecesLaunch)]
+        sc, P = dp.scatter, dp.fused.prog
+        L = -(-32 // world)
+        assert dp.soa_direct and sc.L == L and sc.mine == [g for g in range(32) if g % world == rank]
+        assert sc.permute is None and P.mode & Lw.MODE_OWNER_MAJOR and P.mode & MODE_STREAM
+        assert [P.consts[nat.MAX_CONSTS - i].i for i in (3, 2, 1)] == [16, world, L]
+        assert sc.perm.data_ptr() == dp.gsoa.data_ptr() and sc.perm.numel() == world * L * 16
+        # the JIT module was rebuilt for the changed program
+        if dp.fused.handle is not None:
+            assert "cubed_stream" in nat.program_source(dp.fused.handle)
 
 
 # ------------------------------------------------ multi-GPU matmul (packed A image)
