@@ -75,12 +75,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblk) {
 // one row group (its A panels read by all eight together); the last < 256
 // tiles as contiguous shares.
 template <bool RR_TAIL = true>
-__device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t per_group, int64_t full_groups) {
-  const int64_t main = (full_groups >> 3) * per_group;
-  const int64_t x = b & 7, i = b >> 3;
-  if (nblk < 8 || main == 0) return xcd_remap(b, nblk);
-  if (i < main) return (x + 8 * (i / per_group)) * per_group + i % per_group;
-  int64_t S = nblk - 8 * main, j = i - main, base = 8 * main;
+__device__ __forceinline__ int64_t xcd_tail(int64_t x, int64_t j, int64_t S, int64_t base) {
   if constexpr (RR_TAIL) {
     const int64_t runs = (S >> 8) << 8 >> 5;  // whole rounds of 8 runs of 32
     if (j < runs * 4) return base + ((j >> 5) * 8 + x) * 32 + (j & 31);
@@ -90,6 +85,36 @@ __device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t
   }
   const int64_t q = S >> 3, r = S & 7;
   return base + (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + j;
+}
+
+template <bool RR_TAIL = true>
+__device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t per_group, int64_t full_groups) {
+  const int64_t main = (full_groups >> 3) * per_group;
+  const int64_t x = b & 7, i = b >> 3;
+  if (nblk < 8 || main == 0) return xcd_remap(b, nblk);
+  if (i < main) return (x + 8 * (i / per_group)) * per_group + i % per_group;
+  return xcd_tail<RR_TAIL>(x, i - main, nblk - 8 * main, 8 * main);
+}
+
+// (probe) 4 x 2 XCDs per super-group of 16 tile rows: XCD x on row group
+// 4R + (x & 3) and column half x >> 2 (the halves' widths alternate between
+// the two super-groups of a pair, so every XCD gets 4 TN tiles per pair);
+// per round the eight XCDs read 16 A and 16 B^T panels (xcd_lockstep: 32 +
+// 8).  GM = 4 only; the rest as xcd_lockstep's tail.
+__device__ __forceinline__ int64_t xcd_quad(int64_t b, int64_t nblk, int64_t TM, int64_t TN) {
+  const int64_t P = (TM / 16) / 2, main = P * 4 * TN;
+  const int64_t x = b & 7, i = b >> 3;
+  if (nblk < 8 || main == 0 || TN < 2) return xcd_remap(b, nblk);
+  if (i >= main) return xcd_tail(x, i - main, nblk - 8 * main, 8 * main);
+  const int64_t h = (TN + 1) / 2, bb = x >> 2, p = i / (4 * TN);
+  int64_t j = i - p * 4 * TN, R = 2 * p, w = bb == 0 ? h : TN - h;
+  if (j >= 4 * w) {
+    j -= 4 * w;
+    R += 1;
+    w = TN - w;
+  }
+  const int64_t col0 = bb == 0 ? 0 : TN - w;
+  return (4 * R + (x & 3)) * 4 * TN + (col0 + (j >> 2)) * 4 + (j & 3);
 }
 
 // tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked
