@@ -50,7 +50,9 @@ constexpr int E8_NSLOT = 10, E8_HALF = 16384, E8_LEAD = 7;
 // every half-tile staged from K tile 0's addresses (L2-resident fills), 32 =
 // no fragment reads in the K loop.  64 = the round-5 tile order (xcd_remap:
 // each XCD a contiguous range of the grouped order) instead of xcd_lockstep;
-// 128 = xcd_lockstep without the round-robin tail; 256 = xcd_quad (GM 4).
+// 128 = xcd_lockstep without the round-robin tail.  (A 4 x 2 arrangement of
+// the XCDs, 16 A + 16 B^T panels per round, ran 88.5-88.8 ms against 87.7-88.1:
+// commit "Probe: 4 x 2 XCD tile arrangement", profiles/r06_gemm_tile_order.log.)
 template <bool OUT_BF16, bool STAMP = false, int VAR = 0, int GM = 4>
 __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_t* __restrict__ tasks,
                                                       const char* __restrict__ PA, const char* __restrict__ PB,
@@ -59,8 +61,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
   __shared__ __attribute__((aligned(1024))) char lds_[E8_NSLOT * E8_HALF];
   CUBED_L char* lds = (CUBED_L char*)lds_;
   int64_t t0, m0, n0;
-  const int64_t lt = (VAR & 256)   ? xcd_quad(blockIdx.x, gridDim.x, pp.TM, pp.TN)
-                     : (VAR & 64)  ? xcd_remap(blockIdx.x, gridDim.x)
+  const int64_t lt = (VAR & 64)    ? xcd_remap(blockIdx.x, gridDim.x)
                      : (VAR & 128) ? xcd_lockstep<false>(blockIdx.x, gridDim.x, GM * pp.TN, pp.TM / GM)
                                    : xcd_lockstep(blockIdx.x, gridDim.x, GM * pp.TN, pp.TM / GM);
   tile_of<HB_BM, HB_BN, GM>(lt, pp.TM, pp.TN, t0, m0, n0);

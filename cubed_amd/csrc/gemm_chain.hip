@@ -96,27 +96,6 @@ __device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t
   return xcd_tail<RR_TAIL>(x, i - main, nblk - 8 * main, 8 * main);
 }
 
-// (probe) 4 x 2 XCDs per super-group of 16 tile rows: XCD x on row group
-// 4R + (x & 3) and column half x >> 2 (the halves' widths alternate between
-// the two super-groups of a pair, so every XCD gets 4 TN tiles per pair);
-// per round the eight XCDs read 16 A and 16 B^T panels (xcd_lockstep: 32 +
-// 8).  GM = 4 only; the rest as xcd_lockstep's tail.
-__device__ __forceinline__ int64_t xcd_quad(int64_t b, int64_t nblk, int64_t TM, int64_t TN) {
-  const int64_t P = (TM / 16) / 2, main = P * 4 * TN;
-  const int64_t x = b & 7, i = b >> 3;
-  if (nblk < 8 || main == 0 || TN < 2) return xcd_remap(b, nblk);
-  if (i >= main) return xcd_tail(x, i - main, nblk - 8 * main, 8 * main);
-  const int64_t h = (TN + 1) / 2, bb = x >> 2, p = i / (4 * TN);
-  int64_t j = i - p * 4 * TN, R = 2 * p, w = bb == 0 ? h : TN - h;
-  if (j >= 4 * w) {
-    j -= 4 * w;
-    R += 1;
-    w = TN - w;
-  }
-  const int64_t col0 = bb == 0 ? 0 : TN - w;
-  return (4 * R + (x & 3)) * 4 * TN + (col0 + (j >> 2)) * 4 + (j & 3);
-}
-
 // tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked
 // column by column, so the workgroups resident on one XCD share A row panels
 // and B column panels in its L2.

@@ -288,13 +288,7 @@ int main(int argc, char** argv) {
     return 0;
   }
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
-  if (arms == 6) {  // 4 x 2 XCD arrangement vs the library's lockstep
-    ARM("8p xcd_quad (4 x 2 XCDs)", 256, 4);
-    run("8p  (library: xcd_lockstep)", e8, 512, false, 16, false);
-    ARM("8p xcd_quad (4 x 2 XCDs)", 256, 4);
-    run("8p  (library: xcd_lockstep)", e8, 512, false, 16, false);
-    ARM("8p xcd_quad (4 x 2 XCDs)", 256, 4);
-  } else if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
+  if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
     ARM("8p lockstep, contiguous tail", 128, 4);
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
