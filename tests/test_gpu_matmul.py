@@ -384,7 +384,7 @@ def test_packed_abi_accumulate(gpu_executor, in_dt, out_dt):
     ((256, 1000), (1000, 256), (256, 1000), (1000, 256)),   # one output chunk (ti = tj = 1)
     ((777, 3000), (3000, 600), (259, 600), (600, 296)),     # ragged everywhere, tiles straddle chunks
     # 47 x 20 tiles: xcd_lockstep's lockstep groups, its round-robin 32-tile runs and contiguous rest
-    ((12000, 256), (256, 5000), (3000, 128), (128, 2500)),
+    ((12000, 256), (256, 5120), (3000, 128), (128, 2560)),
 ])
 def test_packed_matches_unpacked_edge_shapes(gpu_executor, dt, shapes, monkeypatch):
     """Packed vs unpacked kernels on edge geometries (a single K step,
