@@ -34,6 +34,7 @@
 #pragma once
 
 constexpr int E8_NSLOT = 10, E8_HALF = 16384, E8_LEAD = 7;
+constexpr int E8_ROUNDS = 512;  // VAR bit: round_wait / round_done around the K loop (counters at stamp_out)
 
 // Measured on config 5 (tools/gemm_8p_probe.hip, profiles/r06_gemm_bf16_8p*.log,
 // every arm bit-identical to w4p): the library form -- each phase's two
@@ -50,7 +51,9 @@ constexpr int E8_NSLOT = 10, E8_HALF = 16384, E8_LEAD = 7;
 // every half-tile staged from K tile 0's addresses (L2-resident fills), 32 =
 // no fragment reads in the K loop.  64 = the round-5 tile order (xcd_remap:
 // each XCD a contiguous range of the grouped order) instead of xcd_lockstep;
-// 128 = xcd_lockstep without the round-robin tail.  (A 4 x 2 arrangement of
+// 128 = xcd_lockstep without the round-robin tail; E8_ROUNDS (512, the
+// 1-GPU library form) = round_wait / round_done around the K loop: 84.3-84.5
+// ms against 85.0-85.2 (profiles/r06_gemm_round_sync.log).  (A 4 x 2 arrangement of
 // the XCDs, 16 A + 16 B^T panels per round, ran 88.5-88.8 ms against 87.7-88.1:
 // commit "Probe: 4 x 2 XCD tile arrangement", profiles/r06_gemm_tile_order.log.)
 template <bool OUT_BF16, bool STAMP = false, int VAR = 0, int GM = 4>
@@ -66,7 +69,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
                                    : xcd_lockstep(blockIdx.x, gridDim.x, GM * pp.TN, pp.TM / GM);
   tile_of<HB_BM, HB_BN, GM>(lt, pp.TM, pp.TN, t0, m0, n0);
   const int64_t M = pp.M, N = pp.N;
-  if (t0 != 0 || m0 >= M || n0 >= N) return;
+  unsigned* const rctr = (VAR & E8_ROUNDS) ? (unsigned*)stamp_out : nullptr;
+  if (t0 != 0 || m0 >= M || n0 >= N) {
+    if constexpr ((VAR & E8_ROUNDS) != 0) round_done(rctr, blockIdx.x);
+    return;
+  }
+  if constexpr ((VAR & E8_ROUNDS) != 0) round_wait(rctr, blockIdx.x, 32);
   const int ktl = (int)pp.KTL, nph = 4 * ktl;
   // the last K tile holds <= 32 live k: its second 32-k half is not
   // multiplied (w4p's K loop stops at ceil(K / 32) steps too)
@@ -216,6 +224,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
   else
     ktile(ktl - 1, std::false_type{});
   if (g == 0) barrier();  // the same barrier count in both groups
+  if constexpr ((VAR & E8_ROUNDS) != 0) round_done(rctr, blockIdx.x);
   if constexpr (STAMP) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1)::"memory");
     if (lane == 0) {

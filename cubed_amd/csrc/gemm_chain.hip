@@ -96,6 +96,30 @@ __device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t
   return xcd_tail<RR_TAIL>(x, i - main, nblk - 8 * main, 8 * main);
 }
 
+// Tile-round alignment (the 1-GPU packed bf16 GEMM): the i-th workgroup on an XCD (b & 7, local
+// index b >> 3) waits -- one lane polling, bounded -- until the XCD's tiles
+// of earlier rounds of R (one per CU) have left their K loops, so a round's
+// tiles start their K walks together and share panel lines in L2; a timeout
+// only costs the alignment.  ctr: one uint32 per XCD, 128 B apart, zeroed
+// before the launch.
+__device__ __forceinline__ void round_wait(unsigned* ctr, int64_t b, int64_t R) {
+  const int64_t i = b >> 3;
+  if (i >= R) {
+    if (threadIdx.x == 0) {
+      const unsigned need = (unsigned)((i / R) * R);
+      for (int it = 0; it < 20000; ++it) {
+        if (__hip_atomic_load(ctr + (b & 7) * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+    __syncthreads();
+  }
+}
+__device__ __forceinline__ void round_done(unsigned* ctr, int64_t b) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr + (b & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int64_t PACK_CTR_BYTES = 8 * 128;  // round_wait counters: one per XCD, 128 B apart
+
 // tile -> (task, m0, n0): tasks outermost, then groups of GM tile rows walked
 // column by column, so the workgroups resident on one XCD share A row panels
 // and B column panels in its L2.
@@ -1356,7 +1380,8 @@ extern "C" int64_t cubed_gemm_pack_bytes(const cubed_gemm_chain_t* tasks, int64_
   PackPlan pp;
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
-  return (pp.TM + pp.TN) * pp.pstride;
+  // the two images, then the bf16 GEMM's per-XCD round counters (round_wait)
+  return (pp.TM + pp.TN) * pp.pstride + PACK_CTR_BYTES;
 }
 
 extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cubed_gemm_chain_t* d_tasks,
@@ -1368,7 +1393,7 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
   GemmGrid gg;
   if (int rc = pack_plan(tasks, ti, tj, segs, nsegs, in_dtype, out_dtype, pp, gg)) return rc;
   const int64_t bytesA = pp.TM * pp.pstride, bytesB = pp.TN * pp.pstride;
-  if (!d_ws || ws_bytes < bytesA + bytesB || ((uintptr_t)d_ws & 255)) {
+  if (!d_ws || ws_bytes < bytesA + bytesB + PACK_CTR_BYTES || ((uintptr_t)d_ws & 255)) {
     snprintf(g_err, sizeof(g_err), "cubed_gemm_chain_packed: the workspace is missing, short or not 256-B aligned");
     return CUBED_E_WORKSPACE;
   }
@@ -1387,13 +1412,17 @@ extern "C" int cubed_gemm_chain_packed(const cubed_gemm_chain_t* tasks, const cu
     hipLaunchKernelGGL(k_pack_a, ga, dim3(256), 0, st, d_tasks, d_segs, pp, PA);
     hipLaunchKernelGGL(k_pack_bt, gb, dim3(256), 0, st, d_tasks, d_segs, pp, PB);
     // two waves per SIMD on the packed image (gemm_bf16_8p.h; round 6:
-    // 1410-1424 TF against the one-wave w4p kernel's 1301-1317, bit-identical)
+    // 1410-1424 TF against the one-wave w4p kernel's 1301-1317, bit-identical),
+    // each XCD's rounds of tiles aligned on counters zeroed here (E8_ROUNDS)
+    unsigned long long* ctr = (unsigned long long*)(PB + bytesB);
+    hipError_t me = hipMemsetAsync(ctr, 0, PACK_CTR_BYTES, st);
+    if (me != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(me)); return (int)me; }
     if (out_dtype == CUBED_BF16)
-      hipLaunchKernelGGL((k_gemm_bf16_8p<true>), grid, dim3(512), 0, st, d_tasks, (const char*)PA, (const char*)PB,
-                         pp, gg, nullptr);
+      hipLaunchKernelGGL((k_gemm_bf16_8p<true, false, E8_ROUNDS>), grid, dim3(512), 0, st, d_tasks, (const char*)PA,
+                         (const char*)PB, pp, gg, ctr);
     else
-      hipLaunchKernelGGL((k_gemm_bf16_8p<false>), grid, dim3(512), 0, st, d_tasks, (const char*)PA, (const char*)PB,
-                         pp, gg, nullptr);
+      hipLaunchKernelGGL((k_gemm_bf16_8p<false, false, E8_ROUNDS>), grid, dim3(512), 0, st, d_tasks, (const char*)PA,
+                         (const char*)PB, pp, gg, ctr);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) { snprintf(g_err, sizeof(g_err), "%s", hipGetErrorString(e)); return (int)e; }

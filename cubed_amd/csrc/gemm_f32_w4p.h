@@ -95,7 +95,8 @@ __global__ __launch_bounds__(256) void k_pack_b_f32(const cubed_gemm_chain_t* __
 // barrier).  The wait before step p's barrier leaves steps p + 2 and p + 3's
 // 16 pieces in flight.  STAMP: per-wave main-loop cycles (probe builds only).
 // LOCK: tile order xcd_lockstep (probe: false = xcd_remap's contiguous ranges).
-template <bool STAMP = false, bool LOCK = true>
+// SYNC (probe): round_wait / round_done around the K loop, counters at stamp_out.
+template <bool STAMP = false, bool LOCK = true, bool SYNC = false>
 __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_t* __restrict__ tasks,
                                                       const char* __restrict__ PA, const char* __restrict__ PB,
                                                       PackPlan pp, GemmGrid gg,
@@ -107,7 +108,12 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_
   const int64_t lt = LOCK ? xcd_lockstep(blockIdx.x, gridDim.x, 4 * pp.TN, pp.TM / 4) : xcd_remap(blockIdx.x, gridDim.x);
   tile_of<HF_BM, HF_BN, 4>(lt, pp.TM, pp.TN, t, m0, n0);
   const int64_t M = pp.M, N = pp.N;
-  if (t != 0 || m0 >= M || n0 >= N) return;
+  unsigned* const rctr = SYNC ? (unsigned*)stamp_out : nullptr;
+  if (t != 0 || m0 >= M || n0 >= N) {
+    if constexpr (SYNC) round_done(rctr, blockIdx.x);
+    return;
+  }
+  if constexpr (SYNC) round_wait(rctr, blockIdx.x, 32);
   const int64_t nst = pp.KTL;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -246,6 +252,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_f32_w4p(const cubed_gemm_chain_
     f0 = f1;
   }
 #undef WPF_PIECE
+  if constexpr (SYNC) round_done(rctr, blockIdx.x);
 
   // epilogue: accumulator (rb, q) register r = row wm + 32 rb + (r&3) +
   // 8 (r>>2) + 4h, column wn + 4 r32 + q: one float4 per (rb, r)

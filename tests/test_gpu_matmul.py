@@ -352,7 +352,7 @@ def test_packed_abi_accumulate(gpu_executor, in_dt, out_dt):
     d_t2 = torch.from_numpy(tasks.view(np.uint8).copy()).to(dev)
     d_s2 = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
     nbytes = Lb.cubed_gemm_pack_bytes(tasks.ctypes.data, ti, tj, segs.ctypes.data, len(segs), bf, f32)
-    assert nbytes == ((3 + 2) * 18 * 32768 if in_dt == "bf16" else (3 + 2) * 72 * 16384)
+    assert nbytes == ((3 + 2) * 18 * 32768 if in_dt == "bf16" else (3 + 2) * 72 * 16384) + 8 * 128  # + round counters
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     assert ws.data_ptr() % 256 == 0
     rc = Lb.cubed_gemm_chain_packed(tasks.ctypes.data, d_t2.data_ptr(), ti, tj, segs.ctypes.data, d_s2.data_ptr(),

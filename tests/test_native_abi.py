@@ -183,6 +183,9 @@ def _product_grid(ti, tj, cm, cn, ks, last_m=None, last_n=None):
     return tasks, segs
 
 
+CTR = 8 * 128  # the bf16 GEMM's per-XCD round counters after the two images
+
+
 def test_gemm_pack_bytes(built):
     """cubed_gemm_pack_bytes (host logic): the packed path's workspace is
     (256-row panels over M + 256-column panels over N) x k blocks -- bf16
@@ -196,13 +199,13 @@ def test_gemm_pack_bytes(built):
     bf, f32 = ir.dtype_code(ir.bfloat16), ir.dtype_code(np.float32)
     tasks, segs = _product_grid(8, 8, 5000, 5000, [5000] * 8)  # config 5
     args = (tasks.ctypes.data, 8, 8, segs.ctypes.data, len(segs))
-    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (157 + 157) * 625 * 32768
-    assert L_.cubed_gemm_pack_bytes(*args, bf, f32) == (157 + 157) * 625 * 32768
-    assert L_.cubed_gemm_pack_bytes(*args, f32, f32) == (157 + 157) * 2500 * 16384  # f32: 16-k steps of 16 KiB
+    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (157 + 157) * 625 * 32768 + CTR  # + round counters
+    assert L_.cubed_gemm_pack_bytes(*args, bf, f32) == (157 + 157) * 625 * 32768 + CTR
+    assert L_.cubed_gemm_pack_bytes(*args, f32, f32) == (157 + 157) * 2500 * 16384 + CTR  # f32: 16-k steps of 16 KiB
     assert L_.cubed_gemm_pack_bytes(*args, ir.dtype_code(np.float64), ir.dtype_code(np.float64)) < 0
     tasks, segs = _product_grid(3, 2, 300, 256, [520, 520, 104], last_m=100, last_n=136)
     args = (tasks.ctypes.data, 3, 2, segs.ctypes.data, len(segs))
-    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (3 + 2) * 18 * 32768  # M 700, N 392, K 1144
+    assert L_.cubed_gemm_pack_bytes(*args, bf, bf) == (3 + 2) * 18 * 32768 + CTR  # M 700, N 392, K 1144
     segs["a"][len(segs) - 1] += 4096  # task (2, 1) reads another A chunk than (2, 0)
     assert L_.cubed_gemm_pack_bytes(*args, bf, bf) < 0
     assert b"not one chunked product" in L_.cubed_last_error()

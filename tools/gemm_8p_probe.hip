@@ -86,7 +86,7 @@ int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 3;
   const int64_t N = argc > 2 ? atoll(argv[2]) : 40000, Cc = 5000, nb = N / Cc;
   const bool obf = argc > 3 && atoi(argv[3]) == 1;
-  const bool f32in = argc > 4 && atoi(argv[4]) == 3;
+  const bool f32in = argc > 4 && (atoi(argv[4]) == 3 || atoi(argv[4]) == 8);
   const int32_t in_code = f32in ? CUBED_F32 : CUBED_BF16;
   const int64_t al = 32;  // the executor's slot alignment (storage.SLOT_ALIGN)
   const int64_t slot_in = (Cc * Cc * (f32in ? 4 : 2) + al - 1) / al * al;
@@ -147,12 +147,17 @@ int main(int argc, char** argv) {
   unsigned long long* st;
   CHECK(hipMalloc(&st, (size_t)grid.x * 8 * 2 * 8));
   typedef void (*kfn)(const cubed_gemm_chain_t*, const char*, const char*, PackPlan, GemmGrid, unsigned long long*);
+  unsigned* rctr;
+  CHECK(hipMalloc(&rctr, 8 * 128));
+  bool sync = false;  // pass the round counters (zeroed per launch) instead of stamps
   auto run = [&](const char* name, kfn f, int threads, bool stamp, int mfma_cyc, bool check) {
     float best = 1e30f;
     for (int r = 0; r < reps + 1; ++r) {
       CHECK(hipMemset(C1, 0, slot_out * nb * nb));
+      CHECK(hipMemset(rctr, 0, 8 * 128));
       CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(f, grid, dim3(threads), 0, 0, dt1, PA, PB, pp, gg, stamp ? st : nullptr);
+      hipLaunchKernelGGL(f, grid, dim3(threads), 0, 0, dt1, PA, PB, pp, gg,
+                         sync ? (unsigned long long*)rctr : stamp ? st : nullptr);
       CHECK(hipGetLastError());
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
@@ -195,6 +200,17 @@ int main(int argc, char** argv) {
   const int arms = argc > 4 ? atoi(argv[4]) : 0;
   if (f32in) {  // f32 inputs: the library's one-wave w4p kernel (the two-wave f32 form,
     // gemm_f32_8p.h, lost: 943-959 ms vs 876; commit e0bc44c, profiles/r06_gemm_f32_8p.log)
+    if (arms == 8) {  // tile rounds aligned per XCD (round_wait / round_done)
+      run("f32 w4p (library)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
+      sync = true;
+      run("f32 w4p rounds aligned", (kfn)k_gemm_f32_w4p<false, true, true>, 256, false, 32, true);
+      sync = false;
+      run("f32 w4p (library)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, false);
+      sync = true;
+      run("f32 w4p rounds aligned", (kfn)k_gemm_f32_w4p<false, true, true>, 256, false, 32, false);
+      sync = false;
+      return 0;
+    }
     run("f32 w4p (lockstep XCD order)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, true);
     run("f32 w4p (contiguous XCD ranges)", (kfn)k_gemm_f32_w4p<false, false>, 256, false, 32, true);
     run("f32 w4p (lockstep XCD order)", (kfn)k_gemm_f32_w4p<false>, 256, false, 32, false);
@@ -288,6 +304,17 @@ int main(int argc, char** argv) {
     return 0;
   }
 #define ARM(NAME, V, G) run(NAME, obf ? (kfn)k_gemm_bf16_8p<true, false, V, G> : (kfn)k_gemm_bf16_8p<false, false, V, G>, 512, false, 16, true)
+  if (arms == 7) {  // tile rounds aligned per XCD (round_wait / round_done)
+    sync = true;
+    ARM("8p rounds aligned", 512, 4);
+    sync = false;
+    run("8p  (library)", e8, 512, false, 16, false);
+    sync = true;
+    ARM("8p rounds aligned", 512, 4);
+    sync = false;
+    run("8p  (library)", e8, 512, false, 16, false);
+    return 0;
+  }
   if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
     ARM("8p lockstep, contiguous tail", 128, 4);
