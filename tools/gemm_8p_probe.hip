@@ -30,9 +30,11 @@ __global__ void k_fill(uint16_t* p, int64_t n, uint32_t seed) {
 
 // pack A with all 8 rows' loads of a block issued before its stores (the
 // library form unrolls by 2)
+template <bool NTL = true, bool NTS = false>
 __global__ __launch_bounds__(256) void k_pack_a8(const cubed_gemm_chain_t* __restrict__ tasks,
                                                  const cubed_gemm_seg_t* __restrict__ segs, PackPlan pp,
                                                  char* __restrict__ PA) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const int64_t nkt = pp.kt1 - pp.kt0, nblk = pp.TM * nkt;
   const cubed_gemm_seg_t* __restrict__ sg0 = segs + tasks[0].seg0;
   const int sl = threadIdx.x & 7;
@@ -54,15 +56,20 @@ __global__ __launch_bounds__(256) void k_pack_a8(const cubed_gemm_chain_t* __res
         const bool hi = gm >= mb;
         const int64_t I = hi ? I0 + 1 : I0, lm = gm - I * pp.cm;
         const cubed_gemm_seg_t& S = segs[tasks[I * pp.tj].seg0 + s];
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 x = __builtin_nontemporal_load((const u32x4*)((const char*)(uintptr_t)S.a + (lm * S.lda + (k - ks)) * 2));
+        const u32x4* src = (const u32x4*)((const char*)(uintptr_t)S.a + (lm * S.lda + (k - ks)) * 2);
+        const u32x4 x = NTL ? __builtin_nontemporal_load(src) : *src;
         v[j] = uint4{x.x, x.y, x.z, x.w};
       }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int r = (threadIdx.x >> 3) + 32 * j;
-      *(uint4*)(dst + r * 128 + sl * 16) = v[j];
+      if constexpr (NTS) {
+        const u32x4 x = {v[j].x, v[j].y, v[j].z, v[j].w};
+        __builtin_nontemporal_store(x, (u32x4*)(dst + r * 128 + sl * 16));
+      } else {
+        *(uint4*)(dst + r * 128 + sl * 16) = v[j];
+      }
     }
   }
 }
@@ -240,15 +247,26 @@ int main(int argc, char** argv) {
     }
     char* PA2;
     CHECK(hipMalloc(&PA2, pp.TM * pp.pstride));
-    for (int r = 0; r < 3; ++r) {
-      float ma;
-      CHECK(hipEventRecord(e0));
-      hipLaunchKernelGGL(k_pack_a8, ga, dim3(256), 0, 0, dt0, ds, pp, PA2);
-      CHECK(hipEventRecord(e1));
-      CHECK(hipEventSynchronize(e1));
-      CHECK(hipEventElapsedTime(&ma, e0, e1));
-      printf("pack A, 8 loads in flight (nt) %.3f ms (%.0f GB/s moved)\n", ma, 2.0 * pp.TM * pp.pstride / ma / 1e6);
-    }
+    typedef void (*pfn)(const cubed_gemm_chain_t*, const cubed_gemm_seg_t*, PackPlan, char*);
+    const struct { const char* name; pfn f; int grid; } pv[] = {
+        {"pack A, 8 loads in flight (nt loads)", k_pack_a8<true, false>, 16384},
+        {"pack A, 8 loads in flight (plain)", k_pack_a8<false, false>, 16384},
+        {"pack A, 8 loads in flight (plain, nt stores)", k_pack_a8<false, true>, 16384},
+        {"pack A, 8 loads in flight (plain), grid 4096", k_pack_a8<false, false>, 4096},
+        {"pack A, library, grid 4096", k_pack_a, 4096},
+        {"pack A, library, grid 65536", k_pack_a, 65536},
+    };
+    for (const auto& v : pv)
+      for (int r = 0; r < 3; ++r) {
+        float ma;
+        const dim3 g((unsigned)(na < v.grid ? na : v.grid));
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL(v.f, g, dim3(256), 0, 0, dt0, ds, pp, PA2);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        CHECK(hipEventElapsedTime(&ma, e0, e1));
+        printf("%-48s %.3f ms (%.0f GB/s moved)\n", v.name, ma, 2.0 * pp.TM * pp.pstride / ma / 1e6);
+      }
     CHECK(hipMemset(dcnt, 0, 8));
     k_mismatch<<<4096, 256>>>((const uint32_t*)PAw, (const uint32_t*)PA2, pp.TM * pp.pstride / 4, dcnt);
     unsigned long long c;
