@@ -410,3 +410,34 @@ def test_packed_matches_unpacked_edge_shapes(gpu_executor, dt, shapes, monkeypat
     assert np.array_equal(res[True].view(np.uint32), res[False].view(np.uint32))
     rnd = _bf16_round if dt == "bf16" else (lambda v: v)
     _check_bound(res[True], rnd(x).astype(np.float64), rnd(y).astype(np.float64), sa[1], out_bf16=(dt == "bf16"))
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_matmul_against_the_reference_algorithm(gpu_executor, packed, monkeypatch):
+    """f32 (the reference's dtype) on the packed and the unpacked GEMM against
+    the oracle's restatement of linear_algebra_functions.py:13-78 (f32 chunk
+    products, then the f32 k-chunk sum rounds of _sum_wo_cat).  The two sum
+    the same products in different orders, so each is within 8 sqrt(K)
+    2^-24 sum|a||b| of the exact product and they are within twice that of
+    each other."""
+    from cubed_amd.runtime.executors.gpu import GpuDagExecutor
+    from oracle import cubed_ref as R
+
+    r = np.random.default_rng(77)
+    x = (r.random((1024, 2048)) - 0.5).astype(np.float32)
+    y = (r.random((2048, 768)) - 0.5).astype(np.float32)
+    ca, cb = (512, 512), (512, 384)
+    monkeypatch.setattr(L.GemmLaunch, "PACKED", packed)
+    e = GpuDagExecutor("cuda:0")
+    spec = cubed.Spec(allowed_mem="2GB", executor=e)
+    got = xp.matmul(cubed.from_array(x, chunks=ca, spec=spec), cubed.from_array(y, chunks=cb, spec=spec)).compute()
+    gl = _launches(e)
+    assert (gl[0].packed is not None) == packed
+    ref = R.matmul(x, y, ca, cb)
+    scale = np.abs(x).astype(np.float64) @ np.abs(y).astype(np.float64)
+    bound = 8 * np.sqrt(2048) * 2.0 ** -24 * scale
+    assert got.dtype == ref.dtype == np.float32
+    assert np.all(np.abs(got.astype(np.float64) - ref) <= 2 * bound)
+    exact = x.astype(np.float64) @ y.astype(np.float64)
+    assert np.all(np.abs(got - exact) <= bound) and np.all(np.abs(ref - exact) <= bound)
+

@@ -169,3 +169,29 @@ def test_rechunk_values_unchanged():
     out, plan, ntasks = R.rechunk(x, (10, 50), (60, 10), allowed_mem=100_000)
     assert np.array_equal(out, x)
     assert len(ntasks) in (1, 2)
+
+
+def test_matmul_restatement_pinned_by_reference_case():
+    """The reference's own matmul case (test_array_api.py: a 4x4 int array in
+    2x2 chunks times itself) through the restated blockwise products +
+    _sum_wo_cat rounds."""
+    c = load("reference_cases.json")["matmul"]
+    a = np.asarray(c["a"])
+    got = R.matmul(a, a, tuple(c["chunks"]), tuple(c["chunks"]))
+    assert np.array_equal(got, np.asarray(c["expected"]))
+
+
+def test_matmul_restatement_rounds():
+    """f32 operands with several k chunks: the result is the f32 sum of f32
+    chunk products in k order (one combine round at 2 GB), equal to numpy's
+    own chunked computation, and within the f32 bound of an f64 product."""
+    r = np.random.default_rng(4)
+    x = r.random((70, 90)).astype(np.float32)
+    y = r.random((90, 50)).astype(np.float32)
+    got = R.matmul(x, y, (32, 30), (30, 20))
+    parts = [np.matmul(x[:, k:k + 30], y[k:k + 30]) for k in range(0, 90, 30)]
+    exp = (parts[0] + parts[1]) + parts[2]
+    assert got.dtype == np.float32 and np.array_equal(got, exp)
+    ex64 = x.astype(np.float64) @ y.astype(np.float64)
+    assert np.all(np.abs(got - ex64) <= 90 * 2.0 ** -24 * (np.abs(x).astype(np.float64) @ np.abs(y)))
+
