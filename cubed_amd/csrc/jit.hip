@@ -37,6 +37,7 @@ struct JitKernel {
 
 static std::mutex g_mu;
 static std::unordered_map<std::string, JitKernel*> g_cache;
+static int g_stream_force_unroll = 0;  // cubed_stream_force_unroll() (probes: rows in flight per lane)
 
 static void emit_insns(std::string& out, const cubed_insn_t* ins, int n) {
   char buf[160];
@@ -130,7 +131,14 @@ std::string jit_source(const cubed_program_t& P, const std::string& name) {
   const int kernel = P.mode & 3, vec = (P.mode & 4) ? 4 : 1;
   char buf[512];
   if (P.mode & CUBED_MODE_STREAM) {
-    const int U = stream_unroll(P.vtype == CUBED_V_F32 ? 4 : 8, P.nleaves);
+    // rows in flight per lane: stream_unroll()'s ~128 B per lane, except f64
+    // programs of three or more leaves, where some leaves are usually
+    // broadcast over the reduced rows (loaded once, not per row: vorticity's
+    // x, y) -- 4 rows there, 1 % faster on vorticity than 2 (3: slower, 8:
+    // slower; tools/stream_unroll_probe.py, profiles/r06_stream_unroll.log)
+    const int U = g_stream_force_unroll > 0                 ? g_stream_force_unroll
+                  : P.vtype == CUBED_V_F64 && P.nleaves >= 3 ? 4
+                                                             : stream_unroll(P.vtype == CUBED_V_F32 ? 4 : 8, P.nleaves);
     snprintf(buf, sizeof(buf),
              "extern \"C\" __global__ __launch_bounds__(256) void %s(const cubed_task_t* __restrict__ tasks, "
              "int64_t ntasks, int64_t bpt, int32_t nsplit, cubed::Acc* __restrict__ ws, int64_t max_kept) {\n"
@@ -244,6 +252,7 @@ extern "C" int cubed_fused_compile(const cubed_program_t* prog, const char* incl
   if (!prog || !handle) { set_error("cubed_fused_compile: null argument"); return CUBED_E_ARG; }
   if (int rc = check_program(*prog)) return rc;
   std::string key((const char*)prog, sizeof(*prog));
+  key += std::to_string(g_stream_force_unroll);
   {
     std::lock_guard<std::mutex> g(g_mu);
     auto it = g_cache.find(key);
@@ -421,4 +430,14 @@ extern "C" int cubed_fold_groups_compiled(void* handle, const cubed_program_t* p
   hipError_t e = hipModuleLaunchKernel(ff, grid.x, grid.y, 1, kBlock, 1, 1, 0, st, args, nullptr);
   if (e != hipSuccess) { set_error(hipGetErrorString(e)); return (int)e; }
   return 0;
+}
+
+// Probes only (tools/stream_unroll_probe.py): rows in flight per lane of the
+// JIT streaming kernels compiled from now on (0 = stream_unroll()'s choice);
+// returns the previous value.  Not part of the C ABI header.
+extern "C" int cubed_stream_force_unroll(int u) {
+  std::lock_guard<std::mutex> g(g_mu);
+  const int prev = g_stream_force_unroll;
+  if (u >= 0) g_stream_force_unroll = u;
+  return prev;
 }
