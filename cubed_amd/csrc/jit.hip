@@ -139,11 +139,17 @@ std::string jit_source(const cubed_program_t& P, const std::string& name) {
     const int U = g_stream_force_unroll > 0                 ? g_stream_force_unroll
                   : P.vtype == CUBED_V_F64 && P.nleaves >= 3 ? 4
                                                              : stream_unroll(P.vtype == CUBED_V_F32 ? 4 : 8, P.nleaves);
+    // the unsplit kernel (a grid that fills the chip without splitting the
+    // rows): 2 rows for f32 two-leaf programs -- quad-means 1.184-1.192 ms
+    // against 1.212-1.215 with 4, three plans each in one process
+    // (profiles/r06_stream_unroll.log); the split planner's in-flight
+    // estimate (stream_unroll) does not concern unsplit launches
+    const int Um = g_stream_force_unroll > 0 ? U : P.vtype == CUBED_V_F32 && P.nleaves == 2 ? 2 : U;
     snprintf(buf, sizeof(buf),
              "extern \"C\" __global__ __launch_bounds__(256) void %s(const cubed_task_t* __restrict__ tasks, "
              "int64_t ntasks, int64_t bpt, int32_t nsplit, cubed::Acc* __restrict__ ws, int64_t max_kept) {\n"
              "  cubed::stream_body<%s, %d, %d, %d, false>(JP, tasks, ntasks, bpt, nsplit, ws, max_kept);\n}\n",
-             name.c_str(), V, P.nleaves, U, stream_groups(P));
+             name.c_str(), V, P.nleaves, Um, stream_groups(P));
     s += buf;
     if (P.nfields > 0) {
       // the split variant (nsplit > 1: arrival counters + in-kernel fold)

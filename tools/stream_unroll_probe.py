@@ -1,10 +1,11 @@
 """Development probe (not part of the library): rows in flight per lane of
 the JIT streaming kernels (cubed_stream_force_unroll, jit.hip) on the
-vorticity reduction (configs[3], f64, two streamed + two broadcast leaves)
-and the headline quad-means (f32, two leaves), each U in its own plan, all in
-one process, alternating.
+vorticity reduction (configs[3], f64, two streamed + two broadcast leaves),
+the headline quad-means (f32, two leaves), the 7000-row per-rank share of
+config 3's rechunk + mean (f32, one leaf) and config 1 (f64, one leaf), each
+U in its own plan, all in one process, alternating.
 
-    python tools/stream_unroll_probe.py [rounds]
+    python tools/stream_unroll_probe.py [rounds] [U,U,...]   (0 = the library's choice)
 """
 import os
 import random
@@ -38,28 +39,38 @@ def main():
     y = crandom.random((900, 800), chunks=100, spec=spec)
     u = xp.astype(crandom.random((1000, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
     v = xp.astype(crandom.random((1000, 720, 1440), chunks=(10, 720, 1440), spec=spec), xp.float32)
-    arrays_to_plan(a, b, x, y, u, v).execute(executor=ex, array_names=[a.name, b.name, x.name, y.name, u.name, v.name])
-    vort_bytes = 2 * 999 * 900 * 800 * 8
-    qm_bytes = 2 * 1000 * 720 * 1440 * 4
-    steps = {}
-    for U in (0, 4, 8, 3):
+    spec2 = cubed.Spec(allowed_mem="288GB", executor=ex)
+    s7 = xp.astype(crandom.random((7000, 50000), chunks=(1000, 50000), spec=spec2), xp.float32)
+    c1 = crandom.random((20000, 20000), chunks=(5000, 5000), spec=spec)
+    arrays_to_plan(a, b, x, y, u, v, c1).execute(
+        executor=ex, array_names=[a.name, b.name, x.name, y.name, u.name, v.name, c1.name])
+    arrays_to_plan(s7).execute(executor=ex, array_names=[s7.name])
+    work = {  # name: (bytes, plan builder)
+        "vorticity": (2 * 999 * 900 * 800 * 8, lambda: (xp.mean(a[1:] * x + b[1:] * y), (a, b, x, y))),
+        "quad-means": (2 * 1000 * 720 * 1440 * 4, lambda: (xp.mean(u * v, axis=0), (u, v))),
+        "share-7000": (7000 * 50000 * 4, lambda: (xp.mean(s7.rechunk((7000, 1000)), axis=0), s7)),
+        "config1": (20000 * 20000 * 8, lambda: (xp.mean((c1 + 1) * 2, axis=0), c1)),
+    }
+    us = [int(t) for t in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 4, 8, 16]
+    steps = {}  # (position in the U list, workload): a plan of its own (its own buffers) per entry
+    for ui, U in enumerate(us):
         L.cubed_stream_force_unroll(U)
-        mv = xp.mean(a[1:] * x + b[1:] * y)
-        mq = xp.mean(u * v, axis=0)
-        steps[U] = (bench.step_fn(arrays_to_plan(mv), ex, [mv], (a, b, x, y)),
-                    bench.step_fn(arrays_to_plan(mq), ex, [mq], (u, v)))
-        for s in steps[U]:
-            s()  # lowering + JIT compile with this U
+        for name, (_, build) in work.items():
+            m, keep = build()
+            st = bench.step_fn(arrays_to_plan(m), ex, [m], keep)
+            st()  # lowering + JIT compile with this U
+            steps[(ui, name)] = st
     L.cubed_stream_force_unroll(0)
     for r in range(rounds):
-        for U, (sv, sq) in steps.items():
-            for _ in range(3):
-                sv()
-                sq()
-            dv = bench.timed(sv, 10, 1)
-            dq = bench.timed(sq, 10, 1)
-            print(f"round {r} U {U or 'default'}: vorticity {dv * 1e3:.4f} ms ({vort_bytes / dv / 8e12:.4f} of 8 TB/s)"
-                  f"  quad-means {dq * 1e3:.4f} ms ({qm_bytes / dq / 8e12:.4f})", flush=True)
+        for ui, U in enumerate(us):
+            line = []
+            for name, (nbytes, _) in work.items():
+                st = steps[(ui, name)]
+                for _ in range(3):
+                    st()
+                d = bench.timed(st, 10, 1)
+                line.append(f"{name} {d * 1e3:.4f} ms ({nbytes / d / 8e12:.4f})")
+            print(f"round {r} plan {ui} U {U or 'default'}: " + "  ".join(line), flush=True)
 
 
 if __name__ == "__main__":
