@@ -5,7 +5,7 @@ the headline quad-means (f32, two leaves), the 7000-row per-rank share of
 config 3's rechunk + mean (f32, one leaf) and config 1 (f64, one leaf), each
 U in its own plan, all in one process, alternating.
 
-    python tools/stream_unroll_probe.py [rounds] [U,U,...]   (0 = the library's choice)
+    python tools/stream_unroll_probe.py [rounds] [U[wW],...] [workload,...]   (U 0 = the library's choice)
 """
 import os
 import random
@@ -51,16 +51,25 @@ def main():
         "share-7000": (7000 * 50000 * 4, lambda: (xp.mean(s7.rechunk((7000, 1000)), axis=0), s7)),
         "config1": (20000 * 20000 * 8, lambda: (xp.mean((c1 + 1) * 2, axis=0), c1)),
     }
-    us = [int(t) for t in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 4, 8, 16]
+    # entries "U" or "UwW" (W: kept groups per lane, lowering.FORCE_STREAM_W)
+    us = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "4", "8", "16"]
+    if len(sys.argv) > 3:  # workloads to run (comma list of names)
+        keep_names = sys.argv[3].split(",")
+        work = {k: v for k, v in work.items() if k in keep_names}
+    import cubed_amd.lowering as Lw
+
     steps = {}  # (position in the U list, workload): a plan of its own (its own buffers) per entry
-    for ui, U in enumerate(us):
-        L.cubed_stream_force_unroll(U)
+    for ui, tag in enumerate(us):
+        U, _, W = tag.partition("w")
+        L.cubed_stream_force_unroll(int(U))
+        Lw.FORCE_STREAM_W = int(W) if W else None
         for name, (_, build) in work.items():
             m, keep = build()
             st = bench.step_fn(arrays_to_plan(m), ex, [m], keep)
             st()  # lowering + JIT compile with this U
             steps[(ui, name)] = st
     L.cubed_stream_force_unroll(0)
+    Lw.FORCE_STREAM_W = None
     for r in range(rounds):
         for ui, U in enumerate(us):
             line = []
@@ -70,7 +79,7 @@ def main():
                     st()
                 d = bench.timed(st, 10, 1)
                 line.append(f"{name} {d * 1e3:.4f} ms ({nbytes / d / 8e12:.4f})")
-            print(f"round {r} plan {ui} U {U or 'default'}: " + "  ".join(line), flush=True)
+            print(f"round {r} plan {ui} U {U if U != '0' else 'default'}: " + "  ".join(line), flush=True)
 
 
 if __name__ == "__main__":
