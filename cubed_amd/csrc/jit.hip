@@ -140,11 +140,15 @@ std::string jit_source(const cubed_program_t& P, const std::string& name) {
                   : P.vtype == CUBED_V_F64 && P.nleaves >= 3 ? 4
                                                              : stream_unroll(P.vtype == CUBED_V_F32 ? 4 : 8, P.nleaves);
     // the unsplit kernel (a grid that fills the chip without splitting the
-    // rows): 2 rows for f32 two-leaf programs -- quad-means 1.184-1.192 ms
-    // against 1.212-1.215 with 4, three plans each in one process
-    // (profiles/r06_stream_unroll.log); the split planner's in-flight
-    // estimate (stream_unroll) does not concern unsplit launches
-    const int Um = g_stream_force_unroll > 0 ? U : P.vtype == CUBED_V_F32 && P.nleaves == 2 ? 2 : U;
+    // rows), f32 two-leaf programs: 1 row per lane with W = 4 kept groups
+    // (the host's choice for them), 2 rows with W = 2 -- quad-means 1.149-
+    // 1.153 ms (W 4, U 1), 1.173-1.179 (W 2, U 2), 1.212-1.215 (W 2, U 4),
+    // plans of their own in one process (profiles/r06_stream_unroll.log);
+    // the split planner's in-flight estimate (stream_unroll) does not
+    // concern unsplit launches
+    const int Um = g_stream_force_unroll > 0                      ? U
+                   : P.vtype == CUBED_V_F32 && P.nleaves == 2 ? (stream_groups(P) == 4 ? 1 : 2)
+                                                                  : U;
     snprintf(buf, sizeof(buf),
              "extern \"C\" __global__ __launch_bounds__(256) void %s(const cubed_task_t* __restrict__ tasks, "
              "int64_t ntasks, int64_t bpt, int32_t nsplit, cubed::Acc* __restrict__ ws, int64_t max_kept) {\n"

@@ -1784,14 +1784,21 @@ def _stream_groups_mode(P, ntasks: int, max_kept: int) -> int:
     if FORCE_STREAM_W is not None:  # tests: every W on one program
         w = FORCE_STREAM_W
     else:
-        w = 256 // (_stream_unroll(isz, nl) * nl * 4 * isz)
-        w = 4 if w >= 4 else 2 if w >= 2 else 1
-        slots = -(-max_kept // (256 * w)) * 64
-        # the W-wide grid must hold >= 96 KiB of loads in flight per CU
-        # unsplit (fused.hip plan_launch splits below that)
-        inflight = 256 * _stream_unroll(isz, nl) * nl * w * 4 * isz
-        if w > 1 and (ntasks * -(-slots // 256) * inflight < 256 * 96 * 1024 or max_kept < 8 * 1024 * w):
-            w = 1
+        w0 = 256 // (_stream_unroll(isz, nl) * nl * 4 * isz)
+        # f32 two-leaf programs (quad-means, var / std of a product): W = 4
+        # with ONE row per lane in flight (jit.hip) -- quad-means 1.149-1.153
+        # ms against 1.173-1.179 for W = 2 with 2 rows and 1.164-1.169 with 1
+        # (profiles/r06_stream_unroll.log); W = 2 where W = 4 does not fit
+        cands = [4, 2] if isz == 4 and nl == 2 else [4 if w0 >= 4 else 2 if w0 >= 2 else 1]
+        w = 1
+        for c in cands:
+            slots = -(-max_kept // (256 * c)) * 64
+            # the W-wide grid must hold >= 96 KiB of loads in flight per CU
+            # unsplit (fused.hip plan_launch splits below that)
+            inflight = 256 * _stream_unroll(isz, nl) * nl * c * 4 * isz
+            if c == 1 or (ntasks * -(-slots // 256) * inflight >= 256 * 96 * 1024 and max_kept >= 8 * 1024 * c):
+                w = c
+                break
     return MODE_STREAM_W4 if w == 4 else MODE_STREAM_W2 if w == 2 else 0
 
 

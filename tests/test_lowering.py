@@ -608,8 +608,11 @@ def test_stream_groups_per_thread_choice(monkeypatch):
     def bits(vtype, nleaves, ntasks, max_kept):
         return Lw._stream_groups_mode(SimpleNamespace(vtype=vtype, nleaves=nleaves), ntasks, max_kept)
 
-    # config 2 quad-means: 2 f32 leaves, 1 task of 720*1440 kept -> W = 2, 506 workgroups
-    assert bits(Lw.V_F32, 2, 1, 720 * 1440) == Lw.MODE_STREAM_W2
+    # config 2 quad-means: 2 f32 leaves, 1 task of 720*1440 kept -> W = 4 (254
+    # workgroups; the JIT kernel then keeps one row per lane in flight)
+    assert bits(Lw.V_F32, 2, 1, 720 * 1440) == Lw.MODE_STREAM_W4
+    # ... W = 1 where the wide grid would not fill the CUs unsplit
+    assert bits(Lw.V_F32, 2, 1, 400000) == 0
     # config 1: 1 f64 leaf, 20000 kept -> the W = 2 grid (10 workgroups) would split: W = 1
     assert bits(Lw.V_F64, 1, 1, 20000) == 0
     # the elided rechunk+mean: 2500 source-chunk pieces of 1000 kept -> W = 1
