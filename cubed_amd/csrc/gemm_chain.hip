@@ -107,7 +107,8 @@ __device__ __forceinline__ void round_wait(unsigned* ctr, int64_t b, int64_t R) 
   if (i >= R) {
     if (threadIdx.x == 0) {
       const unsigned need = (unsigned)((i / R) * R);
-      for (int it = 0; it < 20000; ++it) {
+      // ~1.5 us per poll: a few ms at most (a round's spread is tens of us)
+      for (int it = 0; it < 2000; ++it) {
         if (__hip_atomic_load(ctr + (b & 7) * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;
         __builtin_amdgcn_s_sleep(4);
       }
