@@ -1,7 +1,10 @@
-"""BASELINE configs 1, 4 and 5 at FULL size on the MI355X (``-m gpu``),
+"""BASELINE configs 1, 3, 4 and 5 at FULL size on the MI355X (``-m gpu``),
 checked through size-independent properties (the full oracle would take
 minutes on the host):
 
+* config 3: rechunk 50000^2 f32 rows -> columns on the reference's 2 GB
+  plan -- every target chunk bit-exact against the resident source, one
+  source chunk bit-exact against the oracle's Philox;
 * config 1: (a + 1) * 2 -> mean(axis=0), random((20000, 20000), (5000,
   5000)) f64 -- 64 sampled columns summed in f64 from the resident chunks
   (rtol 1e-12) and the grand mean of U[0,1) data ~ 3;
@@ -53,6 +56,40 @@ def _free():
 
     gc.collect()
     torch.cuda.empty_cache()
+
+
+def test_rechunk_full_size(ex):
+    """config 3: rechunk 50000^2 f32 rows -> columns with the reference's own
+    2 GB plan (two rechunk ops, composed into one copy): EVERY target chunk
+    bit-exact against the resident source chunks, and one source row chunk
+    bit-exact against the oracle's Philox (random.py:31-36), so the whole
+    chain is pinned at full size."""
+    import torch
+
+    from oracle import cubed_ref as R
+
+    N = 50000
+    spec = cubed.Spec(allowed_mem="2GB", executor=ex)
+    random.seed(2000)
+    x = xp.astype(crandom.random((N, N), chunks=(1000, N), spec=spec), xp.float32)
+    arrays_to_plan(x).execute(executor=ex, array_names=[x.name])
+    y = x.rechunk((N, 1000))
+    plan = arrays_to_plan(y)
+    ops = [d for _, d in plan._finalize_dag().nodes(data=True) if d.get("op_name") == "rechunk"]
+    assert len(ops) == 2  # the reference's read / write stages at 2 GB
+    plan.execute(executor=ex, resume=True, array_names=[y.name])
+    X, Y = x.zarray, y.zarray
+    assert Y.numblocks == (1, 50)
+    for j in range(50):
+        got = _chunk(Y, (0, j)).view(torch.int32)
+        for i in range(50):
+            src = _chunk(X, (i, 0))[:, j * 1000:(j + 1) * 1000].view(torch.int32)
+            assert torch.equal(got[i * 1000:(i + 1) * 1000], src), (i, j)
+    b = 17  # a source row chunk against the oracle (block offset = its index)
+    exp = R.random_block(R.root_seed_after(2000), b, (1000, N)).astype(np.float32)
+    assert np.array_equal(_chunk(X, (b, 0)).cpu().numpy().view(np.int32), exp.view(np.int32))
+    del x, y, plan, X, Y
+    _free()
 
 
 def test_config1_full_size(ex):
