@@ -52,7 +52,8 @@ constexpr int E8_ROUNDS = 512;  // VAR bit: round_wait / round_done around the K
 // no fragment reads in the K loop.  64 = the round-5 tile order (xcd_remap:
 // each XCD a contiguous range of the grouped order) instead of xcd_lockstep;
 // 128 = xcd_lockstep without the round-robin tail; E8_ROUNDS (512, the
-// 1-GPU library form) = round_wait / round_done around the K loop: 84.3-84.5
+// 1-GPU library form) = round_wait / round_done around the K loop (probe:
+// + 1024 / 2048 = a round may start with 4 / 8 of the last one unfinished): 84.3-84.5
 // ms against 85.0-85.2 (profiles/r06_gemm_round_sync.log).  (A 4 x 2 arrangement of
 // the XCDs, 16 A + 16 B^T panels per round, ran 88.5-88.8 ms against 87.7-88.1:
 // commit "Probe: 4 x 2 XCD tile arrangement", profiles/r06_gemm_tile_order.log.)
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_bf16_8p(const cubed_gemm_chain_
     if constexpr ((VAR & E8_ROUNDS) != 0) round_done(rctr, blockIdx.x);
     return;
   }
-  if constexpr ((VAR & E8_ROUNDS) != 0) round_wait(rctr, blockIdx.x, 32);
+  if constexpr ((VAR & E8_ROUNDS) != 0) round_wait(rctr, blockIdx.x, 32, (VAR & 1024) ? 4 : (VAR & 2048) ? 8 : 0);
   const int ktl = (int)pp.KTL, nph = 4 * ktl;
   // the last K tile holds <= 32 live k: its second 32-k half is not
   // multiplied (w4p's K loop stops at ceil(K / 32) steps too)

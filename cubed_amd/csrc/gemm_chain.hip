@@ -102,11 +102,11 @@ __device__ __forceinline__ int64_t xcd_lockstep(int64_t b, int64_t nblk, int64_t
 // tiles start their K walks together and share panel lines in L2; a timeout
 // only costs the alignment.  ctr: one uint32 per XCD, 128 B apart, zeroed
 // before the launch.
-__device__ __forceinline__ void round_wait(unsigned* ctr, int64_t b, int64_t R) {
+__device__ __forceinline__ void round_wait(unsigned* ctr, int64_t b, int64_t R, int64_t slack = 0) {
   const int64_t i = b >> 3;
   if (i >= R) {
     if (threadIdx.x == 0) {
-      const unsigned need = (unsigned)((i / R) * R);
+      const unsigned need = (unsigned)((i / R) * R - slack);
       // ~1.5 us per poll: a few ms at most (a round's spread is tens of us)
       for (int it = 0; it < 2000; ++it) {
         if (__hip_atomic_load(ctr + (b & 7) * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need) break;

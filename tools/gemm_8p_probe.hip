@@ -333,6 +333,17 @@ int main(int argc, char** argv) {
     run("8p  (library)", e8, 512, false, 16, false);
     return 0;
   }
+  if (arms == 10) {  // round alignment with slack (a round starts with 4 / 8 of the last unfinished)
+    sync = true;
+    ARM("8p rounds aligned", 512, 4);
+    ARM("8p rounds aligned, slack 4", 512 | 1024, 4);
+    ARM("8p rounds aligned, slack 8", 512 | 2048, 4);
+    ARM("8p rounds aligned", 512, 4);
+    ARM("8p rounds aligned, slack 4", 512 | 1024, 4);
+    ARM("8p rounds aligned, slack 8", 512 | 2048, 4);
+    sync = false;
+    return 0;
+  }
   if (arms == 5) {  // tile orders (the library form: xcd_lockstep, GM 4)
     ARM("8p contiguous XCD ranges GM 4 (round 5 order)", 64, 4);
     ARM("8p lockstep, contiguous tail", 128, 4);
